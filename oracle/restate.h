@@ -1,0 +1,44 @@
+// oracle/restate.h — TEST INFRASTRUCTURE ONLY.  C API of the CPU restatement (oracle/restate.cpp), loaded by
+// tests/ and by bench.py's cpu_baseline leg through ctypes.  Never linked into the product.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+// RNG modes.
+//   ORC_MT  : one global std::mt19937 (default seed 5489) shared by scene build and render, libstdc++
+//             generate_canonical restated, g++ argument-evaluation order made explicit
+//             (/root/reference/src/utils/tracer_utils.h:27-41).  Single-threaded.  Bit-exact vs oracle/_ref.
+//   ORC_PCG : scene built with mt19937 (identical geometry); render draws come from per-(pixel, sample)
+//             PCG32 streams, the product's RNG contract; iterative integrator.  Multi-threaded.
+enum { ORC_MT = 0, ORC_PCG = 1 };
+
+// Directory holding assets produced from the reference inputs (cow/dino triangle lists, decoded textures).
+void orc_set_asset_dir(const char* dir);
+
+// First n values of random_double() from a fresh generator.
+int orc_kat(int n, double* out);
+
+// The k random_double() values that follow the scene build (pins RNG consumption of the scene build).
+int orc_probe(const char* scene, int k, double* out);
+
+// Canonical JSON dump of the restated scene graph (same schema as `ref_harness dump`).  Returns the
+// required size (including NUL); writes at most cap bytes.
+size_t orc_dump(const char* scene, char* buf, size_t cap);
+
+// Render rows [row0, row0+nrows) of a WxH image.  rgb_out: nrows*W*3 u8 (may be NULL);
+// acc_out: nrows*W*3 f64 per-pixel radiance sums (may be NULL).  segments_out: world.hit calls.
+// threads <= 0 -> hardware_concurrency.  ORC_MT ignores threads and requires row0 == 0, nrows == H.
+// Returns 0 on success, <0 on error (orc_last_error()).
+int orc_render(const char* scene, int W, int H, int spp, int max_depth, int mode, uint64_t seed,
+               int row0, int nrows, int threads, uint8_t* rgb_out, double* acc_out,
+               long long* segments_out, double* ms_out);
+
+const char* orc_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif

@@ -1,0 +1,83 @@
+"""Regenerate the golden fixtures from the reference itself (oracle/_ref/ref_harness).
+
+Run in the build container only (needs /root/reference and `make -C oracle ref`):
+
+    python tests/golden/make_golden.py
+
+Everything written here is DATA: inputs and outputs of the unmodified reference program
+(/root/reference/src compiled by oracle/Makefile, driven by oracle/ref_harness.cpp).  The
+fixtures pin:
+  * kat.json           first 32 random_double() of the reference's global mt19937 (tracer_utils.h:27-31)
+  * scenes.json        per scene: the 8 random_double() following the scene build (RNG consumption of the
+                       scene build incl. BVH-build draws) and the sha256 of the canonical scene dump
+  * render_<scene>.npz reference renders (engine_mode::single semantics): RGB8, f64 per-pixel sums and the
+                       exact segment count (world.hit calls)
+Assets (assets/*.tris, assets/earthmap.rgb) are the reference's post-triangulation meshes and stb-decoded
+texture bytes, written by the same harness.
+"""
+import hashlib
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+HARNESS = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+REF = "/root/reference"
+
+SCENES = ["c1", "1", "2", "3", "4", "5", "6", "7", "8", "cow", "dino"]
+SMALL = (64, 36, 4)          # every scene, RGB + f64 sums + segments
+CONFIG1 = ("c1", 400, 225, 64)  # BASELINE configs[0]: the CPU reference path at full size
+
+
+def run(*args):
+    return subprocess.run([HARNESS, *map(str, args)], check=True, capture_output=True, text=True).stdout
+
+
+def render(scene, W, H, spp, tmp="/tmp/golden_ref"):
+    info = json.loads(run("render", scene, W, H, spp, tmp).strip().splitlines()[-1])
+    rgb = np.fromfile(tmp + ".rgb", np.uint8).reshape(H, W, 3)
+    acc = np.fromfile(tmp + ".acc", np.float64).reshape(H, W, 3)
+    return rgb, acc, info
+
+
+def main():
+    if not os.path.exists(HARNESS):
+        sys.exit("build the reference harness first: make -C oracle ref")
+    assets = os.path.join(ROOT, "assets")
+    os.makedirs(assets, exist_ok=True)
+    run("mesh", "cow", os.path.join(assets, "cow.tris"))
+    run("mesh", "dino", os.path.join(assets, "dino.tris"))
+    run("texture", f"{REF}/textures/earthmap.jpg", os.path.join(assets, "earthmap.rgb"))
+
+    kat = [float(x) for x in run("kat", 32).split()]
+    with open(os.path.join(HERE, "kat.json"), "w") as f:
+        json.dump({"seed": 5489, "random_double": kat}, f, indent=1)
+
+    scenes = {}
+    for sc in SCENES:
+        # the harness may log texture loads on stdout first: the values are the last 8 lines
+        probe = [float(x) for x in run("probe", sc, 8).strip().splitlines()[-8:]]
+        run("dump", sc, "/tmp/golden_dump.json")
+        dump = open("/tmp/golden_dump.json", "rb").read()
+        scenes[sc] = {"probe": probe, "dump_sha256": hashlib.sha256(dump).hexdigest(), "dump_len": len(dump)}
+        W, H, spp = SMALL
+        rgb, acc, info = render(sc, W, H, spp)
+        np.savez_compressed(os.path.join(HERE, f"render_{sc}_{W}x{H}x{spp}.npz"), rgb=rgb, acc=acc,
+                            segments=np.int64(info["segments"]), W=W, H=H, spp=spp)
+        print(sc, info)
+    with open(os.path.join(HERE, "scenes.json"), "w") as f:
+        json.dump(scenes, f, indent=1)
+
+    sc, W, H, spp = CONFIG1
+    rgb, acc, info = render(sc, W, H, spp)
+    np.savez_compressed(os.path.join(HERE, f"render_{sc}_{W}x{H}x{spp}.npz"), rgb=rgb,
+                        acc=acc.astype(np.float64), segments=np.int64(info["segments"]), W=W, H=H, spp=spp)
+    print(sc, info)
+
+
+if __name__ == "__main__":
+    main()
