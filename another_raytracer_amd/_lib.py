@@ -1,0 +1,124 @@
+"""ctypes binding of libart.so (include/art.h).
+
+The HIP path is the only compute path: if libart.so is missing this module raises ImportError at import time
+instead of falling back to anything (there is no CPU fallback in the product).
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libart.so")
+
+RT_OK = 0
+RT_FP32, RT_FP64 = 0, 1
+RT_OUT_DEVICE, RT_PROFILE = 1, 2
+ERRORS = {-1: "RT_E_INVALID", -2: "RT_E_SCENE", -3: "RT_E_DEVICE", -4: "RT_E_INTERNAL"}
+
+
+class rt_camera(ctypes.Structure):
+    _fields_ = [("lookfrom", ctypes.c_double * 3), ("lookat", ctypes.c_double * 3), ("vup", ctypes.c_double * 3),
+                ("vfov", ctypes.c_double), ("aspect", ctypes.c_double), ("aperture", ctypes.c_double),
+                ("focus_dist", ctypes.c_double), ("time0", ctypes.c_double), ("time1", ctypes.c_double)]
+
+
+class rt_params(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32), ("spp", ctypes.c_int32),
+                ("max_depth", ctypes.c_int32), ("seed", ctypes.c_uint64), ("fp_mode", ctypes.c_int32),
+                ("band_rows", ctypes.c_int32), ("band_count", ctypes.c_int32), ("band_index", ctypes.c_int32),
+                ("samples_per_pass", ctypes.c_int32), ("flags", ctypes.c_int32), ("stream", ctypes.c_void_p),
+                ("background", ctypes.c_double * 3)]
+
+
+class rt_stats(ctypes.Structure):
+    _fields_ = [("segments", ctypes.c_uint64), ("primary", ctypes.c_uint64), ("ms", ctypes.c_double),
+                ("extend_ms", ctypes.c_double), ("shade_ms", ctypes.c_double),
+                ("extend_launches", ctypes.c_uint64), ("shade_launches", ctypes.c_uint64),
+                ("passes", ctypes.c_int32), ("samples_per_pass", ctypes.c_int32), ("local_rows", ctypes.c_int32),
+                ("pad", ctypes.c_int32)]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_ if f != "pad"}
+
+
+class rt_scene_info(ctypes.Structure):
+    _fields_ = [("lookfrom", ctypes.c_double * 3), ("lookat", ctypes.c_double * 3), ("vfov", ctypes.c_double),
+                ("aperture", ctypes.c_double), ("background", ctypes.c_double * 3),
+                ("spheres", ctypes.c_int64), ("triangles", ctypes.c_int64), ("rects", ctypes.c_int64),
+                ("boxes", ctypes.c_int64), ("bvh_nodes", ctypes.c_int64), ("objects", ctypes.c_int64),
+                ("materials", ctypes.c_int64), ("textures", ctypes.c_int64), ("has_media", ctypes.c_int32),
+                ("max_bvh_depth", ctypes.c_int32), ("device_bytes_f32", ctypes.c_uint64),
+                ("device_bytes_f64", ctypes.c_uint64)]
+
+
+# Every symbol include/art.h declares, with its ctypes signature (tests/test_abi.py checks the header agrees).
+_P, _I, _D, _S = ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_size_t
+_DP = ctypes.POINTER(ctypes.c_double)
+_IP = ctypes.POINTER(ctypes.c_int)
+SIGNATURES = {
+    "rt_abi_version": (_I, []),
+    "rt_last_error": (ctypes.c_char_p, []),
+    "rt_device_count": (_I, []),
+    "rt_scene_build": (_I, [ctypes.c_char_p, ctypes.c_char_p, _I, ctypes.POINTER(_P)]),
+    "rt_scene_info_get": (_I, [_P, ctypes.POINTER(rt_scene_info)]),
+    "rt_scene_dump": (_S, [_P, ctypes.c_char_p, _S]),
+    "rt_scene_destroy": (None, [_P]),
+    "rt_render": (_I, [_P, ctypes.POINTER(rt_camera), ctypes.POINTER(rt_params), _P, _P, ctypes.POINTER(rt_stats)]),
+    "rt_local_rows": (_I, [ctypes.POINTER(rt_params), ctypes.POINTER(ctypes.c_int32)]),
+    "rt_graph_new": (_P, []),
+    "rt_graph_free": (None, [_P]),
+    "rt_graph_random_double": (_I, [_P, _DP]),
+    "rt_tex_solid": (_I, [_P, _D, _D, _D]),
+    "rt_tex_checker": (_I, [_P, _I, _I]),
+    "rt_tex_noise": (_I, [_P, _D]),
+    "rt_tex_image": (_I, [_P, _I, _I, _I, _P]),
+    "rt_mat_lambertian": (_I, [_P, _I]),
+    "rt_mat_metal": (_I, [_P, _D, _D, _D, _D]),
+    "rt_mat_dielectric": (_I, [_P, _D]),
+    "rt_mat_diffuse_light": (_I, [_P, _I]),
+    "rt_obj_sphere": (_I, [_P, _DP, _D, _I]),
+    "rt_obj_moving_sphere": (_I, [_P, _DP, _DP, _D, _D, _D, _I]),
+    "rt_obj_triangle": (_I, [_P, _DP, _DP, _DP, _I]),
+    "rt_obj_rect": (_I, [_P, _I, _D, _D, _D, _D, _D, _I]),
+    "rt_obj_box": (_I, [_P, _DP, _DP, _I]),
+    "rt_obj_list": (_I, [_P, _I, _IP]),
+    "rt_obj_bvh": (_I, [_P, _I, _IP]),
+    "rt_obj_translate": (_I, [_P, _I, _DP]),
+    "rt_obj_rotate_y": (_I, [_P, _I, _D]),
+    "rt_obj_constant_medium": (_I, [_P, _I, _D, _I]),
+    "rt_graph_add_world": (_I, [_P, _I]),
+    "rt_graph_clear_world": (_I, [_P]),
+    "rt_graph_set_view": (_I, [_P, _DP, _DP, _D, _D, _DP]),
+    "rt_graph_compile": (_I, [_P, _I, ctypes.POINTER(_P)]),
+}
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                          "(or `make -C another_raytracer_amd/csrc`); there is no CPU fallback")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+class RTError(RuntimeError):
+    def __init__(self, code, where):
+        msg = lib.rt_last_error().decode(errors="replace")
+        super().__init__(f"{where} failed ({ERRORS.get(code, code)}): {msg}")
+        self.code = code
+
+
+def check(code, where):
+    if code < 0:
+        raise RTError(code, where)
+    return code
+
+
+def dvec(v):
+    return (ctypes.c_double * 3)(*[float(x) for x in v])

@@ -1,0 +1,302 @@
+// abi.cpp — the extern "C" boundary (include/art.h).  No exception crosses it.
+#include <cstring>
+#include <exception>
+#include <stdexcept>
+#include <memory>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "art.h"
+#include "renderer.h"
+#include "scene.h"
+
+namespace art {
+int device_count();  // kernels.hip
+}
+
+struct rt_scene {
+    art::SceneGraph graph;
+    art::FlatScene flat;
+    int device = 0;
+    std::unique_ptr<art::Renderer> renderer;  // created on first render (scene build/dump works without a GPU)
+};
+struct rt_graph {
+    art::SceneGraph g;
+};
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+template <class F>
+int guard(int code_on_exception, F&& f) {
+    try {
+        return f();
+    } catch (const std::bad_alloc&) {
+        return fail(RT_E_INTERNAL, "out of memory");
+    } catch (const std::exception& e) {
+        return fail(code_on_exception, e.what());
+    } catch (...) {
+        return fail(RT_E_INTERNAL, "unknown error");
+    }
+}
+art::Vec3 v3(const double* p) { return art::Vec3(p[0], p[1], p[2]); }
+bool valid_params(const rt_params* p, std::string& why) {
+    if (!p) { why = "params is NULL"; return false; }
+    if (p->width < 2 || p->height < 2) { why = "width and height must be >= 2 (u = (i + r)/(W-1), engine.h:62-63)"; return false; }
+    if (p->spp < 1) { why = "spp must be >= 1"; return false; }
+    if (p->max_depth < 0) { why = "max_depth must be >= 0"; return false; }
+    if (p->band_rows < 1 || p->band_count < 1 || p->band_index < 0 || p->band_index >= p->band_count) {
+        why = "band partition must satisfy band_rows >= 1, band_count >= 1, 0 <= band_index < band_count";
+        return false;
+    }
+    if (p->fp_mode != RT_FP32 && p->fp_mode != RT_FP64) { why = "fp_mode must be RT_FP32 or RT_FP64"; return false; }
+    if (static_cast<int64_t>(p->width) * p->height > (int64_t(1) << 31)) { why = "image too large"; return false; }
+    return true;
+}
+int scene_from_graph(art::SceneGraph graph, int device, rt_scene** out) {
+    auto s = std::make_unique<rt_scene>();
+    s->graph = std::move(graph);
+    s->flat = art::compile_scene(s->graph);
+    s->device = device;
+    *out = s.release();
+    return RT_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int rt_abi_version(void) { return RT_ABI_VERSION; }
+const char* rt_last_error(void) { return g_err.c_str(); }
+int rt_device_count(void) {
+    return guard(RT_E_DEVICE, [] { return art::device_count(); });
+}
+
+int rt_scene_build(const char* name, const char* asset_dir, int device, rt_scene** out) {
+    if (!name || !out) return fail(RT_E_INVALID, "name and out must be non-NULL");
+    *out = nullptr;
+    return guard(RT_E_SCENE, [&] {
+        art::SceneGraph g;
+        art::build_builtin_scene(g, name, asset_dir ? asset_dir : "assets");
+        return scene_from_graph(std::move(g), device, out);
+    });
+}
+
+int rt_scene_info_get(const rt_scene* s, rt_scene_info* info) {
+    if (!s || !info) return fail(RT_E_INVALID, "scene and info must be non-NULL");
+    std::memset(info, 0, sizeof *info);
+    for (int a = 0; a < 3; ++a) {
+        info->lookfrom[a] = s->graph.lookfrom[a];
+        info->lookat[a] = s->graph.lookat[a];
+        info->background[a] = s->graph.background[a];
+    }
+    info->vfov = s->graph.vfov;
+    info->aperture = s->graph.aperture;
+    info->spheres = static_cast<int64_t>(s->flat.spheres.size());
+    info->triangles = static_cast<int64_t>(s->flat.tris.size());
+    info->rects = static_cast<int64_t>(s->flat.rects.size());
+    info->boxes = static_cast<int64_t>(s->flat.boxes.size());
+    info->bvh_nodes = static_cast<int64_t>(s->flat.nodes.size());
+    info->objects = static_cast<int64_t>(s->flat.world.size());
+    info->materials = static_cast<int64_t>(s->flat.mats.size());
+    info->textures = static_cast<int64_t>(s->flat.texs.size());
+    info->has_media = s->flat.has_media ? 1 : 0;
+    info->max_bvh_depth = s->flat.max_bvh_depth;
+    if (s->renderer) {
+        info->device_bytes_f32 = s->renderer->scene_bytes(RT_FP32);
+        info->device_bytes_f64 = s->renderer->scene_bytes(RT_FP64);
+    }
+    return RT_OK;
+}
+
+size_t rt_scene_dump(const rt_scene* s, char* buf, size_t cap) {
+    if (!s) {
+        fail(RT_E_INVALID, "scene is NULL");
+        return 0;
+    }
+    try {
+        std::string d = art::dump_scene(s->graph);
+        if (buf && cap) {
+            size_t n = std::min(cap - 1, d.size());
+            std::memcpy(buf, d.data(), n);
+            buf[n] = 0;
+        }
+        return d.size() + 1;
+    } catch (const std::exception& e) {
+        fail(RT_E_INTERNAL, e.what());
+        return 0;
+    }
+}
+
+void rt_scene_destroy(rt_scene* s) {
+    try {
+        delete s;
+    } catch (...) {
+    }
+}
+
+int rt_local_rows(const rt_params* p, int32_t* rows_out) {
+    std::string why;
+    if (!p || p->height < 1 || p->band_rows < 1 || p->band_count < 1 || p->band_index < 0 || p->band_index >= p->band_count)
+        return fail(RT_E_INVALID, "invalid band partition");
+    int n = 0;
+    for (int ly = 0;; ++ly) {
+        int gy = (ly / p->band_rows) * (p->band_rows * p->band_count) + p->band_index * p->band_rows + (ly % p->band_rows);
+        if (gy >= p->height) break;
+        if (rows_out) rows_out[n] = gy;
+        ++n;
+    }
+    return n;
+}
+
+int rt_render(rt_scene* s, const rt_camera* cam, const rt_params* p, uint8_t* out_rgb8, double* out_accum, rt_stats* stats) {
+    std::string why;
+    if (!s || !cam) return fail(RT_E_INVALID, "scene and camera must be non-NULL");
+    if (!valid_params(p, why)) return fail(RT_E_INVALID, why);
+    return guard(RT_E_DEVICE, [&] {
+        if (!s->renderer) s->renderer = std::make_unique<art::Renderer>(s->flat, s->device);
+        art::CameraRec<double> c = art::make_camera(cam->lookfrom, cam->lookat, cam->vup, cam->vfov, cam->aspect, cam->aperture,
+                                                    cam->focus_dist, cam->time0, cam->time1);
+        art::RenderParams rp;
+        rp.width = p->width;
+        rp.height = p->height;
+        rp.spp = p->spp;
+        rp.max_depth = p->max_depth;
+        rp.seed = p->seed;
+        rp.fp_mode = p->fp_mode;
+        rp.band_rows = p->band_rows;
+        rp.band_count = p->band_count;
+        rp.band_index = p->band_index;
+        rp.samples_per_pass = p->samples_per_pass;
+        rp.flags = p->flags;
+        rp.stream = p->stream;
+        for (int c = 0; c < 3; ++c) rp.background[c] = p->background[c];
+        art::RenderStats st;
+        s->renderer->render(c, rp, out_rgb8, out_accum, st);
+        if (stats) {
+            std::memset(stats, 0, sizeof *stats);
+            stats->segments = st.segments;
+            stats->primary = st.primary;
+            stats->ms = st.ms;
+            stats->extend_ms = st.extend_ms;
+            stats->shade_ms = st.shade_ms;
+            stats->extend_launches = st.extend_launches;
+            stats->shade_launches = st.shade_launches;
+            stats->passes = st.passes;
+            stats->samples_per_pass = st.samples_per_pass;
+            stats->local_rows = st.local_rows;
+        }
+        return RT_OK;
+    });
+}
+
+// ---------------------------------------------------------------------------------------------- graph builder
+rt_graph* rt_graph_new(void) {
+    try {
+        return new rt_graph();
+    } catch (...) {
+        fail(RT_E_INTERNAL, "out of memory");
+        return nullptr;
+    }
+}
+void rt_graph_free(rt_graph* g) { delete g; }
+
+#define GRAPH_CALL(expr)                                                \
+    do {                                                                \
+        if (!g) return fail(RT_E_INVALID, "graph is NULL");             \
+        return guard(RT_E_INVALID, [&] { return static_cast<int>(expr); }); \
+    } while (0)
+
+namespace {
+void check_tex(const rt_graph* g, int t) {
+    if (t < 0 || t >= static_cast<int>(g->g.textures.size())) throw std::runtime_error("bad texture id");
+}
+void check_mat(const rt_graph* g, int m) {
+    if (m < 0 || m >= static_cast<int>(g->g.materials.size())) throw std::runtime_error("bad material id");
+}
+void check_obj(const rt_graph* g, int o) {
+    if (o < 0 || o >= static_cast<int>(g->g.nodes.size())) throw std::runtime_error("bad object id");
+}
+std::vector<int> items_of(const rt_graph* g, int n, const int* items) {
+    if (n < 0 || (n > 0 && !items)) throw std::runtime_error("bad item list");
+    std::vector<int> v(items, items + n);
+    for (int o : v) check_obj(g, o);
+    return v;
+}
+}  // namespace
+
+int rt_graph_random_double(rt_graph* g, double* out) {
+    if (!g || !out) return fail(RT_E_INVALID, "graph/out is NULL");
+    *out = g->g.rng.d();
+    return RT_OK;
+}
+int rt_tex_solid(rt_graph* g, double r, double gr, double b) { GRAPH_CALL(g->g.solid(art::Vec3(r, gr, b))); }
+int rt_tex_checker(rt_graph* g, int even, int odd) {
+    GRAPH_CALL((check_tex(g, even), check_tex(g, odd), g->g.checker(even, odd)));
+}
+int rt_tex_noise(rt_graph* g, double scale) { GRAPH_CALL(g->g.noise(scale)); }
+int rt_tex_image(rt_graph* g, int w, int h, int bpp, const uint8_t* texels) {
+    GRAPH_CALL(([&] {
+        if (w <= 0 || h <= 0 || bpp < 3 || !texels) throw std::runtime_error("bad image");
+        art::Image im;
+        im.w = w;
+        im.h = h;
+        im.bpp = bpp;
+        im.data.assign(texels, texels + static_cast<size_t>(w) * h * bpp);
+        return g->g.image(std::move(im));
+    }()));
+}
+int rt_mat_lambertian(rt_graph* g, int tex) { GRAPH_CALL((check_tex(g, tex), g->g.lambertian(tex))); }
+int rt_mat_metal(rt_graph* g, double r, double gr, double b, double fuzz) { GRAPH_CALL(g->g.metal(art::Vec3(r, gr, b), fuzz)); }
+int rt_mat_dielectric(rt_graph* g, double ir) { GRAPH_CALL(g->g.dielectric(ir)); }
+int rt_mat_diffuse_light(rt_graph* g, int tex) { GRAPH_CALL((check_tex(g, tex), g->g.diffuse_light(tex))); }
+int rt_obj_sphere(rt_graph* g, const double c[3], double r, int mat) { GRAPH_CALL((check_mat(g, mat), g->g.sphere(v3(c), r, mat))); }
+int rt_obj_moving_sphere(rt_graph* g, const double c0[3], const double c1[3], double t0, double t1, double r, int mat) {
+    GRAPH_CALL((check_mat(g, mat), g->g.moving_sphere(v3(c0), v3(c1), t0, t1, r, mat)));
+}
+int rt_obj_triangle(rt_graph* g, const double p1[3], const double p2[3], const double p3[3], int mat) {
+    GRAPH_CALL((check_mat(g, mat), g->g.triangle(v3(p1), v3(p2), v3(p3), mat)));
+}
+int rt_obj_rect(rt_graph* g, int axis, double a0, double a1, double b0, double b1, double k, int mat) {
+    GRAPH_CALL(([&] {
+        if (axis < 0 || axis > 2) throw std::runtime_error("rect axis must be 0 (xy), 1 (xz) or 2 (yz)");
+        check_mat(g, mat);
+        return g->g.rect(axis, a0, a1, b0, b1, k, mat);
+    }()));
+}
+int rt_obj_box(rt_graph* g, const double p0[3], const double p1[3], int mat) { GRAPH_CALL((check_mat(g, mat), g->g.box(v3(p0), v3(p1), mat))); }
+int rt_obj_list(rt_graph* g, int n, const int* items) { GRAPH_CALL(g->g.list(items_of(g, n, items))); }
+int rt_obj_bvh(rt_graph* g, int n, const int* items) { GRAPH_CALL(g->g.bvh(items_of(g, n, items))); }
+int rt_obj_translate(rt_graph* g, int child, const double offset[3]) { GRAPH_CALL((check_obj(g, child), g->g.translate(child, v3(offset)))); }
+int rt_obj_rotate_y(rt_graph* g, int child, double degrees) { GRAPH_CALL((check_obj(g, child), g->g.rotate_y(child, degrees))); }
+int rt_obj_constant_medium(rt_graph* g, int boundary, double density, int tex) {
+    GRAPH_CALL((check_obj(g, boundary), check_tex(g, tex), g->g.constant_medium(boundary, density, tex)));
+}
+int rt_graph_add_world(rt_graph* g, int obj) {
+    GRAPH_CALL((check_obj(g, obj), g->g.world.push_back(obj), static_cast<int>(g->g.world.size()) - 1));
+}
+int rt_graph_clear_world(rt_graph* g) {
+    if (!g) return fail(RT_E_INVALID, "graph is NULL");
+    g->g.world.clear();
+    return RT_OK;
+}
+int rt_graph_set_view(rt_graph* g, const double lookfrom[3], const double lookat[3], double vfov, double aperture, const double background[3]) {
+    if (!g || !lookfrom || !lookat || !background) return fail(RT_E_INVALID, "NULL argument");
+    g->g.lookfrom = v3(lookfrom);
+    g->g.lookat = v3(lookat);
+    g->g.vfov = vfov;
+    g->g.aperture = aperture;
+    g->g.background = v3(background);
+    return RT_OK;
+}
+int rt_graph_compile(rt_graph* g, int device, rt_scene** out) {
+    if (!g || !out) return fail(RT_E_INVALID, "graph and out must be non-NULL");
+    *out = nullptr;
+    return guard(RT_E_SCENE, [&] { return scene_from_graph(g->g, device, out); });
+}
+
+}  // extern "C"

@@ -1,0 +1,24 @@
+// bvh.h — binned-SAH BVH over primitive boxes, emitted as the flat 64-B two-child node array of layout.h.
+//
+// Replaces the reference's bvh_node (primitives/bvh.cpp:3-42: random split axis, median split, O(N^2) object
+// copies, 1-spans tested twice).  Closest-hit results do not depend on the tree, so the product builds the tree
+// that minimises expected traversal cost instead: 16-bin SAH on centroids, leaves of <= kMaxLeafPrims, depth
+// capped at kMaxBvhDepth (the LDS traversal stack), child boxes rounded outward to f32 and padded so that f32
+// traversal never rejects a box the f64 leaf test could hit.
+#pragma once
+#include <cstdint>
+#include <vector>
+
+#include "layout.h"
+#include "scene.h"
+
+namespace art {
+
+// Appends nodes/primrefs for one BVH and returns its root node index.  max_depth receives the tree depth.
+int32_t build_sah_bvh(const std::vector<AABBd>& boxes, const std::vector<uint32_t>& refs, std::vector<BvhNode>& nodes,
+                      std::vector<uint32_t>& primrefs, int& max_depth);
+
+// f32 box rounded outward + relative pad (the conservative box the traversal tests).
+void conservative_box(const AABBd& b, float lo[3], float hi[3]);
+
+}  // namespace art

@@ -1,0 +1,567 @@
+// device.h — device-side math, RNG, intersection and shading routines (templated on the real type R).
+//
+// Every routine restates the reference function it cites with the SAME operation order (v/t == (1/t)*v, dot summed
+// left to right, ...), so that the f64 instantiation reproduces the CPU restatement (oracle/restate.cpp, pcg mode)
+// to the last bit up to libm-vs-OCML transcendental ulps.  The f32 instantiation runs the identical code in float.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cstdint>
+
+#include "layout.h"
+
+namespace art {
+
+// ------------------------------------------------------------------------------------------------ vec3 (core/vec3.h)
+template <class R>
+struct V3 {
+    R x, y, z;
+};
+template <class R> __device__ __forceinline__ V3<R> mk(R a, R b, R c) { return V3<R>{a, b, c}; }
+template <class R> __device__ __forceinline__ V3<R> operator+(V3<R> u, V3<R> v) { return {u.x + v.x, u.y + v.y, u.z + v.z}; }
+template <class R> __device__ __forceinline__ V3<R> operator-(V3<R> u, V3<R> v) { return {u.x - v.x, u.y - v.y, u.z - v.z}; }
+template <class R> __device__ __forceinline__ V3<R> operator-(V3<R> u) { return {-u.x, -u.y, -u.z}; }
+template <class R> __device__ __forceinline__ V3<R> operator*(V3<R> u, V3<R> v) { return {u.x * v.x, u.y * v.y, u.z * v.z}; }
+template <class R> __device__ __forceinline__ V3<R> operator*(R t, V3<R> v) { return {t * v.x, t * v.y, t * v.z}; }
+template <class R> __device__ __forceinline__ R dot(V3<R> u, V3<R> v) { return u.x * v.x + u.y * v.y + u.z * v.z; }
+template <class R> __device__ __forceinline__ R len2(V3<R> v) { return v.x * v.x + v.y * v.y + v.z * v.z; }
+template <class R> __device__ __forceinline__ V3<R> cross(V3<R> u, V3<R> v) {
+    return {u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x};
+}
+template <class R> __device__ __forceinline__ V3<R> divs(V3<R> v, R t) { return (R(1) / t) * v; }  // vec3.h:97-99
+template <class R> __device__ __forceinline__ V3<R> unit(V3<R> v) { return divs(v, sqrt(len2(v))); }
+template <class R> __device__ __forceinline__ bool near_zero(V3<R> v) {  // vec3.h:49-53
+    const R s = R(1e-8);
+    return fabs(v.x) < s && fabs(v.y) < s && fabs(v.z) < s;
+}
+template <class R> __device__ __forceinline__ V3<R> reflect(V3<R> v, V3<R> n) { return v - (R(2) * dot(v, n)) * n; }
+template <class R> __device__ __forceinline__ V3<R> refract(V3<R> uv, V3<R> n, R eta) {  // vec3.h:149-154
+    R cos_theta = fmin(dot(-uv, n), R(1));
+    V3<R> perp = eta * (uv + cos_theta * n);
+    V3<R> par = (-sqrt(fabs(R(1) - len2(perp)))) * n;
+    return perp + par;
+}
+template <class R> __device__ __forceinline__ V3<R> ld3(const R* p) { return {p[0], p[1], p[2]}; }
+
+template <class R>
+struct Ray {
+    V3<R> o, d;
+    R tm;
+    __device__ __forceinline__ V3<R> at(R t) const { return o + t * d; }
+};
+
+// ------------------------------------------------------------------------------------------------ RNG contract
+// PCG32 (O'Neill), one 64-bit state per path, seeded from (seed, global pixel, sample) through splitmix64 so the
+// stream depends only on what is rendered, never on tiling or GPU count.  Uniforms carry 24 bits: exact in f32/f64.
+__host__ __device__ inline uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+__host__ __device__ inline uint64_t pcg_seed(uint64_t seed, uint32_t pixel, uint32_t sample) {
+    return splitmix64(((static_cast<uint64_t>(pixel) << 32) | sample) ^ splitmix64(seed));
+}
+template <class R>
+__device__ __forceinline__ R uniform(uint64_t& s) {
+    const uint64_t old = s;
+    s = old * 6364136223846793005ull + 1442695040888963407ull;
+    const uint32_t xs = static_cast<uint32_t>(((old >> 18u) ^ old) >> 27u);
+    const uint32_t rot = static_cast<uint32_t>(old >> 59u);
+    const uint32_t x = (xs >> rot) | (xs << ((32u - rot) & 31u));
+    return static_cast<R>(x >> 8) * static_cast<R>(1.0 / 16777216.0);
+}
+template <class R> __device__ __forceinline__ R uniform(uint64_t& s, R lo, R hi) { return lo + (hi - lo) * uniform<R>(s); }
+template <class R>
+__device__ __forceinline__ V3<R> in_unit_sphere(uint64_t& s) {  // vec3.h:117-123, draws x, y, z
+    for (;;) {
+        V3<R> p;
+        p.x = uniform<R>(s, R(-1), R(1));
+        p.y = uniform<R>(s, R(-1), R(1));
+        p.z = uniform<R>(s, R(-1), R(1));
+        if (len2(p) >= R(1)) continue;
+        return p;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------ device scene view
+template <class R>
+struct DevScene {
+    const SphereRec<R>* spheres;
+    const TriRec<R>* tris;
+    const RectRec<R>* rects;
+    const BoxRec<R>* boxes;
+    const uint32_t* primrefs;
+    const BvhNode* nodes;
+    const ObjRec<R>* objs;
+    const int32_t* world;
+    const MatRec<R>* mats;
+    const TexRec<R>* texs;
+    const PerlinRec<R>* perlins;
+    const ImageRec* images;
+    const uint8_t* texels;
+    int32_t nworld;
+    int32_t pad;
+    R bg[3];
+};
+
+constexpr uint32_t kMediumHit = 0xFFFFFFFFu;  // hit.prim value of a constant_medium scattering event
+
+// ------------------------------------------------------------------------------------------------ primitives
+// sphere.h:39-65 / moving_sphere.h:41-58 (root selection only; the surface is rebuilt in shade).
+template <class R>
+__device__ __forceinline__ bool hit_sphere(const SphereRec<R>& s, const Ray<R>& r, R tmin, R tmax, R& t) {
+    V3<R> center = ld3(s.c);
+    if (s.flags & SPH_MOVING) center = center + ((r.tm - s.t0) / s.dt) * ld3(s.d);
+    const V3<R> oc = r.o - center;
+    const R a = len2(r.d);
+    const R half_b = dot(oc, r.d);
+    const R c = len2(oc) - s.r * s.r;
+    const R disc = half_b * half_b - a * c;
+    if (disc < R(0)) return false;
+    const R sqrtd = sqrt(disc);
+    R root = (-half_b - sqrtd) / a;
+    if (root < tmin || tmax < root) {
+        root = (-half_b + sqrtd) / a;
+        if (root < tmin || tmax < root) return false;
+    }
+    t = root;
+    return true;
+}
+
+// triangle.h:22-88 (geometric test, unnormalised normal).
+template <class R>
+__device__ __forceinline__ bool hit_tri(const TriRec<R>& tr, const Ray<R>& r, R tmin, R tmax, R& t) {
+    const V3<R> p1 = ld3(tr.p), p2 = ld3(tr.p + 3), p3 = ld3(tr.p + 6);
+    const V3<R> N = cross(p2 - p1, p3 - p1);
+    const R ndd = dot(N, r.d);
+    if (fabs(ndd) < R(DBL_EPSILON)) return false;
+    const R dd = -dot(N, p1);
+    const R tt = -(dot(N, r.o) + dd) / ndd;
+    if (tt < tmin || tmax < tt) return false;
+    const V3<R> p = r.o + tt * r.d;
+    if (dot(N, cross(p2 - p1, p - p1)) < R(0)) return false;
+    if (dot(N, cross(p3 - p2, p - p2)) < R(0)) return false;
+    if (dot(N, cross(p1 - p3, p - p3)) < R(0)) return false;
+    t = tt;
+    return true;
+}
+
+template <class R> __device__ __forceinline__ R comp(V3<R> v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
+
+// aarect.cpp:3-55.  axis 0: xy (k on z), 1: xz (k on y), 2: yz (k on x).
+template <class R>
+__device__ __forceinline__ bool hit_rect(int axis, R a0, R a1, R b0, R b1, R k, const Ray<R>& r, R tmin, R tmax, R& t) {
+    const int ka = axis == 0 ? 2 : (axis == 1 ? 1 : 0);
+    const int ia = axis == 2 ? 1 : 0;
+    const int ib = axis == 0 ? 1 : 2;
+    const R tt = (k - comp(r.o, ka)) / comp(r.d, ka);
+    if (tt < tmin || tt > tmax) return false;
+    const R x = comp(r.o, ia) + tt * comp(r.d, ia);
+    const R y = comp(r.o, ib) + tt * comp(r.d, ib);
+    if (x < a0 || x > a1 || y < b0 || y > b1) return false;
+    t = tt;
+    return true;
+}
+
+// box.cpp:3-19: face f of a box, in the reference's side order.
+template <class R>
+__device__ __forceinline__ void box_face(const BoxRec<R>& b, int f, int& axis, R& a0, R& a1, R& b0, R& b1, R& k) {
+    const int pair = f >> 1;       // 0: xy, 1: xz, 2: yz
+    const bool hi = (f & 1) == 0;  // even faces sit on p1
+    axis = pair;
+    if (pair == 0) { a0 = b.mn[0]; a1 = b.mx[0]; b0 = b.mn[1]; b1 = b.mx[1]; k = hi ? b.mx[2] : b.mn[2]; }
+    else if (pair == 1) { a0 = b.mn[0]; a1 = b.mx[0]; b0 = b.mn[2]; b1 = b.mx[2]; k = hi ? b.mx[1] : b.mn[1]; }
+    else { a0 = b.mn[1]; a1 = b.mx[1]; b0 = b.mn[2]; b1 = b.mx[2]; k = hi ? b.mx[0] : b.mn[0]; }
+}
+template <class R>
+__device__ __forceinline__ bool hit_box(const BoxRec<R>& b, const Ray<R>& r, R tmin, R tmax, R& t, uint32_t& face) {
+    bool any = false;  // hittable_list semantics over the six sides: closest wins, a later equal t replaces
+    R closest = tmax;
+    for (int f = 0; f < 6; ++f) {
+        int axis;
+        R a0, a1, b0, b1, k, tt;
+        box_face(b, f, axis, a0, a1, b0, b1, k);
+        if (hit_rect(axis, a0, a1, b0, b1, k, r, tmin, closest, tt)) {
+            any = true;
+            closest = tt;
+            face = static_cast<uint32_t>(f);
+        }
+    }
+    t = closest;
+    return any;
+}
+
+template <class R>
+__device__ __forceinline__ bool hit_prim(const DevScene<R>& S, uint32_t ref, const Ray<R>& r, R tmin, R tmax, R& t, uint32_t& face) {
+    const uint32_t idx = primref_index(ref);
+    switch (primref_type(ref)) {
+        case PRIM_SPHERE: return hit_sphere(S.spheres[idx], r, tmin, tmax, t);
+        case PRIM_TRIANGLE: return hit_tri(S.tris[idx], r, tmin, tmax, t);
+        case PRIM_RECT: {
+            const RectRec<R>& q = S.rects[idx];
+            return hit_rect(static_cast<int>(q.axis), q.a0, q.a1, q.b0, q.b1, q.k, r, tmin, tmax, t);
+        }
+        default: return hit_box(S.boxes[idx], r, tmin, tmax, t, face);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------ BVH traversal
+// While-while traversal of the two-child f32 node array with a per-lane stack in LDS (stk[k * kBlock] is entry k of
+// this lane).  Box tests are f32 and conservative (boxes padded at build time, interval widened here); leaves run the
+// exact R tests and shrink tmax, so the closest hit equals the reference's bvh_node::hit (bvh.cpp:44-52) up to ties.
+constexpr int kBlock = 256;
+
+__device__ __forceinline__ float f_lo(double t) { return t == -__builtin_inf() ? -__builtin_inff() : static_cast<float>(t) * (1.0f - 2e-6f) - 1e-30f; }
+__device__ __forceinline__ float f_lo(float t) { return t * (1.0f - 2e-6f) - 1e-30f; }
+__device__ __forceinline__ float f_hi(double t) { return t == __builtin_inf() ? __builtin_inff() : static_cast<float>(t) * (1.0f + 2e-6f) + 1e-30f; }
+__device__ __forceinline__ float f_hi(float t) { return t * (1.0f + 2e-6f) + 1e-30f; }
+
+template <class R>
+__device__ __forceinline__ bool traverse(const DevScene<R>& S, int32_t root, const Ray<R>& r, R tmin, R tmax, int32_t* stk, R& t,
+                                         uint32_t& prim, uint32_t& face) {
+    const float ox = static_cast<float>(r.o.x), oy = static_cast<float>(r.o.y), oz = static_cast<float>(r.o.z);
+    const float ix = 1.0f / static_cast<float>(r.d.x), iy = 1.0f / static_cast<float>(r.d.y), iz = 1.0f / static_cast<float>(r.d.z);
+    const float oix = ox * ix, oiy = oy * iy, oiz = oz * iz;
+    const float tminf = f_lo(tmin);
+    float tmaxf = f_hi(tmax);
+    bool hit = false;
+    int sp = 0;
+    int32_t node = root;
+    for (;;) {
+        while (node >= 0) {
+            const float4* np = reinterpret_cast<const float4*>(S.nodes + node);
+            const float4 a = np[0], b = np[1], c = np[2];
+            const int4 ch = reinterpret_cast<const int4*>(np)[3];
+            const float l0x = a.x * ix - oix, l1x = a.y * ix - oix, l0y = a.z * iy - oiy, l1y = a.w * iy - oiy;
+            const float l0z = c.x * iz - oiz, l1z = c.y * iz - oiz;
+            const float r0x = b.x * ix - oix, r1x = b.y * ix - oix, r0y = b.z * iy - oiy, r1y = b.w * iy - oiy;
+            const float r0z = c.z * iz - oiz, r1z = c.w * iz - oiz;
+            const float llo = fmaxf(fmaxf(fminf(l0x, l1x), fminf(l0y, l1y)), fmaxf(fminf(l0z, l1z), tminf));
+            const float lhi = fminf(fminf(fmaxf(l0x, l1x), fmaxf(l0y, l1y)), fminf(fmaxf(l0z, l1z), tmaxf));
+            const float rlo = fmaxf(fmaxf(fminf(r0x, r1x), fminf(r0y, r1y)), fmaxf(fminf(r0z, r1z), tminf));
+            const float rhi = fminf(fminf(fmaxf(r0x, r1x), fmaxf(r0y, r1y)), fminf(fmaxf(r0z, r1z), tmaxf));
+            const bool hl = llo <= lhi, hr = rlo <= rhi;
+            if (!hl && !hr) {
+                node = sp > 0 ? stk[(--sp) * kBlock] : kNodeEmpty;
+            } else {
+                int32_t first = hl ? ch.x : ch.y;
+                if (hl && hr) {
+                    int32_t second = ch.y;
+                    if (rlo < llo) {
+                        first = ch.y;
+                        second = ch.x;
+                    }
+                    stk[(sp++) * kBlock] = second;
+                }
+                node = first;
+            }
+        }
+        if (node == kNodeEmpty) break;
+        const uint32_t first = leaf_first(node), cnt = leaf_count(node);
+        for (uint32_t k = 0; k < cnt; ++k) {
+            const uint32_t ref = S.primrefs[first + k];
+            R tt;
+            uint32_t fc = 0;
+            if (hit_prim(S, ref, r, tmin, tmax, tt, fc)) {
+                tmax = tt;
+                t = tt;
+                prim = ref;
+                face = fc;
+                hit = true;
+                tmaxf = f_hi(tt);
+            }
+        }
+        node = sp > 0 ? stk[(--sp) * kBlock] : kNodeEmpty;
+    }
+    return hit;
+}
+
+// ------------------------------------------------------------------------------------------------ objects
+template <class R>
+__device__ __forceinline__ Ray<R> xform_in(const ObjRec<R>& o, const Ray<R>& r) {
+    Ray<R> out = r;
+    if (o.kind == OBJ_TRANSLATE) {  // hittable.cpp:4: moved_r(origin - offset, direction, time)
+        out.o = r.o - mk(o.p[0], o.p[1], o.p[2]);
+    } else {  // hittable.cpp:58-67
+        const R s = o.p[0], c = o.p[1];
+        out.o.x = c * r.o.x - s * r.o.z;
+        out.o.z = s * r.o.x + c * r.o.z;
+        out.d.x = c * r.d.x - s * r.d.z;
+        out.d.z = s * r.d.x + c * r.d.z;
+    }
+    return out;
+}
+
+// Any non-medium object: prim, BVH, or a translate/rotate_y chain (<= kMaxXformChain) over one of them.
+template <class R>
+__device__ __forceinline__ bool hit_object(const DevScene<R>& S, int32_t oi, Ray<R> r, R tmin, R tmax, int32_t* stk, R& t, uint32_t& prim,
+                                           uint32_t& face) {
+#pragma unroll
+    for (int c = 0; c < kMaxXformChain; ++c) {
+        const ObjRec<R>& o = S.objs[oi];
+        if (o.kind != OBJ_TRANSLATE && o.kind != OBJ_ROTATE_Y) break;
+        r = xform_in(o, r);
+        oi = o.a;
+    }
+    const ObjRec<R>& o = S.objs[oi];
+    if (o.kind == OBJ_PRIM) {
+        prim = static_cast<uint32_t>(o.a);
+        return hit_prim(S, prim, r, tmin, tmax, t, face);
+    }
+    return traverse(S, o.a, r, tmin, tmax, stk, t, prim, face);
+}
+
+// constant_medium.h:37-82.  Consumes one uniform when the clamped interval is non-empty.
+template <class R>
+__device__ __forceinline__ bool hit_medium(const DevScene<R>& S, const ObjRec<R>& m, const Ray<R>& r, R tmin, R tmax, int32_t* stk,
+                                           uint64_t& rng, R& t) {
+    const R inf = R(__builtin_inf());
+    R t1, t2;
+    uint32_t p, f;
+    if (!hit_object(S, m.a, r, -inf, inf, stk, t1, p, f)) return false;
+    if (!hit_object(S, m.a, r, t1 + R(0.0001), inf, stk, t2, p, f)) return false;
+    if (t1 < tmin) t1 = tmin;
+    if (t2 > tmax) t2 = tmax;
+    if (t1 >= t2) return false;
+    if (t1 < R(0)) t1 = R(0);
+    const R ray_length = sqrt(len2(r.d));
+    const R inside = (t2 - t1) * ray_length;
+    const R hit_distance = m.p[0] * log(uniform<R>(rng));
+    if (hit_distance > inside) return false;
+    t = t1 + hit_distance / ray_length;
+    return true;
+}
+
+// The world hittable_list (hittable_list.cpp:5-19): objects in order, t_max = closest so far.
+struct HitOut {
+    uint32_t prim, obj;  // obj: world slot | box face << 16
+};
+template <class R, bool MEDIA>
+__device__ __forceinline__ bool trace_world(const DevScene<R>& S, const Ray<R>& r, int32_t* stk, uint64_t& rng, R& t, HitOut& h) {
+    R closest = R(__builtin_inf());
+    bool any = false;
+    for (int w = 0; w < S.nworld; ++w) {
+        const int32_t oi = S.world[w];
+        const ObjRec<R>& o = S.objs[oi];
+        R tt;
+        if (MEDIA && o.kind == OBJ_MEDIUM) {
+            if (hit_medium(S, o, r, R(0.001), closest, stk, rng, tt)) {
+                closest = tt;
+                any = true;
+                h.prim = kMediumHit;
+                h.obj = static_cast<uint32_t>(w);
+            }
+        } else if (!MEDIA || o.kind != OBJ_MEDIUM) {
+            uint32_t prim = 0, face = 0;
+            if (hit_object(S, oi, r, R(0.001), closest, stk, tt, prim, face)) {
+                closest = tt;
+                any = true;
+                h.prim = prim;
+                h.obj = static_cast<uint32_t>(w) | (face << 16);
+            }
+        }
+    }
+    t = closest;
+    return any;
+}
+
+// ------------------------------------------------------------------------------------------------ surfaces
+template <class R>
+struct Surf {
+    V3<R> p, n;
+    R u, v;
+    bool ff;
+    uint32_t mat;
+};
+template <class R>
+__device__ __forceinline__ void set_face_normal(Surf<R>& s, const Ray<R>& r, V3<R> outward) {  // hittable.h:18-22
+    s.ff = dot(r.d, outward) < R(0);
+    s.n = s.ff ? outward : -outward;
+}
+template <class R>
+__device__ __forceinline__ void rect_surface(Surf<R>& s, int axis, R a0, R a1, R b0, R b1, R k, const Ray<R>& r, R t) {
+    const int ia = axis == 2 ? 1 : 0;
+    const int ib = axis == 0 ? 1 : 2;
+    const R x = comp(r.o, ia) + t * comp(r.d, ia);
+    const R y = comp(r.o, ib) + t * comp(r.d, ib);
+    s.u = (x - a0) / (a1 - a0);
+    s.v = (y - b0) / (b1 - b0);
+    const V3<R> n = axis == 0 ? mk(R(0), R(0), R(1)) : (axis == 1 ? mk(R(0), R(1), R(0)) : mk(R(1), R(0), R(0)));
+    set_face_normal(s, r, n);
+    s.p = r.at(t);
+}
+template <class R>
+__device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref, uint32_t face, const Ray<R>& r, R t, Surf<R>& s) {
+    const uint32_t idx = primref_index(ref);
+    switch (primref_type(ref)) {
+        case PRIM_SPHERE: {  // sphere.h:57-63, :24-37
+            const SphereRec<R>& sp = S.spheres[idx];
+            V3<R> center = ld3(sp.c);
+            const bool moving = (sp.flags & SPH_MOVING) != 0;
+            if (moving) center = center + ((r.tm - sp.t0) / sp.dt) * ld3(sp.d);
+            s.p = r.at(t);
+            const V3<R> outward = divs(s.p - center, sp.r);
+            set_face_normal(s, r, outward);
+            if (!moving) {
+                const R pi = R(3.1415926535897932385);
+                const R theta = acos(-outward.y);
+                const R phi = atan2(-outward.z, outward.x) + pi;
+                s.u = phi / (R(2) * pi);
+                s.v = theta / pi;
+            } else {
+                s.u = R(0);
+                s.v = R(0);
+            }
+            s.mat = sp.mat;
+            break;
+        }
+        case PRIM_TRIANGLE: {  // triangle.h:57-85
+            const TriRec<R>& tr = S.tris[idx];
+            const V3<R> p1 = ld3(tr.p), p2 = ld3(tr.p + 3), p3 = ld3(tr.p + 6);
+            const V3<R> N = cross(p2 - p1, p3 - p1);
+            const V3<R> p = r.o + t * r.d;
+            const R u = dot(N, cross(p3 - p2, p - p2));
+            const R v = dot(N, cross(p1 - p3, p - p3));
+            s.p = p;
+            set_face_normal(s, r, N);
+            s.u = u / len2(N);
+            s.v = v / len2(N);
+            s.mat = tr.mat;
+            break;
+        }
+        case PRIM_RECT: {
+            const RectRec<R>& q = S.rects[idx];
+            rect_surface(s, static_cast<int>(q.axis), q.a0, q.a1, q.b0, q.b1, q.k, r, t);
+            s.mat = q.mat;
+            break;
+        }
+        default: {
+            const BoxRec<R>& b = S.boxes[idx];
+            int axis;
+            R a0, a1, b0, b1, k;
+            box_face(b, static_cast<int>(face), axis, a0, a1, b0, b1, k);
+            rect_surface(s, axis, a0, a1, b0, b1, k, r, t);
+            s.mat = b.mat;
+            break;
+        }
+    }
+}
+
+// Rebuilds the hit_record of the world object that won (transform chain unwound as translate::hit / rotate_y::hit
+// do it: hittable.cpp:7-11, :72-84, including set_face_normal against the transformed ray).
+template <class R>
+__device__ __forceinline__ void world_surface(const DevScene<R>& S, const HitOut& h, const Ray<R>& r, R t, Surf<R>& s) {
+    const int32_t w = static_cast<int32_t>(h.obj & 0xFFFFu);
+    int32_t oi = S.world[w];
+    if (h.prim == kMediumHit) {  // constant_medium.h:75-79
+        s.p = r.at(t);
+        s.n = mk(R(1), R(0), R(0));
+        s.ff = true;
+        s.u = R(0);
+        s.v = R(0);
+        s.mat = static_cast<uint32_t>(S.objs[oi].b);
+        return;
+    }
+    static_assert(kMaxXformChain == 2, "world_surface unwinds at most two transforms");
+    int32_t o0 = -1, o1 = -1;
+    Ray<R> r1 = r, r2 = r;
+    {
+        const ObjRec<R>& o = S.objs[oi];
+        if (o.kind == OBJ_TRANSLATE || o.kind == OBJ_ROTATE_Y) {
+            o0 = oi;
+            r1 = xform_in(o, r);
+            oi = o.a;
+            const ObjRec<R>& q = S.objs[oi];
+            if (q.kind == OBJ_TRANSLATE || q.kind == OBJ_ROTATE_Y) {
+                o1 = oi;
+                r2 = xform_in(q, r1);
+                oi = q.a;
+            } else {
+                r2 = r1;
+            }
+        }
+    }
+    prim_surface(S, h.prim, h.obj >> 16, r2, t, s);
+    auto unwind = [&](int32_t xo, const Ray<R>& inner) {
+        const ObjRec<R>& o = S.objs[xo];
+        if (o.kind == OBJ_TRANSLATE) {
+            s.p = s.p + mk(o.p[0], o.p[1], o.p[2]);
+            set_face_normal(s, inner, s.n);
+        } else {
+            const R sn = o.p[0], c = o.p[1];
+            V3<R> p = s.p, n = s.n;
+            p.x = c * s.p.x + sn * s.p.z;
+            p.z = -sn * s.p.x + c * s.p.z;
+            n.x = c * s.n.x + sn * s.n.z;
+            n.z = -sn * s.n.x + c * s.n.z;
+            s.p = p;
+            set_face_normal(s, inner, n);
+        }
+    };
+    if (o1 >= 0) unwind(o1, r2);
+    if (o0 >= 0) unwind(o0, r1);
+}
+
+// ------------------------------------------------------------------------------------------------ textures
+template <class R>
+__device__ __forceinline__ R perlin_noise(const PerlinRec<R>& pn, V3<R> p) {  // perlin.h:21-40, :83-97
+    const R u = p.x - floor(p.x), v = p.y - floor(p.y), w = p.z - floor(p.z);
+    const int i = static_cast<int>(floor(p.x)), j = static_cast<int>(floor(p.y)), k = static_cast<int>(floor(p.z));
+    const R uu = u * u * (R(3) - R(2) * u), vv = v * v * (R(3) - R(2) * v), ww = w * w * (R(3) - R(2) * w);
+    R accum = R(0);
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++)
+#pragma unroll
+            for (int c = 0; c < 2; c++) {
+                const int idx = pn.perm[0][(i + a) & 255] ^ pn.perm[1][(j + b) & 255] ^ pn.perm[2][(k + c) & 255];
+                const V3<R> g = ld3(pn.ranvec[idx]);
+                const V3<R> wv = mk(u - R(a), v - R(b), w - R(c));
+                accum += (R(a) * uu + R(1 - a) * (R(1) - uu)) * (R(b) * vv + R(1 - b) * (R(1) - vv)) *
+                         (R(c) * ww + R(1 - c) * (R(1) - ww)) * dot(g, wv);
+            }
+    return accum;
+}
+template <class R>
+__device__ __forceinline__ V3<R> image_value(const DevScene<R>& S, int32_t im, R u, R v) {  // texture.h:90-117
+    const ImageRec& I = S.images[im];
+    u = fmin(fmax(u, R(0)), R(1));
+    v = R(1) - fmin(fmax(v, R(0)), R(1));
+    int i = static_cast<int>(u * R(I.w));
+    int j = static_cast<int>(v * R(I.h));
+    if (i >= I.w) i = I.w - 1;
+    if (j >= I.h) j = I.h - 1;
+    const R cs = R(1.0 / 255.0);
+    const uint8_t* px = S.texels + I.offset + static_cast<uint64_t>(j) * static_cast<uint64_t>(I.bpp * I.w) + static_cast<uint64_t>(i) * I.bpp;
+    return mk(cs * R(px[0]), cs * R(px[1]), cs * R(px[2]));
+}
+template <class R>
+__device__ __forceinline__ V3<R> tex_value(const DevScene<R>& S, int32_t ti, R u, R v, V3<R> p) {  // rendering/texture.h
+    for (int level = 0; level < 4; ++level) {
+        const TexRec<R>& t = S.texs[ti];
+        switch (t.type) {
+            case TEX_SOLID: return ld3(t.c);
+            case TEX_CHECKER: {
+                const R sines = sin(R(10) * p.x) * sin(R(10) * p.y) * sin(R(10) * p.z);
+                ti = sines < R(0) ? t.odd : t.even;
+                continue;
+            }
+            case TEX_NOISE: {
+                const R n = perlin_noise(S.perlins[t.perlin], t.scale * p);
+                const R h = (R(1) + n) * R(0.5);
+                return mk(h, h, h);
+            }
+            case TEX_IMAGE: return image_value(S, t.image, u, v);
+            default: {
+                const R w = R(1) - u - v;
+                return image_value(S, t.image, u * t.uv[0] + v * t.uv[2] + w * t.uv[4], u * t.uv[1] + v * t.uv[3] + w * t.uv[5]);
+            }
+        }
+    }
+    return mk(R(0), R(1), R(1));
+}
+
+}  // namespace art

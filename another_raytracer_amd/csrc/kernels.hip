@@ -1,0 +1,732 @@
+// kernels.hip — the wavefront path tracer for gfx950 (MI355X).
+//
+// The reference's recursive integrator (engine.h:58-68 _stochastic_sample + engine.h:447-466 _ray_color) is
+// flattened into an iterative per-ray wavefront loop over a pool of P = k * npix paths (k samples of every local
+// pixel per pass).  Per pass:
+//   k_gen                      camera rays for every (pixel, sample) slot; PCG32 keyed by (seed, pixel, sample)
+//   for depth d < max_depth:
+//     k_extend<R, MEDIA>       closest hit over the world list (LDS-stack BVH traversal, f32 boxes, R leaf tests),
+//                              misses finish their path (L += T*background); hits are appended to one of five
+//                              material queues (branch sorting for the shade stage)
+//     k_shade<R>               per material queue: emitted + scatter; survivors go to the next active queue
+//   k_accum                    adds the k per-slot radiances into the f64 pixel sums in sample order
+// then k_finalize (write_color, color.h:6-22).  All queue sizes live on the device; extend/shade are persistent
+// grids whose waves claim 64 items at a time from an atomic counter, so no host round trip happens inside a render.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "device.h"
+#include "renderer.h"
+
+namespace art {
+
+#define HIP_OK(x)                                                                                         \
+    do {                                                                                                  \
+        hipError_t e_ = (x);                                                                              \
+        if (e_ != hipSuccess) throw std::runtime_error(std::string(#x) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+// Per-(pass, depth) counter block.
+constexpr int kCStride = 8;  // [0] active queue size, [1] extend claim, [2] shade claim, [3..7] material queue sizes
+constexpr int kCQueue = 0, kCExtGrab = 1, kCShadeGrab = 2, kCMat = 3;
+
+// ------------------------------------------------------------------------------------------------ path records
+// One path = one AoS record so that a lane touching a scattered slot reads whole cache lines:
+//   f32: 64 B = {o.xyz, time} {d.xyz, -} {T.rgb, L.r} {L.gb, rng}       f64: 128 B, same fields.
+template <class R> struct PathRec;
+template <> struct PathRec<float> {
+    float4 ot, d, tl, lr;
+};
+template <> struct PathRec<double> {
+    double2 a, b, c, e, f, g, h, i;  // (ox,oy) (oz,tm) (dx,dy) (dz,-) (Tr,Tg) (Tb,Lr) (Lg,Lb) (rng,-)
+};
+template <class R>
+struct PathState {
+    Ray<R> ray;
+    V3<R> T, L;
+    uint64_t rng;
+};
+__device__ __forceinline__ void load_path(const PathRec<float>* P, uint32_t q, PathState<float>& s, bool full) {
+    const PathRec<float>& p = P[q];
+    const float4 ot = p.ot, d = p.d;
+    s.ray.o = mk(ot.x, ot.y, ot.z);
+    s.ray.tm = ot.w;
+    s.ray.d = mk(d.x, d.y, d.z);
+    const float4 lr = p.lr;
+    s.rng = (static_cast<uint64_t>(__float_as_uint(lr.w)) << 32) | __float_as_uint(lr.z);
+    if (full) {
+        const float4 tl = p.tl;
+        s.T = mk(tl.x, tl.y, tl.z);
+        s.L = mk(tl.w, lr.x, lr.y);
+    }
+}
+__device__ __forceinline__ void store_path(PathRec<float>* P, uint32_t q, const PathState<float>& s) {
+    PathRec<float>& p = P[q];
+    p.ot = make_float4(s.ray.o.x, s.ray.o.y, s.ray.o.z, s.ray.tm);
+    p.d = make_float4(s.ray.d.x, s.ray.d.y, s.ray.d.z, 0.0f);
+    p.tl = make_float4(s.T.x, s.T.y, s.T.z, s.L.x);
+    p.lr = make_float4(s.L.y, s.L.z, __uint_as_float(static_cast<uint32_t>(s.rng)), __uint_as_float(static_cast<uint32_t>(s.rng >> 32)));
+}
+__device__ __forceinline__ void store_rng(PathRec<float>* P, uint32_t q, uint64_t rng) {
+    float2* p = reinterpret_cast<float2*>(&P[q].lr) + 1;
+    *p = make_float2(__uint_as_float(static_cast<uint32_t>(rng)), __uint_as_float(static_cast<uint32_t>(rng >> 32)));
+}
+__device__ __forceinline__ void load_path(const PathRec<double>* P, uint32_t q, PathState<double>& s, bool full) {
+    const PathRec<double>& p = P[q];
+    const double2 a = p.a, b = p.b, c = p.c, e = p.e, i = p.i;
+    s.ray.o = mk(a.x, a.y, b.x);
+    s.ray.tm = b.y;
+    s.ray.d = mk(c.x, c.y, e.x);
+    s.rng = static_cast<uint64_t>(__double_as_longlong(i.x));
+    if (full) {
+        const double2 f = p.f, g = p.g, h = p.h;
+        s.T = mk(f.x, f.y, g.x);
+        s.L = mk(g.y, h.x, h.y);
+    }
+}
+__device__ __forceinline__ void store_path(PathRec<double>* P, uint32_t q, const PathState<double>& s) {
+    PathRec<double>& p = P[q];
+    p.a = make_double2(s.ray.o.x, s.ray.o.y);
+    p.b = make_double2(s.ray.o.z, s.ray.tm);
+    p.c = make_double2(s.ray.d.x, s.ray.d.y);
+    p.e = make_double2(s.ray.d.z, 0.0);
+    p.f = make_double2(s.T.x, s.T.y);
+    p.g = make_double2(s.T.z, s.L.x);
+    p.h = make_double2(s.L.y, s.L.z);
+    p.i = make_double2(__longlong_as_double(static_cast<long long>(s.rng)), 0.0);
+}
+__device__ __forceinline__ void store_rng(PathRec<double>* P, uint32_t q, uint64_t rng) {
+    P[q].i.x = __longlong_as_double(static_cast<long long>(rng));
+}
+
+template <class R>
+struct HitRecD {  // extend -> shade hand-off, 16 B
+    R t;
+    uint32_t prim, obj;
+};
+template <> struct HitRecD<double> {
+    double t;
+    uint32_t prim, obj;
+};
+
+template <class R> struct ResRec;  // final per-slot radiance
+template <> struct ResRec<float> { float4 v; };
+template <> struct ResRec<double> { double2 a, b; };
+__device__ __forceinline__ void store_res(ResRec<float>* res, uint32_t q, V3<float> L) { res[q].v = make_float4(L.x, L.y, L.z, 0.0f); }
+__device__ __forceinline__ void store_res(ResRec<double>* res, uint32_t q, V3<double> L) {
+    res[q].a = make_double2(L.x, L.y);
+    res[q].b = make_double2(L.z, 0.0);
+}
+__device__ __forceinline__ void load_res(const ResRec<float>* res, uint32_t q, double& r, double& g, double& b) {
+    const float4 v = res[q].v;
+    r = v.x; g = v.y; b = v.z;
+}
+__device__ __forceinline__ void load_res(const ResRec<double>* res, uint32_t q, double& r, double& g, double& b) {
+    const double2 a = res[q].a, c = res[q].b;
+    r = a.x; g = a.y; b = c.x;
+}
+
+// ------------------------------------------------------------------------------------------------ launch arguments
+struct PassGeom {
+    int32_t W, H;               // full image
+    int32_t rows;               // local rows
+    int32_t band_rows, band_count, band_index;
+    uint32_t tiles_x, npix_pad; // 8x8 tiles over (W x rows)
+    uint32_t k;                 // samples in this pass
+    uint32_t sample_base;       // first sample index of the pass
+    uint32_t P;                 // k * npix_pad
+    int32_t max_depth;
+    uint64_t seed;
+};
+template <class R>
+struct Work {
+    PathRec<R>* paths;
+    HitRecD<R>* hits;
+    ResRec<R>* res;
+    uint32_t* queue[2];
+    uint32_t* mq[kNumMatTypes];
+    uint32_t* counters;  // this pass's block: (max_depth + 1) * kCStride
+    double* acc;         // local pixels * 3
+};
+
+__device__ __forceinline__ int global_row(const PassGeom& g, int ly) {  // row-interleaved band partition
+    return (ly / g.band_rows) * (g.band_rows * g.band_count) + g.band_index * g.band_rows + (ly % g.band_rows);
+}
+__device__ __forceinline__ bool slot_pixel(const PassGeom& g, uint32_t qi, int& lx, int& ly) {
+    const uint32_t tile = qi >> 6, within = qi & 63u;
+    lx = static_cast<int>((tile % g.tiles_x) * 8 + (within & 7u));
+    ly = static_cast<int>((tile / g.tiles_x) * 8 + (within >> 3));
+    return lx < g.W && ly < g.rows;
+}
+
+// Wave-aggregated append: one atomic per wave, lanes write in lane order.
+__device__ __forceinline__ void wave_append(bool pred, uint32_t val, uint32_t* queue, uint32_t* counter) {
+    const uint64_t mask = __ballot(pred);
+    if (mask == 0) return;
+    const uint32_t lane = __lane_id();
+    const int leader = __ffsll(static_cast<long long>(mask)) - 1;
+    uint32_t base = 0;
+    if (static_cast<int>(lane) == leader) base = atomicAdd(counter, static_cast<uint32_t>(__popcll(mask)));
+    base = __shfl(base, leader);
+    if (pred) {
+        const uint32_t off = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(mask >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(mask), 0u));
+        queue[base + off] = val;
+    }
+}
+__device__ __forceinline__ uint32_t wave_claim(uint32_t* counter) {
+    uint32_t base = 0;
+    if (__lane_id() == 0) base = atomicAdd(counter, 64u);
+    return __shfl(base, 0);
+}
+
+// ------------------------------------------------------------------------------------------------ kernels
+// engine.h:58-68 + camera.h:38-47 for one slot.
+template <class R>
+__global__ __launch_bounds__(256) void k_gen(PassGeom g, CameraRec<R> cam, Work<R> w) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    bool live = false;
+    if (q < g.P) {
+        const uint32_t j = q / g.npix_pad;
+        const uint32_t qi = q - j * g.npix_pad;
+        int lx, ly;
+        if (j < g.k && slot_pixel(g, qi, lx, ly)) {
+            const int gy = global_row(g, ly);
+            const uint32_t pixel = static_cast<uint32_t>(gy) * static_cast<uint32_t>(g.W) + static_cast<uint32_t>(lx);
+            uint64_t rng = pcg_seed(g.seed, pixel, g.sample_base + j);
+            const R ru = uniform<R>(rng);
+            const R rv = uniform<R>(rng);
+            const R s = (R(lx) + ru) / R(g.W - 1);
+            const R t = (R(g.H - 1 - gy) + rv) / R(g.H - 1);
+            V3<R> p;
+            for (;;) {  // random_in_unit_disk (vec3.h:137-143): x, then y
+                p.x = uniform<R>(rng, R(-1), R(1));
+                p.y = uniform<R>(rng, R(-1), R(1));
+                p.z = R(0);
+                if (len2(p) >= R(1)) continue;
+                break;
+            }
+            const V3<R> rd = cam.lens_radius * p;
+            const V3<R> offset = rd.x * ld3(cam.u) + rd.y * ld3(cam.v);
+            PathState<R> st;
+            st.ray.o = ld3(cam.origin) + offset;
+            st.ray.d = ld3(cam.llc) + s * ld3(cam.horizontal) + t * ld3(cam.vertical) - ld3(cam.origin) - offset;
+            st.ray.tm = uniform<R>(rng, cam.time0, cam.time1);
+            st.T = mk(R(1), R(1), R(1));
+            st.L = mk(R(0), R(0), R(0));
+            st.rng = rng;
+            if (g.max_depth > 0) {
+                store_path(w.paths, q, st);
+                live = true;
+            } else {
+                store_res(w.res, q, st.L);
+            }
+        }
+    }
+    wave_append(live, q, w.queue[0], &w.counters[kCQueue]);
+}
+
+template <class R, bool MEDIA>
+__global__ __launch_bounds__(kBlock) void k_extend(DevScene<R> S, Work<R> w, int d) {
+    __shared__ int32_t stack[kStackDepth * kBlock];
+    int32_t* stk = stack + threadIdx.x;
+    uint32_t* cnt = w.counters + d * kCStride;
+    const uint32_t count = __hip_atomic_load(&cnt[kCQueue], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t* queue = w.queue[d & 1];
+    for (;;) {
+        const uint32_t base = wave_claim(&cnt[kCExtGrab]);
+        if (base >= count) break;
+        const uint32_t i = base + __lane_id();
+        int mtype = -1;
+        uint32_t q = 0;
+        if (i < count) {
+            q = queue[i];
+            PathState<R> st;
+            load_path(w.paths, q, st, false);
+            R t;
+            HitOut h{0, 0};
+            if (trace_world<R, MEDIA>(S, st.ray, stk, st.rng, t, h)) {
+                w.hits[q] = HitRecD<R>{t, h.prim, h.obj};
+                uint32_t m;
+                if (h.prim == kMediumHit) {
+                    m = static_cast<uint32_t>(S.objs[S.world[h.obj & 0xFFFFu]].b);
+                } else {
+                    const uint32_t idx = primref_index(h.prim);
+                    switch (primref_type(h.prim)) {
+                        case PRIM_SPHERE: m = S.spheres[idx].mat; break;
+                        case PRIM_TRIANGLE: m = S.tris[idx].mat; break;
+                        case PRIM_RECT: m = S.rects[idx].mat; break;
+                        default: m = S.boxes[idx].mat; break;
+                    }
+                }
+                mtype = static_cast<int>(S.mats[m].type);
+                if (MEDIA) store_rng(w.paths, q, st.rng);
+            } else {  // engine.h:455-456: miss -> background
+                load_path(w.paths, q, st, true);
+                st.L = st.L + st.T * mk(S.bg[0], S.bg[1], S.bg[2]);
+                store_res(w.res, q, st.L);
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < kNumMatTypes; ++m) wave_append(mtype == m, q, w.mq[m], &cnt[kCMat + m]);
+    }
+}
+
+// material.h scatter() + emitted() for one hit; returns false when the path ends here.
+template <class R>
+__device__ __forceinline__ bool scatter(const DevScene<R>& S, const MatRec<R>& m, const Surf<R>& s, PathState<R>& st, V3<R>& att, V3<R>& dir) {
+    switch (m.type) {
+        case MAT_LAMBERTIAN: {  // material.h:20-43
+            const V3<R> rv = unit(in_unit_sphere<R>(st.rng));
+            dir = s.n + rv;
+            if (near_zero(dir)) dir = s.n;
+            att = tex_value(S, m.tex, s.u, s.v, s.p);
+            return true;
+        }
+        case MAT_METAL: {  // material.h:45-61
+            const V3<R> reflected = reflect(unit(st.ray.d), s.n);
+            dir = reflected + m.fuzz * in_unit_sphere<R>(st.rng);
+            att = ld3(m.albedo);
+            return dot(dir, s.n) > R(0);
+        }
+        case MAT_DIELECTRIC: {  // material.h:63-99
+            att = mk(R(1), R(1), R(1));
+            const R ratio = s.ff ? (R(1) / m.ir) : m.ir;
+            const V3<R> ud = unit(st.ray.d);
+            const R cos_theta = fmin(dot(-ud, s.n), R(1));
+            const R sin_theta = sqrt(R(1) - cos_theta * cos_theta);
+            const bool cannot = ratio * sin_theta > R(1);
+            bool refl = cannot;
+            if (!cannot) {
+                R r0 = (R(1) - ratio) / (R(1) + ratio);
+                r0 = r0 * r0;
+                const R refl_p = r0 + (R(1) - r0) * pow((R(1) - cos_theta), R(5));
+                refl = refl_p > uniform<R>(st.rng);
+            }
+            dir = refl ? reflect(ud, s.n) : refract(ud, s.n, ratio);
+            return true;
+        }
+        case MAT_ISOTROPIC: {  // material.h:120-135
+            dir = in_unit_sphere<R>(st.rng);
+            att = tex_value(S, m.tex, s.u, s.v, s.p);
+            return true;
+        }
+        default: return false;  // diffuse_light
+    }
+}
+
+template <class R>
+__global__ __launch_bounds__(kBlock) void k_shade(DevScene<R> S, Work<R> w, int d, int max_depth) {
+    uint32_t* cnt = w.counters + d * kCStride;
+    uint32_t pre[kNumMatTypes + 1];
+    pre[0] = 0;
+#pragma unroll
+    for (int m = 0; m < kNumMatTypes; ++m) pre[m + 1] = pre[m] + __hip_atomic_load(&cnt[kCMat + m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t total = pre[kNumMatTypes];
+    uint32_t* next_q = w.queue[(d + 1) & 1];
+    uint32_t* next_cnt = w.counters + (d + 1) * kCStride + kCQueue;
+    const bool last = d + 1 >= max_depth;
+    for (;;) {
+        const uint32_t base = wave_claim(&cnt[kCShadeGrab]);
+        if (base >= total) break;
+        const uint32_t i = base + __lane_id();
+        bool cont = false;
+        uint32_t q = 0;
+        if (i < total) {
+            const uint32_t* mq = w.mq[0];
+            uint32_t first = 0;
+#pragma unroll
+            for (int k = 1; k < kNumMatTypes; ++k)
+                if (i >= pre[k]) {
+                    mq = w.mq[k];
+                    first = pre[k];
+                }
+            q = mq[i - first];
+            PathState<R> st;
+            load_path(w.paths, q, st, true);
+            const HitRecD<R> h = w.hits[q];
+            Surf<R> s;
+            world_surface(S, HitOut{h.prim, h.obj}, st.ray, h.t, s);
+            const MatRec<R>& mat = S.mats[s.mat];
+            if (mat.type == MAT_LIGHT) st.L = st.L + st.T * tex_value(S, mat.tex, s.u, s.v, s.p);  // material.h:114-116
+            if (!last) {
+                V3<R> att, dir;
+                if (scatter(S, mat, s, st, att, dir)) {
+                    st.T = st.T * att;
+                    st.ray.o = s.p;
+                    st.ray.d = dir;
+                    store_path(w.paths, q, st);
+                    cont = true;
+                }
+            }
+            if (!cont) store_res(w.res, q, st.L);
+        }
+        wave_append(cont, q, next_q, next_cnt);
+    }
+}
+
+template <class R>
+__global__ __launch_bounds__(256) void k_accum(PassGeom g, Work<R> w) {
+    const uint32_t qi = blockIdx.x * blockDim.x + threadIdx.x;
+    if (qi >= g.npix_pad) return;
+    int lx, ly;
+    if (!slot_pixel(g, qi, lx, ly)) return;
+    double* a = w.acc + 3 * (static_cast<size_t>(ly) * g.W + lx);
+    double r = a[0], gg = a[1], b = a[2];
+    for (uint32_t j = 0; j < g.k; ++j) {  // sample order == the reference's `pixel_color +=` order
+        double x, y, z;
+        load_res(w.res, j * g.npix_pad + qi, x, y, z);
+        r += x;
+        gg += y;
+        b += z;
+    }
+    a[0] = r;
+    a[1] = gg;
+    a[2] = b;
+}
+
+__global__ void k_finalize(const double* acc, uint8_t* rgb, uint32_t n, int spp) {  // color.h:6-22
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double scale = 1.0 / spp;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        double x = sqrt(scale * acc[3 * i + c]);
+        x = x < 0.0 ? 0.0 : (x > 0.999 ? 0.999 : x);
+        rgb[3 * i + c] = static_cast<uint8_t>(256 * x);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------ device scene
+template <class R>
+struct DeviceScene {
+    std::vector<void*> allocs;
+    DevScene<R> view{};
+    bool media = false;
+    size_t bytes = 0;
+
+    template <class T>
+    const T* upload(const std::vector<T>& v) {
+        if (v.empty()) return nullptr;
+        void* p = nullptr;
+        HIP_OK(hipMalloc(&p, v.size() * sizeof(T)));
+        HIP_OK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+        allocs.push_back(p);
+        bytes += v.size() * sizeof(T);
+        return static_cast<const T*>(p);
+    }
+    void release() {
+        for (void* p : allocs) (void)hipFree(p);
+        allocs.clear();
+    }
+};
+
+template <class R, class D>
+static void cvt_sphere(const SphereRec<D>& s, SphereRec<R>& o) {
+    for (int a = 0; a < 3; ++a) { o.c[a] = R(s.c[a]); o.d[a] = R(s.d[a]); }
+    o.r = R(s.r); o.t0 = R(s.t0); o.dt = R(s.dt); o.mat = s.mat; o.flags = s.flags;
+}
+
+template <class R>
+static void build_device_scene(const FlatScene& f, DeviceScene<R>& ds) {
+    std::vector<SphereRec<R>> sph(f.spheres.size());
+    for (size_t i = 0; i < sph.size(); ++i) cvt_sphere(f.spheres[i], sph[i]);
+    std::vector<TriRec<R>> tri(f.tris.size());
+    for (size_t i = 0; i < tri.size(); ++i) {
+        for (int a = 0; a < 9; ++a) tri[i].p[a] = R(f.tris[i].p[a]);
+        tri[i].mat = f.tris[i].mat;
+        tri[i].pad = 0;
+    }
+    std::vector<RectRec<R>> rect(f.rects.size());
+    for (size_t i = 0; i < rect.size(); ++i) {
+        const auto& s = f.rects[i];
+        rect[i] = RectRec<R>{R(s.a0), R(s.a1), R(s.b0), R(s.b1), R(s.k), s.axis, s.mat};
+    }
+    std::vector<BoxRec<R>> box(f.boxes.size());
+    for (size_t i = 0; i < box.size(); ++i) {
+        for (int a = 0; a < 3; ++a) { box[i].mn[a] = R(f.boxes[i].mn[a]); box[i].mx[a] = R(f.boxes[i].mx[a]); }
+        box[i].mat = f.boxes[i].mat;
+        box[i].pad = 0;
+    }
+    std::vector<ObjRec<R>> objs(f.objs.size());
+    for (size_t i = 0; i < objs.size(); ++i) {
+        objs[i].kind = f.objs[i].kind; objs[i].a = f.objs[i].a; objs[i].b = f.objs[i].b; objs[i].pad = 0;
+        for (int a = 0; a < 4; ++a) objs[i].p[a] = R(f.objs[i].p[a]);
+    }
+    std::vector<MatRec<R>> mats(f.mats.size());
+    for (size_t i = 0; i < mats.size(); ++i) {
+        mats[i].type = f.mats[i].type; mats[i].tex = f.mats[i].tex;
+        for (int a = 0; a < 3; ++a) mats[i].albedo[a] = R(f.mats[i].albedo[a]);
+        mats[i].fuzz = R(f.mats[i].fuzz); mats[i].ir = R(f.mats[i].ir);
+    }
+    std::vector<TexRec<R>> texs(f.texs.size());
+    for (size_t i = 0; i < texs.size(); ++i) {
+        const auto& s = f.texs[i];
+        texs[i].type = s.type; texs[i].even = s.even; texs[i].odd = s.odd; texs[i].perlin = s.perlin; texs[i].image = s.image; texs[i].pad = 0;
+        for (int a = 0; a < 3; ++a) texs[i].c[a] = R(s.c[a]);
+        texs[i].scale = R(s.scale);
+        for (int a = 0; a < 6; ++a) texs[i].uv[a] = R(s.uv[a]);
+    }
+    std::vector<PerlinRec<R>> per(f.perlins.size());
+    for (size_t i = 0; i < per.size(); ++i) {
+        for (int v = 0; v < 256; ++v) for (int a = 0; a < 3; ++a) per[i].ranvec[v][a] = R(f.perlins[i].ranvec[v][a]);
+        std::memcpy(per[i].perm, f.perlins[i].perm, sizeof per[i].perm);
+    }
+    ds.view.spheres = ds.upload(sph);
+    ds.view.tris = ds.upload(tri);
+    ds.view.rects = ds.upload(rect);
+    ds.view.boxes = ds.upload(box);
+    ds.view.primrefs = ds.upload(f.primrefs);
+    ds.view.nodes = ds.upload(f.nodes);
+    ds.view.objs = ds.upload(objs);
+    ds.view.world = ds.upload(f.world);
+    ds.view.mats = ds.upload(mats);
+    ds.view.texs = ds.upload(texs);
+    ds.view.perlins = ds.upload(per);
+    ds.view.images = ds.upload(f.images);
+    ds.view.texels = ds.upload(f.texels);
+    ds.view.nworld = static_cast<int32_t>(f.world.size());
+    for (int a = 0; a < 3; ++a) ds.view.bg[a] = R(f.background[a]);
+    ds.media = f.has_media;
+}
+
+// ------------------------------------------------------------------------------------------------ renderer
+struct Renderer::Impl {
+    int device = 0;
+    int num_cu = 256;
+    hipStream_t own_stream = nullptr;
+    FlatScene flat;
+    DeviceScene<float> s32;
+    DeviceScene<double> s64;
+    bool up32 = false, up64 = false;
+    // workspace (grow-only)
+    void* ws = nullptr;
+    size_t ws_bytes = 0;
+    hipEvent_t ev[2] = {nullptr, nullptr};
+
+    ~Impl() {
+        s32.release();
+        s64.release();
+        if (ws) (void)hipFree(ws);
+        for (auto& e : ev) if (e) (void)hipEventDestroy(e);
+        if (own_stream) (void)hipStreamDestroy(own_stream);
+    }
+    void* workspace(size_t bytes) {
+        if (bytes > ws_bytes) {
+            if (ws) HIP_OK(hipFree(ws));
+            ws = nullptr;
+            HIP_OK(hipMalloc(&ws, bytes));
+            ws_bytes = bytes;
+        }
+        return ws;
+    }
+};
+
+Renderer::Renderer(FlatScene flat, int device) : impl_(new Impl) {
+    impl_->device = device;
+    HIP_OK(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HIP_OK(hipGetDeviceProperties(&prop, device));
+    impl_->num_cu = prop.multiProcessorCount;
+    impl_->flat = std::move(flat);
+    HIP_OK(hipStreamCreateWithFlags(&impl_->own_stream, hipStreamNonBlocking));
+}
+Renderer::~Renderer() {
+    if (impl_) {
+        (void)hipSetDevice(impl_->device);
+        delete impl_;
+    }
+}
+size_t Renderer::scene_bytes(int fp) const {
+    return fp == RT_FP64 ? impl_->s64.bytes : impl_->s32.bytes;
+}
+const FlatScene& Renderer::flat() const { return impl_->flat; }
+
+template <class R, bool MEDIA>
+static int persistent_blocks(int num_cu) {
+    static int ext = 0;
+    if (!ext) {
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_extend<R, MEDIA>, kBlock, 0) != hipSuccess || per_cu < 1) per_cu = 2;
+        ext = per_cu;
+    }
+    return ext * num_cu;
+}
+template <class R>
+static int shade_blocks(int num_cu) {
+    static int sh = 0;
+    if (!sh) {
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_shade<R>, kBlock, 0) != hipSuccess || per_cu < 1) per_cu = 2;
+        sh = per_cu;
+    }
+    return sh * num_cu;
+}
+
+template <class R>
+static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<double>& camd, const RenderParams& p, uint8_t* out_rgb,
+                        double* out_acc, RenderStats& stats) {
+    hipStream_t stream = p.stream ? static_cast<hipStream_t>(p.stream) : I.own_stream;
+    for (int a = 0; a < 3; ++a) ds.view.bg[a] = R(p.background[a]);  // engine::set_scene's background
+    // local rows of this band partition
+    std::vector<int> rows;
+    for (int ly = 0;; ++ly) {
+        int gy = (ly / p.band_rows) * (p.band_rows * p.band_count) + p.band_index * p.band_rows + (ly % p.band_rows);
+        if (gy >= p.height) break;
+        rows.push_back(gy);
+    }
+    const int nrows = static_cast<int>(rows.size());
+    stats.local_rows = nrows;
+    if (nrows == 0) return;
+    PassGeom g{};
+    g.W = p.width;
+    g.H = p.height;
+    g.rows = nrows;
+    g.band_rows = p.band_rows;
+    g.band_count = p.band_count;
+    g.band_index = p.band_index;
+    g.tiles_x = static_cast<uint32_t>((p.width + 7) / 8);
+    const uint32_t tiles_y = static_cast<uint32_t>((nrows + 7) / 8);
+    g.npix_pad = g.tiles_x * tiles_y * 64u;
+    g.max_depth = p.max_depth;
+    g.seed = p.seed;
+    // samples per pass: ~16M path slots per pass (memory is cheap on a 288 GB part; big passes amortise the
+    // per-depth launch tail), never more than spp.
+    uint32_t k = p.samples_per_pass > 0 ? static_cast<uint32_t>(p.samples_per_pass)
+                                        : std::max<uint32_t>(1u, (16u << 20) / g.npix_pad);
+    k = std::min<uint32_t>(k, static_cast<uint32_t>(p.spp));
+    const uint32_t Pmax = k * g.npix_pad;
+    const int npasses = static_cast<int>((p.spp + k - 1) / k);
+    const int depth_slots = p.max_depth + 1;
+    const size_t local_pix = static_cast<size_t>(nrows) * p.width;
+
+    auto al = [](size_t x) { return (x + 255) & ~static_cast<size_t>(255); };
+    size_t off = 0;
+    const size_t o_paths = off; off += al(sizeof(PathRec<R>) * Pmax);
+    const size_t o_hits = off; off += al(sizeof(HitRecD<R>) * Pmax);
+    const size_t o_res = off; off += al(sizeof(ResRec<R>) * Pmax);
+    const size_t o_q0 = off; off += al(4ull * Pmax);
+    const size_t o_q1 = off; off += al(4ull * Pmax);
+    size_t o_mq[kNumMatTypes];
+    for (int m = 0; m < kNumMatTypes; ++m) { o_mq[m] = off; off += al(4ull * Pmax); }
+    const size_t cnt_words = static_cast<size_t>(npasses) * depth_slots * kCStride;
+    const size_t o_cnt = off; off += al(4ull * cnt_words);
+    const size_t o_acc = off; off += al(sizeof(double) * 3 * local_pix);
+    const size_t o_rgb = off; off += al(3 * local_pix);
+    char* base = static_cast<char*>(I.workspace(off));
+
+    Work<R> w{};
+    w.paths = reinterpret_cast<PathRec<R>*>(base + o_paths);
+    w.hits = reinterpret_cast<HitRecD<R>*>(base + o_hits);
+    w.res = reinterpret_cast<ResRec<R>*>(base + o_res);
+    w.queue[0] = reinterpret_cast<uint32_t*>(base + o_q0);
+    w.queue[1] = reinterpret_cast<uint32_t*>(base + o_q1);
+    for (int m = 0; m < kNumMatTypes; ++m) w.mq[m] = reinterpret_cast<uint32_t*>(base + o_mq[m]);
+    uint32_t* counters = reinterpret_cast<uint32_t*>(base + o_cnt);
+    w.acc = reinterpret_cast<double*>(base + o_acc);
+    uint8_t* drgb = reinterpret_cast<uint8_t*>(base + o_rgb);
+
+    CameraRec<R> cam{};
+    for (int a = 0; a < 3; ++a) {
+        cam.origin[a] = R(camd.origin[a]); cam.llc[a] = R(camd.llc[a]); cam.horizontal[a] = R(camd.horizontal[a]);
+        cam.vertical[a] = R(camd.vertical[a]); cam.u[a] = R(camd.u[a]); cam.v[a] = R(camd.v[a]);
+    }
+    cam.lens_radius = R(camd.lens_radius);
+    cam.time0 = R(camd.time0);
+    cam.time1 = R(camd.time1);
+
+    const bool prof = (p.flags & RT_PROFILE) != 0;
+    std::vector<hipEvent_t> evs;
+
+    for (auto& e : I.ev)
+        if (!e) HIP_OK(hipEventCreate(&e));
+    if (prof) {  // event pool created before the timed region
+        evs.resize(static_cast<size_t>(npasses) * p.max_depth * 3);
+        for (auto& e : evs) HIP_OK(hipEventCreate(&e));
+    }
+    size_t ev_next = 0;
+    auto mark = [&]() { HIP_OK(hipEventRecord(evs[ev_next++], stream)); };
+    HIP_OK(hipEventRecord(I.ev[0], stream));
+    HIP_OK(hipMemsetAsync(counters, 0, 4ull * cnt_words, stream));
+    HIP_OK(hipMemsetAsync(w.acc, 0, sizeof(double) * 3 * local_pix, stream));
+    const int ext_blocks = ds.media ? persistent_blocks<R, true>(I.num_cu) : persistent_blocks<R, false>(I.num_cu);
+    const int sh_blocks = shade_blocks<R>(I.num_cu);
+    for (int pass = 0; pass < npasses; ++pass) {
+        g.sample_base = static_cast<uint32_t>(pass) * k;
+        g.k = std::min<uint32_t>(k, static_cast<uint32_t>(p.spp) - g.sample_base);
+        g.P = g.k * g.npix_pad;
+        w.counters = counters + static_cast<size_t>(pass) * depth_slots * kCStride;
+        hipLaunchKernelGGL(k_gen<R>, dim3((g.P + 255) / 256), dim3(256), 0, stream, g, cam, w);
+        for (int d = 0; d < p.max_depth; ++d) {
+            if (prof) mark();
+            if (ds.media) hipLaunchKernelGGL((k_extend<R, true>), dim3(ext_blocks), dim3(kBlock), 0, stream, ds.view, w, d);
+            else hipLaunchKernelGGL((k_extend<R, false>), dim3(ext_blocks), dim3(kBlock), 0, stream, ds.view, w, d);
+            if (prof) mark();
+            hipLaunchKernelGGL(k_shade<R>, dim3(sh_blocks), dim3(kBlock), 0, stream, ds.view, w, d, p.max_depth);
+            if (prof) mark();
+        }
+        hipLaunchKernelGGL(k_accum<R>, dim3((g.npix_pad + 255) / 256), dim3(256), 0, stream, g, w);
+    }
+    HIP_OK(hipGetLastError());
+    const uint32_t npix = static_cast<uint32_t>(local_pix);
+    hipLaunchKernelGGL(k_finalize, dim3((npix + 255) / 256), dim3(256), 0, stream, w.acc, drgb, npix, p.spp);
+    HIP_OK(hipEventRecord(I.ev[1], stream));
+    const hipMemcpyKind kind_rgb = (p.flags & RT_OUT_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    if (out_rgb) HIP_OK(hipMemcpyAsync(out_rgb, drgb, 3 * local_pix, kind_rgb, stream));
+    if (out_acc) HIP_OK(hipMemcpyAsync(out_acc, w.acc, sizeof(double) * 3 * local_pix, kind_rgb, stream));
+    std::vector<uint32_t> hc(cnt_words);
+    HIP_OK(hipMemcpyAsync(hc.data(), counters, 4ull * cnt_words, hipMemcpyDeviceToHost, stream));
+    HIP_OK(hipStreamSynchronize(stream));
+    float ms = 0;
+    HIP_OK(hipEventElapsedTime(&ms, I.ev[0], I.ev[1]));
+    stats.ms = ms;
+    stats.passes = npasses;
+    stats.samples_per_pass = static_cast<int>(k);
+    uint64_t segs = 0;
+    for (int pass = 0; pass < npasses; ++pass)
+        for (int d = 0; d < p.max_depth; ++d) segs += hc[(static_cast<size_t>(pass) * depth_slots + d) * kCStride + kCQueue];
+    stats.segments = segs;
+    stats.primary = static_cast<uint64_t>(local_pix) * static_cast<uint64_t>(p.spp);
+    if (prof) {
+        double ext_ms = 0, sh_ms = 0;
+        for (size_t e = 0; e + 2 < evs.size(); e += 3) {
+            float a = 0, b = 0;
+            HIP_OK(hipEventElapsedTime(&a, evs[e], evs[e + 1]));
+            HIP_OK(hipEventElapsedTime(&b, evs[e + 1], evs[e + 2]));
+            ext_ms += a;
+            sh_ms += b;
+        }
+        stats.extend_ms = ext_ms;
+        stats.shade_ms = sh_ms;
+        stats.extend_launches = static_cast<uint64_t>(npasses) * p.max_depth;
+        stats.shade_launches = stats.extend_launches;
+        for (auto e : evs) (void)hipEventDestroy(e);
+    }
+}
+
+void Renderer::render(const CameraRec<double>& cam, const RenderParams& p, uint8_t* out_rgb, double* out_acc, RenderStats& stats) {
+    HIP_OK(hipSetDevice(impl_->device));
+    if (p.fp_mode == RT_FP64) {
+        if (!impl_->up64) { build_device_scene(impl_->flat, impl_->s64); impl_->up64 = true; }
+        render_impl<double>(*impl_, impl_->s64, cam, p, out_rgb, out_acc, stats);
+    } else {
+        if (!impl_->up32) { build_device_scene(impl_->flat, impl_->s32); impl_->up32 = true; }
+        render_impl<float>(*impl_, impl_->s32, cam, p, out_rgb, out_acc, stats);
+    }
+}
+
+}  // namespace art
+
+namespace art {
+int device_count() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+}  // namespace art

@@ -1,0 +1,131 @@
+// layout.h — the flat scene and path-state layout in HBM, shared by host (g++) and device (hipcc) code.
+//
+// The reference walks an OOP graph of shared_ptr<hittable> with virtual hit()/scatter()/value()
+// (engine/hittable.h:25-29, rendering/material.h:10-17, rendering/texture.h:11-14).  Here the same graph is
+// compiled (scene.cpp: compile()) into typed arrays:
+//   * primitives   per-type AoS records (SphereRec, TriRec, RectRec, BoxRec), addressed by a 32-bit prim ref
+//   * BVH          one flat array of 64-B two-child nodes (f32, conservatively rounded boxes) per scene
+//   * objects      the top-level hittable_list (world) as ObjRec: PRIM | BVH | XFORM (translate/rotate_y) | MEDIUM
+//   * materials    MatRec, textures TexRec, perlin tables, image texel pool
+// Every record exists in an f64 and an f32 instantiation (template R); the BVH is always f32.
+#pragma once
+#include <cstdint>
+
+#if defined(__HIPCC__)
+#define ART_HD __host__ __device__ inline
+#else
+#define ART_HD inline
+#endif
+
+namespace art {
+
+// ---------------------------------------------------------------------------------------------- prims
+enum PrimType : uint32_t { PRIM_SPHERE = 0, PRIM_TRIANGLE = 1, PRIM_RECT = 2, PRIM_BOX = 3 };
+constexpr uint32_t kPrimTypeShift = 30;
+constexpr uint32_t kPrimIndexMask = (1u << kPrimTypeShift) - 1;
+ART_HD uint32_t make_primref(uint32_t type, uint32_t idx) { return (type << kPrimTypeShift) | idx; }
+ART_HD uint32_t primref_type(uint32_t ref) { return ref >> kPrimTypeShift; }
+ART_HD uint32_t primref_index(uint32_t ref) { return ref & kPrimIndexMask; }
+
+enum SphereFlags : uint32_t { SPH_MOVING = 1u };  // moving_sphere: centre lerp over [t0, t0+dt], no u,v
+
+template <class R>
+struct SphereRec {      // sphere.h / moving_sphere.h
+    R c[3];             // center (center0 for moving spheres)
+    R r;                // radius
+    R d[3];             // center1 - center0 (moving only)
+    R t0, dt;           // time0, time1 - time0 (moving only)
+    uint32_t mat;
+    uint32_t flags;
+};
+template <class R>
+struct TriRec {         // triangle.h: pt1, pt2, pt3
+    R p[9];
+    uint32_t mat;
+    uint32_t pad;
+};
+template <class R>
+struct RectRec {        // aarect.h: axis 0 = xy_rect (k on z), 1 = xz_rect (k on y), 2 = yz_rect (k on x)
+    R a0, a1, b0, b1, k;
+    uint32_t axis;
+    uint32_t mat;
+};
+template <class R>
+struct BoxRec {         // box.cpp: six rects in a fixed order (face index 0..5 = box.cpp:8-17 order)
+    R mn[3], mx[3];
+    uint32_t mat;
+    uint32_t pad;
+};
+
+// ---------------------------------------------------------------------------------------------- BVH
+// Two-child node, 64 B = one cache line, fetched as four 16-B loads.  Child boxes are rounded outward to
+// f32 and padded, so f32 traversal is conservative; leaf tests run in R.
+//   child >= 0 : inner node index;   child < 0 : leaf ~((count << 24) | first_primref_slot);   -1 : empty
+struct BvhNode {
+    float lx0, lx1, ly0, ly1;   // left  child box x/y
+    float rx0, rx1, ry0, ry1;   // right child box x/y
+    float lz0, lz1, rz0, rz1;   // z of both
+    int32_t left, right, pad0, pad1;
+};
+static_assert(sizeof(BvhNode) == 64, "BvhNode must be one 64-B line");
+constexpr int32_t kNodeEmpty = -1;
+ART_HD int32_t make_leaf(uint32_t first, uint32_t count) { return ~static_cast<int32_t>((count << 24) | first); }
+ART_HD uint32_t leaf_first(int32_t c) { return static_cast<uint32_t>(~c) & 0xFFFFFFu; }
+ART_HD uint32_t leaf_count(int32_t c) { return (static_cast<uint32_t>(~c) >> 24) & 0x7Fu; }
+constexpr int kMaxLeafPrims = 4;
+constexpr int kMaxBvhDepth = 30;   // traversal stack (LDS) depth is kStackDepth >= kMaxBvhDepth + 1
+constexpr int kStackDepth = 32;
+
+// ---------------------------------------------------------------------------------------------- objects
+enum ObjKind : int32_t { OBJ_PRIM = 0, OBJ_BVH = 1, OBJ_TRANSLATE = 2, OBJ_ROTATE_Y = 3, OBJ_MEDIUM = 4 };
+template <class R>
+struct ObjRec {
+    int32_t kind;
+    int32_t a;      // PRIM: prim ref; BVH: root node; TRANSLATE/ROTATE_Y: child object; MEDIUM: boundary object
+    int32_t b;      // MEDIUM: phase material
+    int32_t pad;
+    R p[4];         // TRANSLATE: offset xyz; ROTATE_Y: sin, cos; MEDIUM: neg_inv_density
+};
+constexpr int kMaxXformChain = 2;  // translate(rotate_y(X)) is the deepest chain in the reference scenes
+
+// ---------------------------------------------------------------------------------------------- shading
+enum MatType : uint32_t { MAT_LAMBERTIAN = 0, MAT_METAL = 1, MAT_DIELECTRIC = 2, MAT_LIGHT = 3, MAT_ISOTROPIC = 4 };
+constexpr int kNumMatTypes = 5;
+template <class R>
+struct MatRec {
+    uint32_t type;
+    int32_t tex;    // lambertian / diffuse_light / isotropic
+    R albedo[3];    // metal
+    R fuzz;         // metal (already clamped to <= 1, material.h:47)
+    R ir;           // dielectric
+};
+enum TexType : uint32_t { TEX_SOLID = 0, TEX_CHECKER = 1, TEX_NOISE = 2, TEX_IMAGE = 3, TEX_BARY_IMAGE = 4 };
+template <class R>
+struct TexRec {
+    uint32_t type;
+    int32_t even, odd;   // checker children
+    int32_t perlin;      // noise: perlin table index
+    int32_t image;       // image / bary_image: image index
+    int32_t pad;
+    R c[3];              // solid colour
+    R scale;             // noise scale
+    R uv[6];             // bary_image texcoords a, b, c
+};
+template <class R>
+struct PerlinRec {       // perlin.h: 256 random unit vectors + 3 permutations
+    R ranvec[256][3];
+    int32_t perm[3][256];
+};
+struct ImageRec {
+    uint64_t offset;     // into the texel pool
+    int32_t w, h, bpp, pad;
+};
+
+// ---------------------------------------------------------------------------------------------- camera
+template <class R>
+struct CameraRec {       // camera.h: precomputed on the host in f64 exactly as camera::camera does
+    R origin[3], llc[3], horizontal[3], vertical[3], u[3], v[3];
+    R lens_radius, time0, time1;
+};
+
+}  // namespace art

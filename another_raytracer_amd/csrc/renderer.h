@@ -1,0 +1,44 @@
+// renderer.h — host-side device renderer (implemented in kernels.hip; no HIP types in this header).
+#pragma once
+#include <cstdint>
+
+#include "art.h"
+#include "layout.h"
+#include "scene.h"
+
+namespace art {
+
+struct RenderParams {
+    int width = 0, height = 0, spp = 1, max_depth = 50;
+    uint64_t seed = 0;
+    int fp_mode = RT_FP32;
+    int band_rows = 1, band_count = 1, band_index = 0;
+    int samples_per_pass = 0;
+    int flags = 0;
+    void* stream = nullptr;
+    double background[3] = {0, 0, 0};
+};
+
+struct RenderStats {
+    uint64_t segments = 0, primary = 0;
+    double ms = 0, extend_ms = 0, shade_ms = 0;
+    uint64_t extend_launches = 0, shade_launches = 0;
+    int passes = 0, samples_per_pass = 0, local_rows = 0;
+};
+
+class Renderer {
+public:
+    struct Impl;
+    Renderer(FlatScene flat, int device);
+    ~Renderer();
+    Renderer(const Renderer&) = delete;
+    Renderer& operator=(const Renderer&) = delete;
+    void render(const CameraRec<double>& cam, const RenderParams& p, uint8_t* out_rgb, double* out_acc, RenderStats& stats);
+    size_t scene_bytes(int fp_mode) const;
+    const FlatScene& flat() const;
+
+private:
+    Impl* impl_;
+};
+
+}  // namespace art

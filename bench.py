@@ -1,0 +1,193 @@
+"""Benchmark: Msamples/s (primary + secondary rays) of the HIP path on BASELINE.json's headline workload.
+
+    python bench.py [--gpus N --steps K --warmup W] [--scene 1 --width 1920 --height 1080 --spp 1024]
+
+One step = one full frame of configs[1] ("'One Weekend' final random-spheres scene, 1920x1080, 1024 spp"): every
+rank renders its row-interleaved bands (another_raytracer_amd/distributed.py) and rank 0 gathers the RGB8 frame over
+RCCL.  The total work per step is fixed as N grows ("scaling": "strong"); value = all segments traced by all ranks /
+max-over-ranks wall time of the K timed steps.  A segment is one ray traced through the world (one world.hit call of
+engine.h:453), counted exactly on the device from the wavefront queue sizes.
+
+Extra fields:
+  roofline      dominant kernel (k_extend): algorithmic bytes per segment x segments / summed launch time
+                measured live with HIP events on the render stream during the timed steps; HBM peak 8 TB/s.
+                `traffic` = FETCH_SIZE*2 + WRITE_SIZE per segment from the committed rocprofv3 PMC summary
+                (profiles/, MI355X_MICROARCH.md "HBM") scaled to this run, or null.
+  cpu_baseline  the reference itself (oracle/_ref/ref_harness = /root/reference/src compiled unmodified), its own
+                CPU-parallel mode (engine.h:335-376: 4 row stripes, 4 threads, shared global RNG) on a bounded sample
+                of the same workload (same scene, full 1920x1080, reduced spp), rank 0 at N=1 only.
+"""
+import argparse
+import glob
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# k_extend algorithmic bytes per segment: queue index 4 + ray (origin, time, direction) + hit record 16
+# + material-queue entry 4.  f32 path record: ray = 32 B; f64: 64 B.
+EXTEND_BYTES = {"f32": 4 + 32 + 16 + 4, "f64": 4 + 64 + 16 + 4}
+# whole-bounce (extend + shade) path-record traffic, SURVEY.md §8(d)'s per-segment figure for this layout
+BOUNCE_BYTES = {"f32": 4 + 32 + 16 + 4 + 4 + 64 + 16 + 64 + 4, "f64": 4 + 64 + 16 + 4 + 4 + 128 + 16 + 128 + 4}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scene", default="1")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=1024)
+    ap.add_argument("--max-depth", type=int, default=50)
+    ap.add_argument("--precision", default="f32", choices=["f32", "f64"])
+    ap.add_argument("--band-rows", type=int, default=16)
+    ap.add_argument("--samples-per-pass", type=int, default=0)
+    ap.add_argument("--no-profile", action="store_true", help="skip per-launch HIP events (no roofline)")
+    ap.add_argument("--cpu-baseline-spp", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(args):
+    harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    if not os.path.exists(harness):
+        return None
+    threads = 4
+    out = subprocess.run([harness, "render", args.scene, str(args.width), str(args.height), str(args.cpu_baseline_spp),
+                          "/tmp/bench_cpu_ref", "stripes", str(threads)], capture_output=True, text=True, timeout=900)
+    if out.returncode != 0:
+        return {"error": out.stderr.strip()[-300:]}
+    info = json.loads(out.stdout.strip().splitlines()[-1])
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
+    except OSError:
+        pass
+    return {"value": round(info["mseg_per_s"], 4), "unit": "Msamples/s", "cores": threads, "kind": "reference",
+            "sample": f"scene {args.scene} {args.width}x{args.height}x{args.cpu_baseline_spp}spp "
+                      f"({info['segments']} segments, {info['ms'] / 1e3:.1f} s), engine_mode::parallel_stripes "
+                      f"semantics (4 threads, shared global mt19937); per-segment cost is spp-independent",
+            "cpu_model": model, "host_cpus": os.cpu_count()}
+
+
+def latest_traffic(precision, scene):
+    """Per-segment HBM bytes of k_extend from the newest committed PMC summary (profiles/*pmc*.json), or None."""
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if d.get("precision") == precision and str(d.get("scene")) == str(scene) and d.get("extend_bytes_per_segment"):
+            best = d
+    return best
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    import another_raytracer_amd as art
+    from another_raytracer_amd.distributed import band_rows_of, render_frame
+
+    world_scene = art.scene_manager(device=dev.index).build(args.scene)
+    cam = art.camera(world_scene.lookfrom, world_scene.lookat, (0, 1, 0), world_scene.vfov, args.width / args.height,
+                     world_scene.aperture, 10.0, 0.0, 1.0)
+    eng = art.engine(cam, art.engine_mode.parallel_stripes, width=args.width, height=args.height,
+                     samples_per_pixel=args.spp, max_depth=args.max_depth, device=dev.index, precision=args.precision,
+                     samples_per_pass=args.samples_per_pass)
+    eng.set_scene(world_scene.objects, world_scene.background)
+    rows = band_rows_of(args.height, args.band_rows, world, rank)
+    local = torch.empty((len(rows), args.width, 3), dtype=torch.uint8, device=dev)
+    profile = not args.no_profile
+
+    def step():
+        return render_frame(eng, band_rows=args.band_rows, device=dev, profile=profile, out_local=local)
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    segs = 0
+    ext_ms = shade_ms = gpu_ms = 0.0
+    ext_launches = 0
+    frame = None
+    for _ in range(args.steps):
+        frame, st = step()
+        segs += st["segments"]
+        ext_ms += st["extend_ms"]
+        shade_ms += st["shade_ms"]
+        gpu_ms += st["ms"]
+        ext_launches += st["extend_launches"]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    stats = torch.tensor([elapsed, float(segs), ext_ms, shade_ms, float(ext_launches)], dtype=torch.float64, device=dev)
+    if world > 1:
+        t_max = stats[:1].clone()
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        tot = stats[1:].clone()
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        elapsed = float(t_max.item())
+        segs, ext_ms, shade_ms, ext_launches = (float(x) for x in tot.tolist())
+    if rank == 0:
+        value = segs / elapsed / 1e6
+        primary = args.width * args.height * args.spp * args.steps
+        line = {
+            "metric": "Msamples/sec (primary+secondary rays) at 1920x1080x1024spp; 1/2/4/8 GPU",
+            "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": args.precision, "data": "synthetic",
+            "config": {"workload": f"scene_alias {args.scene} ('One Weekend' final random spheres)" if args.scene == "1"
+                       else f"scene {args.scene}", "width": args.width, "height": args.height, "spp": args.spp,
+                       "max_depth": args.max_depth, "parallelism": f"row-bands({args.band_rows}) x {world} + rccl gather",
+                       "segments_per_step": int(segs / args.steps), "primary_rays_per_step": primary // args.steps,
+                       "mprimary_per_s": round(primary / elapsed / 1e6, 3)},
+        }
+        if profile and ext_ms > 0:
+            per_launch_ms = ext_ms / max(ext_launches, 1)
+            achieved = EXTEND_BYTES[args.precision] * segs / (ext_ms * 1e-3) / 1e9
+            tr = latest_traffic(args.precision, args.scene)
+            line["roofline"] = {
+                "bound": "hbm", "kernel": "k_extend", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                "traffic": (round(tr["extend_bytes_per_segment"] * segs / max(ext_launches, 1)) if tr else None),
+                "algorithmic_bytes_per_segment": EXTEND_BYTES[args.precision],
+                "avg_launch_ms": round(per_launch_ms, 4), "launches": int(ext_launches),
+                "extend_ms_total": round(ext_ms, 2), "shade_ms_total": round(shade_ms, 2),
+                "bounce_bytes_per_segment": BOUNCE_BYTES[args.precision],
+                "bounce_achieved_gbs": round(BOUNCE_BYTES[args.precision] * segs / ((ext_ms + shade_ms) * 1e-3) / 1e9, 2),
+            }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,157 @@
+/* include/art.h — C ABI of the MI355X path tracer (libart.so).
+ *
+ * Drop-in boundary for the hot path of blackccpie/another_raytracer: what `src/main.cpp:29-46` does with the
+ * reference's scene_manager / camera / engine classes maps onto these calls.  Plain pointers and sizes only; no C++,
+ * torch or HIP types cross this boundary (a hipStream_t travels as void*).  No exceptions cross it: every call returns
+ * RT_OK (0) or a negative RT_E* code, with a message in rt_last_error() (thread-local).
+ *
+ *   reference (file:line)                                        replacement
+ *   scene scene_manager::build(scene_alias)  scene_manager.cpp:260  rt_scene_build(name, assets, device, &scene)
+ *   struct scene {lookfrom, lookat, vfov, aperture, background}   rt_scene_info(scene, &info)
+ *     scene_manager.h:6-14
+ *   camera::camera(lookfrom, lookat, vup, vfov, aspect, aperture, rt_camera (POD, same 9 arguments)
+ *     focus_dist, t0, t1)                camera.h:8-36
+ *   engine<W,H,C>(const camera&, engine_mode)  engine.h:22        rt_params (W, H, spp, max_depth are runtime here:
+ *   engine::set_scene(hittable_list, color)   engine.h:24-28       tracer_constants.h:6-14 made them compile-time)
+ *   int engine::run(uint8_t* out)             engine.h:30-54      rt_render(scene, &cam, &params, out_rgb8, ...)
+ *   write_color (gamma 2, clamp, quantize)    color.h:6-22        inside rt_render (f64 sums -> RGB8, row 0 = top)
+ *   hittable constructors (sphere.h, moving_sphere.h, triangle.h, rt_graph_* (one call per constructor, same
+ *     aarect.h, box.h, hittable_list.h, bvh.h, hittable.h,          arguments); rt_graph_compile -> rt_scene
+ *     constant_medium.h, material.h, texture.h)
+ *
+ * RNG contract: the reference draws from one global std::mt19937 (tracer_utils.h:27-31).  Scene construction here
+ * replays that generator exactly (seed 5489, same draw order), so scenes are bit-identical.  Rendering draws come
+ * from PCG32 streams keyed by (seed, global pixel j*W+i, sample index): results depend on neither the tiling nor the
+ * GPU count, and oracle/restate.cpp (ORC_PCG) replays the same streams on the CPU.
+ */
+#ifndef ART_H
+#define ART_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+/* return codes */
+#define RT_OK 0
+#define RT_E_INVALID (-1)   /* bad argument */
+#define RT_E_SCENE (-2)     /* scene build / compile failure (e.g. "Invalid input scene!", engine.h:32-36) */
+#define RT_E_DEVICE (-3)    /* HIP runtime failure or no device */
+#define RT_E_INTERNAL (-4)
+
+/* rt_params.fp_mode: arithmetic of the leaf tests and shading (BVH box tests are always conservative f32) */
+#define RT_FP32 0
+#define RT_FP64 1
+/* rt_params.flags */
+#define RT_OUT_DEVICE 1     /* out_rgb8 / out_accum are device pointers (on the scene's device) */
+#define RT_PROFILE 2        /* time every extend/shade launch with HIP events (rt_stats.*_ms) */
+
+typedef struct rt_scene rt_scene;
+typedef struct rt_graph rt_graph;
+
+typedef struct rt_camera {      /* camera.h:8-18 constructor arguments */
+    double lookfrom[3];
+    double lookat[3];
+    double vup[3];
+    double vfov;                /* vertical field of view, degrees */
+    double aspect;              /* aspect ratio (the reference hard-codes 4:3 in main.cpp:35) */
+    double aperture;
+    double focus_dist;          /* main.cpp:34 uses 10 */
+    double time0, time1;        /* shutter; main.cpp:35 uses 0, 1 */
+} rt_camera;
+
+typedef struct rt_params {
+    int32_t width, height;      /* full image */
+    int32_t spp;                /* samples per pixel (tracer_constants.h:12) */
+    int32_t max_depth;          /* bounce limit (tracer_constants.h:13; 50) */
+    uint64_t seed;              /* render RNG seed */
+    int32_t fp_mode;            /* RT_FP32 | RT_FP64 */
+    int32_t band_rows;          /* row-interleaved partition: global row y belongs to band (y / band_rows) and */
+    int32_t band_count;         /*   is rendered here when band % band_count == band_index; (H, 1, 0) = whole image */
+    int32_t band_index;
+    int32_t samples_per_pass;   /* 0 = auto (~16M path slots per pass) */
+    int32_t flags;              /* RT_OUT_DEVICE | RT_PROFILE */
+    void* stream;               /* hipStream_t to run on, or NULL for the scene's own stream */
+    double background[3];       /* engine::set_scene(world, background) (engine.h:24-28): returned on a miss */
+} rt_params;
+
+typedef struct rt_stats {
+    uint64_t segments;          /* rays traced through the world (world.hit calls): the metric's unit */
+    uint64_t primary;           /* camera rays = local pixels * spp */
+    double ms;                  /* device time, first kernel -> finalized RGB8 (HIP events) */
+    double extend_ms, shade_ms; /* RT_PROFILE only: summed launch durations */
+    uint64_t extend_launches, shade_launches;
+    int32_t passes, samples_per_pass, local_rows, pad;
+} rt_stats;
+
+typedef struct rt_scene_info {  /* scene_manager.h:6-14 */
+    double lookfrom[3], lookat[3];
+    double vfov, aperture;
+    double background[3];
+    int64_t spheres, triangles, rects, boxes, bvh_nodes, objects, materials, textures;
+    int32_t has_media, max_bvh_depth;
+    uint64_t device_bytes_f32, device_bytes_f64;
+} rt_scene_info;
+
+/* ---- library ---- */
+int rt_abi_version(void);
+const char* rt_last_error(void);
+int rt_device_count(void);
+
+/* ---- scenes ---- */
+/* Builtin scenes = scene_manager::build(alias): "1".."8" or "random", "two_spheres", "two_perlin_spheres", "earth",
+ * "simple_light", "cornell_box", "cornell_smoke", "final"; plus "c1" (SURVEY Q7 3-sphere scene), "cow", "dino"
+ * (SURVEY Q8 mesh scenes).  asset_dir holds cow.tris, dino.tris, earthmap.rgb. */
+int rt_scene_build(const char* name, const char* asset_dir, int device, rt_scene** out);
+int rt_scene_info_get(const rt_scene* scene, rt_scene_info* info);
+/* Canonical JSON of the scene graph (schema of oracle/ref_harness `dump`); returns the size needed incl. NUL. */
+size_t rt_scene_dump(const rt_scene* scene, char* buf, size_t cap);
+void rt_scene_destroy(rt_scene* scene);
+
+/* ---- render (engine::run) ----
+ * out_rgb8: local_rows * width * 3 bytes (row-major, local row 0 = the first row this band set owns, top-most first);
+ * out_accum (optional): local_rows * width * 3 f64 radiance sums (pixel_color before write_color).  Host pointers
+ * unless RT_OUT_DEVICE.  Blocking. */
+int rt_render(rt_scene* scene, const rt_camera* cam, const rt_params* params, uint8_t* out_rgb8, double* out_accum, rt_stats* stats);
+/* Number of rows a band partition owns, and optionally their global indices (rows_out may be NULL). */
+int rt_local_rows(const rt_params* params, int32_t* rows_out);
+
+/* ---- scene graph builder (one call per reference constructor; returns an id >= 0 or a negative code) ----
+ * Scene-build randomness (noise textures' perlin tables, rt_graph_bvh's node draws) comes from the graph's own
+ * mt19937 (seed 5489), in call order, exactly as the reference's global generator would produce it. */
+rt_graph* rt_graph_new(void);
+void rt_graph_free(rt_graph* g);
+int rt_graph_random_double(rt_graph* g, double* out);              /* random_double() from the graph's generator */
+int rt_tex_solid(rt_graph* g, double r, double gr, double b);       /* texture.h:16-29 */
+int rt_tex_checker(rt_graph* g, int even, int odd);                 /* texture.h:31-50 */
+int rt_tex_noise(rt_graph* g, double scale);                        /* texture.h:52-65 */
+int rt_tex_image(rt_graph* g, int w, int h, int bpp, const uint8_t* texels); /* texture.h:67-118 */
+int rt_mat_lambertian(rt_graph* g, int tex);                        /* material.h:20-43 */
+int rt_mat_metal(rt_graph* g, double r, double gr, double b, double fuzz); /* material.h:45-61 */
+int rt_mat_dielectric(rt_graph* g, double ir);                      /* material.h:63-99 */
+int rt_mat_diffuse_light(rt_graph* g, int tex);                     /* material.h:101-118 */
+int rt_obj_sphere(rt_graph* g, const double c[3], double r, int mat);                 /* sphere.h */
+int rt_obj_moving_sphere(rt_graph* g, const double c0[3], const double c1[3], double t0, double t1, double r, int mat);
+int rt_obj_triangle(rt_graph* g, const double p1[3], const double p2[3], const double p3[3], int mat); /* triangle.h */
+int rt_obj_rect(rt_graph* g, int axis /*0 xy,1 xz,2 yz*/, double a0, double a1, double b0, double b1, double k, int mat);
+int rt_obj_box(rt_graph* g, const double p0[3], const double p1[3], int mat);         /* box.cpp */
+int rt_obj_list(rt_graph* g, int n, const int* items);                                /* hittable_list */
+int rt_obj_bvh(rt_graph* g, int n, const int* items);                                 /* bvh_node(list, 0, 1) */
+int rt_obj_translate(rt_graph* g, int child, const double offset[3]);                 /* hittable.cpp:3-23 */
+int rt_obj_rotate_y(rt_graph* g, int child, double degrees);                          /* hittable.cpp:25-85 */
+int rt_obj_constant_medium(rt_graph* g, int boundary, double density, int tex);       /* constant_medium.h */
+int rt_graph_add_world(rt_graph* g, int obj);                                         /* world.add(obj) */
+int rt_graph_clear_world(rt_graph* g);
+int rt_graph_set_view(rt_graph* g, const double lookfrom[3], const double lookat[3], double vfov, double aperture,
+                      const double background[3]);
+/* Compiles the graph (flat SoA + SAH BVH) and uploads it to `device`.  The graph stays owned by the caller. */
+int rt_graph_compile(rt_graph* g, int device, rt_scene** out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ART_H */

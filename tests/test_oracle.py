@@ -1,0 +1,89 @@
+"""The oracle (oracle/restate.cpp) pinned against the reference's own outputs (tests/golden/, made by
+tests/golden/make_golden.py from the unmodified reference compiled in oracle/_ref)."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from tests.oracle_lib import REF_HARNESS, oracle_dump, oracle_kat, oracle_probe, oracle_render
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+SCENES = ["c1", "1", "2", "3", "4", "5", "6", "7", "8", "cow", "dino"]
+
+
+def test_mt19937_known_answers():
+    kat = json.load(open(os.path.join(GOLD, "kat.json")))["random_double"]
+    assert oracle_kat(len(kat)) == kat
+    assert kat[:3] == [0.1354770042967805, 0.8350085899945795, 0.96886777112423139]
+
+
+@pytest.mark.parametrize("scene", SCENES)
+def test_scene_build_consumes_the_reference_draws(scene):
+    gold = json.load(open(os.path.join(GOLD, "scenes.json")))[scene]
+    assert oracle_probe(scene, 8) == gold["probe"]
+
+
+@pytest.mark.parametrize("scene", SCENES)
+def test_scene_dump_is_the_reference_scene(scene):
+    gold = json.load(open(os.path.join(GOLD, "scenes.json")))[scene]
+    d = oracle_dump(scene).encode()
+    assert len(d) == gold["dump_len"]
+    assert hashlib.sha256(d).hexdigest() == gold["dump_sha256"]
+
+
+@pytest.mark.parametrize("scene", SCENES)
+def test_mt_render_bit_exact(scene):
+    g = np.load(os.path.join(GOLD, f"render_{scene}_64x36x4.npz"))
+    o = oracle_render(scene, 64, 36, 4, mode="mt")
+    assert o["segments"] == int(g["segments"])
+    assert np.array_equal(o["acc"], g["acc"])
+    assert np.array_equal(o["rgb"], g["rgb"])
+
+
+def test_config0_bit_exact():
+    """BASELINE configs[0]: 3-sphere scene, 400x225, 64 spp, the CPU reference path."""
+    g = np.load(os.path.join(GOLD, "render_c1_400x225x64.npz"))
+    o = oracle_render("c1", 400, 225, 64, mode="mt")
+    assert o["segments"] == int(g["segments"])
+    assert np.array_equal(o["rgb"], g["rgb"])
+    assert np.array_equal(o["acc"], g["acc"])
+
+
+def test_pcg_mode_is_independent_of_threads_and_rows():
+    full = oracle_render("1", 48, 30, 3, mode="pcg", threads=1)
+    many = oracle_render("1", 48, 30, 3, mode="pcg", threads=4)
+    assert np.array_equal(full["acc"], many["acc"]) and full["segments"] == many["segments"]
+    top = oracle_render("1", 48, 30, 3, mode="pcg", row0=0, nrows=13)
+    bot = oracle_render("1", 48, 30, 3, mode="pcg", row0=13, nrows=17)
+    assert np.array_equal(np.concatenate([top["acc"], bot["acc"]]), full["acc"])
+    assert top["segments"] + bot["segments"] == full["segments"]
+
+
+def test_pcg_seed_changes_the_estimate_not_the_mean():
+    a = oracle_render("c1", 40, 24, 32, mode="pcg", seed=1)
+    b = oracle_render("c1", 40, 24, 32, mode="pcg", seed=2)
+    ref = np.load(os.path.join(GOLD, "render_c1_400x225x64.npz"))
+    assert not np.array_equal(a["acc"], b["acc"])
+    assert abs(a["acc"].mean() - b["acc"].mean()) / a["acc"].mean() < 0.02
+    assert abs(a["segments"] / (40 * 24 * 32) - int(ref["segments"]) / (400 * 225 * 64)) < 0.05
+
+
+def test_max_depth_zero_is_black():
+    o = oracle_render("c1", 8, 6, 2, mode="pcg", max_depth=0)
+    assert o["segments"] == 0 and not o["acc"].any()
+
+
+@pytest.mark.skipif(not (os.path.exists(REF_HARNESS) and os.path.isdir("/root/reference/src")),
+                    reason="live reference harness only exists in the build container")
+@pytest.mark.parametrize("scene", ["c1", "1", "7", "8"])
+def test_live_reference_other_size(scene, tmp_path):
+    import subprocess
+    W, H, spp = 37, 23, 3
+    out = subprocess.run([REF_HARNESS, "render", scene, str(W), str(H), str(spp), str(tmp_path / "r")],
+                         capture_output=True, text=True, check=True)
+    info = json.loads(out.stdout.strip().splitlines()[-1])
+    o = oracle_render(scene, W, H, spp, mode="mt")
+    assert o["segments"] == info["segments"]
+    assert np.array_equal(o["rgb"], np.fromfile(tmp_path / "r.rgb", np.uint8).reshape(H, W, 3))
