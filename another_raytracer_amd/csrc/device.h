@@ -193,18 +193,20 @@ __device__ __forceinline__ bool hit_box(const BoxRec<R>& b, const Ray<R>& r, R t
     return any;
 }
 
-template <class R>
+// F (layout.h Feature bits) prunes the primitive kinds a scene cannot contain, so a kernel instantiated for a
+// spheres-only scene carries no triangle/box/transform/medium code and needs far fewer registers.
+template <class R, uint32_t F>
 __device__ __forceinline__ bool hit_prim(const DevScene<R>& S, uint32_t ref, const Ray<R>& r, R tmin, R tmax, R& t, uint32_t& face) {
     const uint32_t idx = primref_index(ref);
-    switch (primref_type(ref)) {
-        case PRIM_SPHERE: return hit_sphere(S.spheres[idx], r, tmin, tmax, t);
-        case PRIM_TRIANGLE: return hit_tri(S.tris[idx], r, tmin, tmax, t);
-        case PRIM_RECT: {
-            const RectRec<R>& q = S.rects[idx];
-            return hit_rect(static_cast<int>(q.axis), q.a0, q.a1, q.b0, q.b1, q.k, r, tmin, tmax, t);
-        }
-        default: return hit_box(S.boxes[idx], r, tmin, tmax, t, face);
+    const uint32_t type = primref_type(ref);
+    if ((F & F_SPHERE) && (F == F_SPHERE || type == PRIM_SPHERE)) return hit_sphere(S.spheres[idx], r, tmin, tmax, t);
+    if ((F & F_TRI) && (F == F_TRI || type == PRIM_TRIANGLE)) return hit_tri(S.tris[idx], r, tmin, tmax, t);
+    if ((F & F_RECT) && type == PRIM_RECT) {
+        const RectRec<R>& q = S.rects[idx];
+        return hit_rect(static_cast<int>(q.axis), q.a0, q.a1, q.b0, q.b1, q.k, r, tmin, tmax, t);
     }
+    if ((F & F_BOX) && type == PRIM_BOX) return hit_box(S.boxes[idx], r, tmin, tmax, t, face);
+    return false;
 }
 
 // ------------------------------------------------------------------------------------------------ BVH traversal
@@ -218,7 +220,7 @@ __device__ __forceinline__ float f_lo(float t) { return t * (1.0f - 2e-6f) - 1e-
 __device__ __forceinline__ float f_hi(double t) { return t == __builtin_inf() ? __builtin_inff() : static_cast<float>(t) * (1.0f + 2e-6f) + 1e-30f; }
 __device__ __forceinline__ float f_hi(float t) { return t * (1.0f + 2e-6f) + 1e-30f; }
 
-template <class R>
+template <class R, uint32_t F>
 __device__ __forceinline__ bool traverse(const DevScene<R>& S, int32_t root, const Ray<R>& r, R tmin, R tmax, int32_t* stk, R& t,
                                          uint32_t& prim, uint32_t& face) {
     const float ox = static_cast<float>(r.o.x), oy = static_cast<float>(r.o.y), oz = static_cast<float>(r.o.z);
@@ -264,7 +266,7 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, int32_t root, con
             const uint32_t ref = S.primrefs[first + k];
             R tt;
             uint32_t fc = 0;
-            if (hit_prim(S, ref, r, tmin, tmax, tt, fc)) {
+            if (hit_prim<R, F>(S, ref, r, tmin, tmax, tt, fc)) {
                 tmax = tt;
                 t = tt;
                 prim = ref;
@@ -295,33 +297,35 @@ __device__ __forceinline__ Ray<R> xform_in(const ObjRec<R>& o, const Ray<R>& r) 
 }
 
 // Any non-medium object: prim, BVH, or a translate/rotate_y chain (<= kMaxXformChain) over one of them.
-template <class R>
+template <class R, uint32_t F>
 __device__ __forceinline__ bool hit_object(const DevScene<R>& S, int32_t oi, Ray<R> r, R tmin, R tmax, int32_t* stk, R& t, uint32_t& prim,
                                            uint32_t& face) {
+    if (F & F_XFORM) {
 #pragma unroll
-    for (int c = 0; c < kMaxXformChain; ++c) {
-        const ObjRec<R>& o = S.objs[oi];
-        if (o.kind != OBJ_TRANSLATE && o.kind != OBJ_ROTATE_Y) break;
-        r = xform_in(o, r);
-        oi = o.a;
+        for (int c = 0; c < kMaxXformChain; ++c) {
+            const ObjRec<R>& o = S.objs[oi];
+            if (o.kind != OBJ_TRANSLATE && o.kind != OBJ_ROTATE_Y) break;
+            r = xform_in(o, r);
+            oi = o.a;
+        }
     }
     const ObjRec<R>& o = S.objs[oi];
     if (o.kind == OBJ_PRIM) {
         prim = static_cast<uint32_t>(o.a);
-        return hit_prim(S, prim, r, tmin, tmax, t, face);
+        return hit_prim<R, F>(S, prim, r, tmin, tmax, t, face);
     }
-    return traverse(S, o.a, r, tmin, tmax, stk, t, prim, face);
+    return traverse<R, F>(S, o.a, r, tmin, tmax, stk, t, prim, face);
 }
 
 // constant_medium.h:37-82.  Consumes one uniform when the clamped interval is non-empty.
-template <class R>
+template <class R, uint32_t F>
 __device__ __forceinline__ bool hit_medium(const DevScene<R>& S, const ObjRec<R>& m, const Ray<R>& r, R tmin, R tmax, int32_t* stk,
                                            uint64_t& rng, R& t) {
     const R inf = R(__builtin_inf());
     R t1, t2;
     uint32_t p, f;
-    if (!hit_object(S, m.a, r, -inf, inf, stk, t1, p, f)) return false;
-    if (!hit_object(S, m.a, r, t1 + R(0.0001), inf, stk, t2, p, f)) return false;
+    if (!hit_object<R, F>(S, m.a, r, -inf, inf, stk, t1, p, f)) return false;
+    if (!hit_object<R, F>(S, m.a, r, t1 + R(0.0001), inf, stk, t2, p, f)) return false;
     if (t1 < tmin) t1 = tmin;
     if (t2 > tmax) t2 = tmax;
     if (t1 >= t2) return false;
@@ -338,7 +342,7 @@ __device__ __forceinline__ bool hit_medium(const DevScene<R>& S, const ObjRec<R>
 struct HitOut {
     uint32_t prim, obj;  // obj: world slot | box face << 16
 };
-template <class R, bool MEDIA>
+template <class R, uint32_t F>
 __device__ __forceinline__ bool trace_world(const DevScene<R>& S, const Ray<R>& r, int32_t* stk, uint64_t& rng, R& t, HitOut& h) {
     R closest = R(__builtin_inf());
     bool any = false;
@@ -346,16 +350,16 @@ __device__ __forceinline__ bool trace_world(const DevScene<R>& S, const Ray<R>& 
         const int32_t oi = S.world[w];
         const ObjRec<R>& o = S.objs[oi];
         R tt;
-        if (MEDIA && o.kind == OBJ_MEDIUM) {
-            if (hit_medium(S, o, r, R(0.001), closest, stk, rng, tt)) {
+        if ((F & F_MEDIA) && o.kind == OBJ_MEDIUM) {
+            if (hit_medium<R, F>(S, o, r, R(0.001), closest, stk, rng, tt)) {
                 closest = tt;
                 any = true;
                 h.prim = kMediumHit;
                 h.obj = static_cast<uint32_t>(w);
             }
-        } else if (!MEDIA || o.kind != OBJ_MEDIUM) {
+        } else {
             uint32_t prim = 0, face = 0;
-            if (hit_object(S, oi, r, R(0.001), closest, stk, tt, prim, face)) {
+            if (hit_object<R, F>(S, oi, r, R(0.001), closest, stk, tt, prim, face)) {
                 closest = tt;
                 any = true;
                 h.prim = prim;
@@ -392,10 +396,11 @@ __device__ __forceinline__ void rect_surface(Surf<R>& s, int axis, R a0, R a1, R
     set_face_normal(s, r, n);
     s.p = r.at(t);
 }
-template <class R>
+template <class R, uint32_t F, bool UV = true>
 __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref, uint32_t face, const Ray<R>& r, R t, Surf<R>& s) {
     const uint32_t idx = primref_index(ref);
-    switch (primref_type(ref)) {
+    const uint32_t type = (F == F_SPHERE) ? PRIM_SPHERE : primref_type(ref);
+    switch (type) {
         case PRIM_SPHERE: {  // sphere.h:57-63, :24-37
             const SphereRec<R>& sp = S.spheres[idx];
             V3<R> center = ld3(sp.c);
@@ -404,7 +409,8 @@ __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref,
             s.p = r.at(t);
             const V3<R> outward = divs(s.p - center, sp.r);
             set_face_normal(s, r, outward);
-            if (!moving) {
+            // u,v only feed image textures: acos/atan2 are skipped for materials that never sample them
+            if (UV && !moving && (S.mats[sp.mat].flags & MATF_NEEDS_UV)) {
                 const R pi = R(3.1415926535897932385);
                 const R theta = acos(-outward.y);
                 const R phi = atan2(-outward.z, outward.x) + pi;
@@ -418,6 +424,7 @@ __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref,
             break;
         }
         case PRIM_TRIANGLE: {  // triangle.h:57-85
+            if (!(F & F_TRI)) break;
             const TriRec<R>& tr = S.tris[idx];
             const V3<R> p1 = ld3(tr.p), p2 = ld3(tr.p + 3), p3 = ld3(tr.p + 6);
             const V3<R> N = cross(p2 - p1, p3 - p1);
@@ -432,12 +439,14 @@ __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref,
             break;
         }
         case PRIM_RECT: {
+            if (!(F & F_RECT)) break;
             const RectRec<R>& q = S.rects[idx];
             rect_surface(s, static_cast<int>(q.axis), q.a0, q.a1, q.b0, q.b1, q.k, r, t);
             s.mat = q.mat;
             break;
         }
         default: {
+            if (!(F & F_BOX)) break;
             const BoxRec<R>& b = S.boxes[idx];
             int axis;
             R a0, a1, b0, b1, k;
@@ -451,11 +460,11 @@ __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref,
 
 // Rebuilds the hit_record of the world object that won (transform chain unwound as translate::hit / rotate_y::hit
 // do it: hittable.cpp:7-11, :72-84, including set_face_normal against the transformed ray).
-template <class R>
+template <class R, uint32_t F, bool UV = true>
 __device__ __forceinline__ void world_surface(const DevScene<R>& S, const HitOut& h, const Ray<R>& r, R t, Surf<R>& s) {
     const int32_t w = static_cast<int32_t>(h.obj & 0xFFFFu);
     int32_t oi = S.world[w];
-    if (h.prim == kMediumHit) {  // constant_medium.h:75-79
+    if ((F & F_MEDIA) && h.prim == kMediumHit) {  // constant_medium.h:75-79
         s.p = r.at(t);
         s.n = mk(R(1), R(0), R(0));
         s.ff = true;
@@ -467,7 +476,7 @@ __device__ __forceinline__ void world_surface(const DevScene<R>& S, const HitOut
     static_assert(kMaxXformChain == 2, "world_surface unwinds at most two transforms");
     int32_t o0 = -1, o1 = -1;
     Ray<R> r1 = r, r2 = r;
-    {
+    if (F & F_XFORM) {
         const ObjRec<R>& o = S.objs[oi];
         if (o.kind == OBJ_TRANSLATE || o.kind == OBJ_ROTATE_Y) {
             o0 = oi;
@@ -483,7 +492,8 @@ __device__ __forceinline__ void world_surface(const DevScene<R>& S, const HitOut
             }
         }
     }
-    prim_surface(S, h.prim, h.obj >> 16, r2, t, s);
+    prim_surface<R, F, UV>(S, h.prim, h.obj >> 16, r2, t, s);
+    if (!(F & F_XFORM)) return;
     auto unwind = [&](int32_t xo, const Ray<R>& inner) {
         const ObjRec<R>& o = S.objs[xo];
         if (o.kind == OBJ_TRANSLATE) {
@@ -538,28 +548,44 @@ __device__ __forceinline__ V3<R> image_value(const DevScene<R>& S, int32_t im, R
     const uint8_t* px = S.texels + I.offset + static_cast<uint64_t>(j) * static_cast<uint64_t>(I.bpp * I.w) + static_cast<uint64_t>(i) * I.bpp;
     return mk(cs * R(px[0]), cs * R(px[1]), cs * R(px[2]));
 }
+// checker_texture (texture.h:41-48): sin(10x)*sin(10y)*sin(10z) < 0.  Only the SIGN of the product matters, so it
+// is evaluated as a sign parity: sin(y) == 0 exactly iff y == 0 for doubles (pi is irrational), and for y != 0
+// sin(y) < 0 iff floor(y / pi) is odd.  Same predicate as the reference's, without the Payne-Hanek reduction of a
+// full f64 sin (46 VGPRs in the shade kernel); it can only differ when y is within ~1 ulp of a multiple of pi.
 template <class R>
-__device__ __forceinline__ V3<R> tex_value(const DevScene<R>& S, int32_t ti, R u, R v, V3<R> p) {  // rendering/texture.h
+__device__ __forceinline__ int sin_sign(R y) {
+    if (y == R(0)) return 0;
+    const R k = floor(y * R(0.31830988618379067154));
+    const long long ki = static_cast<long long>(k);
+    return (ki & 1) ? -1 : 1;
+}
+template <class R>
+__device__ __forceinline__ bool checker_odd(V3<R> p) {
+    const int a = sin_sign(R(10) * p.x), b = sin_sign(R(10) * p.y), c = sin_sign(R(10) * p.z);
+    return a * b * c < 0;
+}
+
+// rendering/texture.h.  TF (layout.h TexFeature bits) prunes the texture kinds a scene cannot contain.
+template <class R, uint32_t TF = TF_ALL>
+__device__ __forceinline__ V3<R> tex_value(const DevScene<R>& S, int32_t ti, R u, R v, V3<R> p) {
     for (int level = 0; level < 4; ++level) {
         const TexRec<R>& t = S.texs[ti];
-        switch (t.type) {
-            case TEX_SOLID: return ld3(t.c);
-            case TEX_CHECKER: {
-                const R sines = sin(R(10) * p.x) * sin(R(10) * p.y) * sin(R(10) * p.z);
-                ti = sines < R(0) ? t.odd : t.even;
-                continue;
-            }
-            case TEX_NOISE: {
-                const R n = perlin_noise(S.perlins[t.perlin], t.scale * p);
-                const R h = (R(1) + n) * R(0.5);
-                return mk(h, h, h);
-            }
-            case TEX_IMAGE: return image_value(S, t.image, u, v);
-            default: {
-                const R w = R(1) - u - v;
-                return image_value(S, t.image, u * t.uv[0] + v * t.uv[2] + w * t.uv[4], u * t.uv[1] + v * t.uv[3] + w * t.uv[5]);
-            }
+        if (TF == TF_SOLID || t.type == TEX_SOLID) return ld3(t.c);
+        if ((TF & TF_CHECKER) && t.type == TEX_CHECKER) {
+            ti = checker_odd(p) ? t.odd : t.even;
+            continue;
         }
+        if ((TF & TF_NOISE) && t.type == TEX_NOISE) {
+            const R n = perlin_noise(S.perlins[t.perlin], t.scale * p);
+            const R h = (R(1) + n) * R(0.5);
+            return mk(h, h, h);
+        }
+        if ((TF & TF_IMAGE) && t.type == TEX_IMAGE) return image_value(S, t.image, u, v);
+        if ((TF & TF_IMAGE) && t.type == TEX_BARY_IMAGE) {
+            const R w = R(1) - u - v;
+            return image_value(S, t.image, u * t.uv[0] + v * t.uv[2] + w * t.uv[4], u * t.uv[1] + v * t.uv[3] + w * t.uv[5]);
+        }
+        break;
     }
     return mk(R(0), R(1), R(1));
 }

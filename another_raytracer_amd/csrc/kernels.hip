@@ -3,18 +3,22 @@
 // The reference's recursive integrator (engine.h:58-68 _stochastic_sample + engine.h:447-466 _ray_color) is
 // flattened into an iterative per-ray wavefront loop over a pool of P = k * npix paths (k samples of every local
 // pixel per pass).  Per pass:
-//   k_gen                      camera rays for every (pixel, sample) slot; PCG32 keyed by (seed, pixel, sample)
 //   for depth d < max_depth:
-//     k_extend<R, MEDIA>       closest hit over the world list (LDS-stack BVH traversal, f32 boxes, R leaf tests),
+//     k_extend<R, F>           closest hit over the world list (LDS-stack BVH traversal, f32 boxes, R leaf tests);
+//                              at depth 0 it first generates the camera ray of every (pixel, sample) slot itself
+//                              (PCG32 keyed by (seed, pixel, sample)); F = the scene's feature subset (layout.h),
 //                              misses finish their path (L += T*background); hits are appended to one of five
 //                              material queues (branch sorting for the shade stage)
-//     k_shade<R>               per material queue: emitted + scatter; survivors go to the next active queue
+//     k_shade<R, F, M, TF>     one launch per material type M present: emitted + scatter on that material's queue
+//                              (branch-sorted shading); survivors go to the next active queue
 //   k_accum                    adds the k per-slot radiances into the f64 pixel sums in sample order
-// then k_finalize (write_color, color.h:6-22).  All queue sizes live on the device; extend/shade are persistent
-// grids whose waves claim 64 items at a time from an atomic counter, so no host round trip happens inside a render.
+// then k_finalize (write_color, color.h:6-22).  All queue sizes live on the device: extend/shade are persistent
+// grids walking their input in a static grid-stride order, and appends go to kShards-way sharded queues, so no
+// host round trip and no hot atomic word exists inside a render (see "work distribution").
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <functional>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -33,19 +37,17 @@ namespace art {
         if (e_ != hipSuccess) throw std::runtime_error(std::string(#x) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
-// Per-(pass, depth) counter block.
-constexpr int kCStride = 8;  // [0] active queue size, [1] extend claim, [2] shade claim, [3..7] material queue sizes
-constexpr int kCQueue = 0, kCExtGrab = 1, kCShadeGrab = 2, kCMat = 3;
-
 // ------------------------------------------------------------------------------------------------ path records
 // One path = one AoS record so that a lane touching a scattered slot reads whole cache lines:
-//   f32: 64 B = {o.xyz, time} {d.xyz, -} {T.rgb, L.r} {L.gb, rng}       f64: 128 B, same fields.
+//   f32: 64 B = {o.xyz, time} {d.xyz, -} {T.rgb, L.r} {L.gb, rng}
+//   f64: 128 B = line 0 {o.xyz, d.xyz, time, rng} (all extend reads) + line 1 {T.rgb, L.rgb}
 template <class R> struct PathRec;
 template <> struct PathRec<float> {
     float4 ot, d, tl, lr;
 };
 template <> struct PathRec<double> {
-    double2 a, b, c, e, f, g, h, i;  // (ox,oy) (oz,tm) (dx,dy) (dz,-) (Tr,Tg) (Tb,Lr) (Lg,Lb) (rng,-)
+    double2 a, b, c, e;  // line 0: (ox,oy) (oz,dx) (dy,dz) (tm,rng)
+    double2 f, g, h, i;  // line 1: (Tr,Tg) (Tb,Lr) (Lg,Lb) (-,-)
 };
 template <class R>
 struct PathState {
@@ -80,11 +82,11 @@ __device__ __forceinline__ void store_rng(PathRec<float>* P, uint32_t q, uint64_
 }
 __device__ __forceinline__ void load_path(const PathRec<double>* P, uint32_t q, PathState<double>& s, bool full) {
     const PathRec<double>& p = P[q];
-    const double2 a = p.a, b = p.b, c = p.c, e = p.e, i = p.i;
+    const double2 a = p.a, b = p.b, c = p.c, e = p.e;
     s.ray.o = mk(a.x, a.y, b.x);
-    s.ray.tm = b.y;
-    s.ray.d = mk(c.x, c.y, e.x);
-    s.rng = static_cast<uint64_t>(__double_as_longlong(i.x));
+    s.ray.d = mk(b.y, c.x, c.y);
+    s.ray.tm = e.x;
+    s.rng = static_cast<uint64_t>(__double_as_longlong(e.y));
     if (full) {
         const double2 f = p.f, g = p.g, h = p.h;
         s.T = mk(f.x, f.y, g.x);
@@ -94,16 +96,15 @@ __device__ __forceinline__ void load_path(const PathRec<double>* P, uint32_t q, 
 __device__ __forceinline__ void store_path(PathRec<double>* P, uint32_t q, const PathState<double>& s) {
     PathRec<double>& p = P[q];
     p.a = make_double2(s.ray.o.x, s.ray.o.y);
-    p.b = make_double2(s.ray.o.z, s.ray.tm);
-    p.c = make_double2(s.ray.d.x, s.ray.d.y);
-    p.e = make_double2(s.ray.d.z, 0.0);
+    p.b = make_double2(s.ray.o.z, s.ray.d.x);
+    p.c = make_double2(s.ray.d.y, s.ray.d.z);
+    p.e = make_double2(s.ray.tm, __longlong_as_double(static_cast<long long>(s.rng)));
     p.f = make_double2(s.T.x, s.T.y);
     p.g = make_double2(s.T.z, s.L.x);
     p.h = make_double2(s.L.y, s.L.z);
-    p.i = make_double2(__longlong_as_double(static_cast<long long>(s.rng)), 0.0);
 }
 __device__ __forceinline__ void store_rng(PathRec<double>* P, uint32_t q, uint64_t rng) {
-    P[q].i.x = __longlong_as_double(static_cast<long long>(rng));
+    P[q].e.y = __longlong_as_double(static_cast<long long>(rng));
 }
 
 template <class R>
@@ -133,7 +134,19 @@ __device__ __forceinline__ void load_res(const ResRec<double>* res, uint32_t q, 
     r = a.x; g = a.y; b = c.x;
 }
 
-// ------------------------------------------------------------------------------------------------ launch arguments
+// ------------------------------------------------------------------------------------------------ work distribution
+// Queues are split into kShards shards, each with its own counter on its own 128-B line.  Persistent waves take
+// 64-item batches in a static grid-stride order (no claim atomic) and a wave appends only to shard
+// (global wave id % kShards): one returning atomic per wave and queue, spread over kShards words instead of one
+// (a single word saturates at ~88 atomics/us, MI355X_MICROARCH.md "dequeue").  Static assignment also bounds every
+// shard: shard s only receives outputs of the batches b with b % kShards == s, so kShardCap(P) slots suffice.
+constexpr int kShards = 32;
+constexpr int kCounterStride = 32;                   // words between counters (128 B)
+constexpr int kQueueKinds = 1 + kNumMatTypes;        // 0: active (extend input), 1..5: material queues
+constexpr int kMatSegs = kNumMatTypes * kShards;     // shade input segments
+// + 2 batches per material kernel: the kNumMatTypes shade launches of one depth all append to the same next-queue shards
+__host__ __device__ inline uint32_t shard_cap(uint32_t P) { return 64u * ((((P + 63u) / 64u) + kShards - 1) / kShards + 2 * kNumMatTypes); }
+
 struct PassGeom {
     int32_t W, H;               // full image
     int32_t rows;               // local rows
@@ -141,7 +154,9 @@ struct PassGeom {
     uint32_t tiles_x, npix_pad; // 8x8 tiles over (W x rows)
     uint32_t k;                 // samples in this pass
     uint32_t sample_base;       // first sample index of the pass
-    uint32_t P;                 // k * npix_pad
+    uint32_t P;                 // k * npix_pad path slots
+    uint32_t cap;               // shard capacity
+    uint32_t live;              // k * rows * W: slots that are real pixels (depth-0 segments)
     int32_t max_depth;
     uint64_t seed;
 };
@@ -150,11 +165,16 @@ struct Work {
     PathRec<R>* paths;
     HitRecD<R>* hits;
     ResRec<R>* res;
-    uint32_t* queue[2];
-    uint32_t* mq[kNumMatTypes];
-    uint32_t* counters;  // this pass's block: (max_depth + 1) * kCStride
-    double* acc;         // local pixels * 3
+    uint32_t* active[2];        // extend input of depth d: active[d & 1], kShards x cap
+    uint32_t* mq;               // material queues: (m * kShards + s) * cap
+    uint32_t* counters;         // [(depth * kQueueKinds + kind) * kShards + shard] * kCounterStride
+    unsigned long long* segments;
+    double* acc;                // local pixels * 3
 };
+template <class R>
+__device__ __forceinline__ uint32_t* counter(const Work<R>& w, int d, int kind, int s) {
+    return w.counters + (static_cast<size_t>((d * kQueueKinds + kind) * kShards + s)) * kCounterStride;
+}
 
 __device__ __forceinline__ int global_row(const PassGeom& g, int ly) {  // row-interleaved band partition
     return (ly / g.band_rows) * (g.band_rows * g.band_count) + g.band_index * g.band_rows + (ly % g.band_rows);
@@ -166,96 +186,126 @@ __device__ __forceinline__ bool slot_pixel(const PassGeom& g, uint32_t qi, int& 
     return lx < g.W && ly < g.rows;
 }
 
-// Wave-aggregated append: one atomic per wave, lanes write in lane order.
-__device__ __forceinline__ void wave_append(bool pred, uint32_t val, uint32_t* queue, uint32_t* counter) {
+// Wave-aggregated append to one shard: one atomic per wave, lanes write in lane order.
+__device__ __forceinline__ void wave_append(bool pred, uint32_t val, uint32_t* shard_buf, uint32_t* ctr) {
     const uint64_t mask = __ballot(pred);
     if (mask == 0) return;
-    const uint32_t lane = __lane_id();
     const int leader = __ffsll(static_cast<long long>(mask)) - 1;
     uint32_t base = 0;
-    if (static_cast<int>(lane) == leader) base = atomicAdd(counter, static_cast<uint32_t>(__popcll(mask)));
+    if (static_cast<int>(__lane_id()) == leader) base = atomicAdd(ctr, static_cast<uint32_t>(__popcll(mask)));
     base = __shfl(base, leader);
     if (pred) {
         const uint32_t off = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(mask >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(mask), 0u));
-        queue[base + off] = val;
+        shard_buf[base + off] = val;
     }
 }
-__device__ __forceinline__ uint32_t wave_claim(uint32_t* counter) {
-    uint32_t base = 0;
-    if (__lane_id() == 0) base = atomicAdd(counter, 64u);
-    return __shfl(base, 0);
+
+// Block-wide exclusive prefix of n <= kBlock shard counts into pre[0..n] (pre[n] = total).
+__device__ __forceinline__ void block_prefix(uint32_t* pre, int n, uint32_t v) {
+    const int t = threadIdx.x;
+    pre[t] = t < n ? v : 0u;
+    __syncthreads();
+    for (int off = 1; off < kBlock; off <<= 1) {
+        const uint32_t x = t >= off ? pre[t - off] : 0u;
+        __syncthreads();
+        pre[t] += x;
+        __syncthreads();
+    }
+    // inclusive -> exclusive, shifted by one: pre[i] = sum of the first i counts
+    const uint32_t inc = pre[t];
+    __syncthreads();
+    if (t < n) pre[t + 1] = inc;
+    if (t == 0) pre[0] = 0u;
+    __syncthreads();
+}
+// Segment of item i: largest s with pre[s] <= i (pre strictly describes n segments).
+__device__ __forceinline__ int find_segment(const uint32_t* pre, int n, uint32_t i) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (pre[mid] <= i) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
 }
 
 // ------------------------------------------------------------------------------------------------ kernels
-// engine.h:58-68 + camera.h:38-47 for one slot.
+// engine.h:58-68 + camera.h:38-47 for slot q (sample j = q / npix_pad of the pass, pixel from the 8x8 tile order).
+// Runs inside the depth-0 extend: the camera ray never round-trips through HBM.
 template <class R>
-__global__ __launch_bounds__(256) void k_gen(PassGeom g, CameraRec<R> cam, Work<R> w) {
-    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-    bool live = false;
-    if (q < g.P) {
-        const uint32_t j = q / g.npix_pad;
-        const uint32_t qi = q - j * g.npix_pad;
-        int lx, ly;
-        if (j < g.k && slot_pixel(g, qi, lx, ly)) {
-            const int gy = global_row(g, ly);
-            const uint32_t pixel = static_cast<uint32_t>(gy) * static_cast<uint32_t>(g.W) + static_cast<uint32_t>(lx);
-            uint64_t rng = pcg_seed(g.seed, pixel, g.sample_base + j);
-            const R ru = uniform<R>(rng);
-            const R rv = uniform<R>(rng);
-            const R s = (R(lx) + ru) / R(g.W - 1);
-            const R t = (R(g.H - 1 - gy) + rv) / R(g.H - 1);
-            V3<R> p;
-            for (;;) {  // random_in_unit_disk (vec3.h:137-143): x, then y
-                p.x = uniform<R>(rng, R(-1), R(1));
-                p.y = uniform<R>(rng, R(-1), R(1));
-                p.z = R(0);
-                if (len2(p) >= R(1)) continue;
-                break;
-            }
-            const V3<R> rd = cam.lens_radius * p;
-            const V3<R> offset = rd.x * ld3(cam.u) + rd.y * ld3(cam.v);
-            PathState<R> st;
-            st.ray.o = ld3(cam.origin) + offset;
-            st.ray.d = ld3(cam.llc) + s * ld3(cam.horizontal) + t * ld3(cam.vertical) - ld3(cam.origin) - offset;
-            st.ray.tm = uniform<R>(rng, cam.time0, cam.time1);
-            st.T = mk(R(1), R(1), R(1));
-            st.L = mk(R(0), R(0), R(0));
-            st.rng = rng;
-            if (g.max_depth > 0) {
-                store_path(w.paths, q, st);
-                live = true;
-            } else {
-                store_res(w.res, q, st.L);
-            }
-        }
+__device__ __forceinline__ void gen_ray(const PassGeom& g, const CameraRec<R>& cam, uint32_t q, int lx, int ly, PathState<R>& st) {
+    const uint32_t j = q / g.npix_pad;
+    const int gy = global_row(g, ly);
+    const uint32_t pixel = static_cast<uint32_t>(gy) * static_cast<uint32_t>(g.W) + static_cast<uint32_t>(lx);
+    uint64_t rng = pcg_seed(g.seed, pixel, g.sample_base + j);
+    const R ru = uniform<R>(rng);
+    const R rv = uniform<R>(rng);
+    const R s = (R(lx) + ru) / R(g.W - 1);
+    const R t = (R(g.H - 1 - gy) + rv) / R(g.H - 1);
+    V3<R> p;
+    for (;;) {  // random_in_unit_disk (vec3.h:137-143): x, then y
+        p.x = uniform<R>(rng, R(-1), R(1));
+        p.y = uniform<R>(rng, R(-1), R(1));
+        p.z = R(0);
+        if (len2(p) >= R(1)) continue;
+        break;
     }
-    wave_append(live, q, w.queue[0], &w.counters[kCQueue]);
+    const V3<R> rd = cam.lens_radius * p;
+    const V3<R> offset = rd.x * ld3(cam.u) + rd.y * ld3(cam.v);
+    st.ray.o = ld3(cam.origin) + offset;
+    st.ray.d = ld3(cam.llc) + s * ld3(cam.horizontal) + t * ld3(cam.vertical) - ld3(cam.origin) - offset;
+    st.ray.tm = uniform<R>(rng, cam.time0, cam.time1);
+    st.T = mk(R(1), R(1), R(1));
+    st.L = mk(R(0), R(0), R(0));
+    st.rng = rng;
 }
 
-template <class R, bool MEDIA>
-__global__ __launch_bounds__(kBlock) void k_extend(DevScene<R> S, Work<R> w, int d) {
+template <class R, uint32_t F>
+__global__ __launch_bounds__(kBlock) void k_extend(DevScene<R> S, PassGeom g, CameraRec<R> cam, Work<R> w, int d) {
     __shared__ int32_t stack[kStackDepth * kBlock];
+    __shared__ uint32_t pre[kBlock + 1];
     int32_t* stk = stack + threadIdx.x;
-    uint32_t* cnt = w.counters + d * kCStride;
-    const uint32_t count = __hip_atomic_load(&cnt[kCQueue], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t* queue = w.queue[d & 1];
-    for (;;) {
-        const uint32_t base = wave_claim(&cnt[kCExtGrab]);
-        if (base >= count) break;
-        const uint32_t i = base + __lane_id();
+    // input: depth 0 = every slot (identity; padding slots are skipped), deeper = the kShards active shards
+    uint32_t count;
+    if (d == 0) {
+        count = g.P;
+    } else {
+        block_prefix(pre, kShards, threadIdx.x < kShards ? *counter(w, d, 0, threadIdx.x) : 0u);
+        count = pre[kShards];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(w.segments, static_cast<unsigned long long>(d == 0 ? g.live : count));
+    const uint32_t* in = w.active[d & 1];
+    const uint32_t wave = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const uint32_t nwaves = gridDim.x * (kBlock / 64);
+    const int shard = static_cast<int>(wave % kShards);
+    for (uint32_t b = wave; b * 64u < count; b += nwaves) {
+        const uint32_t i = b * 64u + __lane_id();
         int mtype = -1;
         uint32_t q = 0;
-        if (i < count) {
-            q = queue[i];
-            PathState<R> st;
-            load_path(w.paths, q, st, false);
+        bool live = i < count;
+        PathState<R> st;
+        if (live) {
+            if (d == 0) {
+                q = i;
+                int lx, ly;
+                live = slot_pixel(g, i % g.npix_pad, lx, ly);
+                if (live) gen_ray(g, cam, q, lx, ly, st);
+            } else {
+                const int s = find_segment(pre, kShards, i);
+                q = in[s * g.cap + (i - pre[s])];
+                load_path(w.paths, q, st, false);
+            }
+        }
+        if (live) {
             R t;
             HitOut h{0, 0};
-            if (trace_world<R, MEDIA>(S, st.ray, stk, st.rng, t, h)) {
+            if (trace_world<R, F>(S, st.ray, stk, st.rng, t, h)) {
                 w.hits[q] = HitRecD<R>{t, h.prim, h.obj};
                 uint32_t m;
-                if (h.prim == kMediumHit) {
+                if ((F & F_MEDIA) && h.prim == kMediumHit) {
                     m = static_cast<uint32_t>(S.objs[S.world[h.obj & 0xFFFFu]].b);
+                } else if (F == F_SPHERE) {
+                    m = S.spheres[primref_index(h.prim)].mat;
                 } else {
                     const uint32_t idx = primref_index(h.prim);
                     switch (primref_type(h.prim)) {
@@ -266,98 +316,88 @@ __global__ __launch_bounds__(kBlock) void k_extend(DevScene<R> S, Work<R> w, int
                     }
                 }
                 mtype = static_cast<int>(S.mats[m].type);
-                if (MEDIA) store_rng(w.paths, q, st.rng);
+                if (d == 0) store_path(w.paths, q, st);
+                else if (F & F_MEDIA) store_rng(w.paths, q, st.rng);
             } else {  // engine.h:455-456: miss -> background
-                load_path(w.paths, q, st, true);
+                if (d != 0) load_path(w.paths, q, st, true);
                 st.L = st.L + st.T * mk(S.bg[0], S.bg[1], S.bg[2]);
                 store_res(w.res, q, st.L);
             }
         }
 #pragma unroll
-        for (int m = 0; m < kNumMatTypes; ++m) wave_append(mtype == m, q, w.mq[m], &cnt[kCMat + m]);
+        for (int m = 0; m < kNumMatTypes; ++m)
+            wave_append(mtype == m, q, w.mq + static_cast<size_t>(m * kShards + shard) * g.cap, counter(w, d, 1 + m, shard));
     }
 }
 
-// material.h scatter() + emitted() for one hit; returns false when the path ends here.
-template <class R>
+// material.h scatter() for one hit of material type M (compile time: one shade kernel per material type, so a wave
+// never carries another material's code or registers); returns false when the path ends here.
+template <class R, uint32_t M, uint32_t TF>
 __device__ __forceinline__ bool scatter(const DevScene<R>& S, const MatRec<R>& m, const Surf<R>& s, PathState<R>& st, V3<R>& att, V3<R>& dir) {
-    switch (m.type) {
-        case MAT_LAMBERTIAN: {  // material.h:20-43
-            const V3<R> rv = unit(in_unit_sphere<R>(st.rng));
-            dir = s.n + rv;
-            if (near_zero(dir)) dir = s.n;
-            att = tex_value(S, m.tex, s.u, s.v, s.p);
-            return true;
+    if (M == MAT_LAMBERTIAN) {  // material.h:20-43
+        const V3<R> rv = unit(in_unit_sphere<R>(st.rng));
+        dir = s.n + rv;
+        if (near_zero(dir)) dir = s.n;
+        att = tex_value<R, TF>(S, m.tex, s.u, s.v, s.p);
+        return true;
+    } else if (M == MAT_METAL) {  // material.h:45-61
+        const V3<R> reflected = reflect(unit(st.ray.d), s.n);
+        dir = reflected + m.fuzz * in_unit_sphere<R>(st.rng);
+        att = ld3(m.albedo);
+        return dot(dir, s.n) > R(0);
+    } else if (M == MAT_DIELECTRIC) {  // material.h:63-99
+        att = mk(R(1), R(1), R(1));
+        const R ratio = s.ff ? (R(1) / m.ir) : m.ir;
+        const V3<R> ud = unit(st.ray.d);
+        const R cos_theta = fmin(dot(-ud, s.n), R(1));
+        const R sin_theta = sqrt(R(1) - cos_theta * cos_theta);
+        const bool cannot = ratio * sin_theta > R(1);
+        bool refl = cannot;
+        if (!cannot) {
+            R r0 = (R(1) - ratio) / (R(1) + ratio);
+            r0 = r0 * r0;
+            const R refl_p = r0 + (R(1) - r0) * pow((R(1) - cos_theta), R(5));
+            refl = refl_p > uniform<R>(st.rng);
         }
-        case MAT_METAL: {  // material.h:45-61
-            const V3<R> reflected = reflect(unit(st.ray.d), s.n);
-            dir = reflected + m.fuzz * in_unit_sphere<R>(st.rng);
-            att = ld3(m.albedo);
-            return dot(dir, s.n) > R(0);
-        }
-        case MAT_DIELECTRIC: {  // material.h:63-99
-            att = mk(R(1), R(1), R(1));
-            const R ratio = s.ff ? (R(1) / m.ir) : m.ir;
-            const V3<R> ud = unit(st.ray.d);
-            const R cos_theta = fmin(dot(-ud, s.n), R(1));
-            const R sin_theta = sqrt(R(1) - cos_theta * cos_theta);
-            const bool cannot = ratio * sin_theta > R(1);
-            bool refl = cannot;
-            if (!cannot) {
-                R r0 = (R(1) - ratio) / (R(1) + ratio);
-                r0 = r0 * r0;
-                const R refl_p = r0 + (R(1) - r0) * pow((R(1) - cos_theta), R(5));
-                refl = refl_p > uniform<R>(st.rng);
-            }
-            dir = refl ? reflect(ud, s.n) : refract(ud, s.n, ratio);
-            return true;
-        }
-        case MAT_ISOTROPIC: {  // material.h:120-135
-            dir = in_unit_sphere<R>(st.rng);
-            att = tex_value(S, m.tex, s.u, s.v, s.p);
-            return true;
-        }
-        default: return false;  // diffuse_light
+        dir = refl ? reflect(ud, s.n) : refract(ud, s.n, ratio);
+        return true;
+    } else if (M == MAT_ISOTROPIC) {  // material.h:120-135
+        dir = in_unit_sphere<R>(st.rng);
+        att = tex_value<R, TF>(S, m.tex, s.u, s.v, s.p);
+        return true;
     }
+    return false;  // diffuse_light (material.h:106-110)
 }
 
-template <class R>
-__global__ __launch_bounds__(kBlock) void k_shade(DevScene<R> S, Work<R> w, int d, int max_depth) {
-    uint32_t* cnt = w.counters + d * kCStride;
-    uint32_t pre[kNumMatTypes + 1];
-    pre[0] = 0;
-#pragma unroll
-    for (int m = 0; m < kNumMatTypes; ++m) pre[m + 1] = pre[m] + __hip_atomic_load(&cnt[kCMat + m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t total = pre[kNumMatTypes];
-    uint32_t* next_q = w.queue[(d + 1) & 1];
-    uint32_t* next_cnt = w.counters + (d + 1) * kCStride + kCQueue;
-    const bool last = d + 1 >= max_depth;
-    for (;;) {
-        const uint32_t base = wave_claim(&cnt[kCShadeGrab]);
-        if (base >= total) break;
-        const uint32_t i = base + __lane_id();
+// Input: the kShards shards of material queue M at depth d (the extend stage sorted hits by material type).
+template <class R, uint32_t F, uint32_t M, uint32_t TF>
+__global__ __launch_bounds__(kBlock) void k_shade(DevScene<R> S, PassGeom g, Work<R> w, int d) {
+    __shared__ uint32_t pre[kBlock + 1];
+    block_prefix(pre, kShards, threadIdx.x < kShards ? *counter(w, d, 1 + static_cast<int>(M), threadIdx.x) : 0u);
+    const uint32_t total = pre[kShards];
+    const uint32_t* in = w.mq + static_cast<size_t>(M) * kShards * g.cap;
+    const bool last = d + 1 >= g.max_depth;
+    uint32_t* next = w.active[(d + 1) & 1];
+    const uint32_t wave = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const uint32_t nwaves = gridDim.x * (kBlock / 64);
+    const int shard = static_cast<int>(wave % kShards);
+    for (uint32_t b = wave; b * 64u < total; b += nwaves) {
+        const uint32_t i = b * 64u + __lane_id();
         bool cont = false;
         uint32_t q = 0;
         if (i < total) {
-            const uint32_t* mq = w.mq[0];
-            uint32_t first = 0;
-#pragma unroll
-            for (int k = 1; k < kNumMatTypes; ++k)
-                if (i >= pre[k]) {
-                    mq = w.mq[k];
-                    first = pre[k];
-                }
-            q = mq[i - first];
+            const int sg = find_segment(pre, kShards, i);
+            q = in[static_cast<size_t>(sg) * g.cap + (i - pre[sg])];
             PathState<R> st;
             load_path(w.paths, q, st, true);
             const HitRecD<R> h = w.hits[q];
             Surf<R> s;
-            world_surface(S, HitOut{h.prim, h.obj}, st.ray, h.t, s);
+            world_surface<R, F, (TF & TF_IMAGE) != 0>(S, HitOut{h.prim, h.obj}, st.ray, h.t, s);
             const MatRec<R>& mat = S.mats[s.mat];
-            if (mat.type == MAT_LIGHT) st.L = st.L + st.T * tex_value(S, mat.tex, s.u, s.v, s.p);  // material.h:114-116
-            if (!last) {
+            if (M == MAT_LIGHT) st.L = st.L + st.T * tex_value<R, TF>(S, mat.tex, s.u, s.v, s.p);  // material.h:114-116
+            if (M != MAT_LIGHT && !last) {
                 V3<R> att, dir;
-                if (scatter(S, mat, s, st, att, dir)) {
+                if (scatter<R, M, TF>(S, mat, s, st, att, dir)) {
                     st.T = st.T * att;
                     st.ray.o = s.p;
                     st.ray.d = dir;
@@ -367,7 +407,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(DevScene<R> S, Work<R> w, int 
             }
             if (!cont) store_res(w.res, q, st.L);
         }
-        wave_append(cont, q, next_q, next_cnt);
+        wave_append(cont, q, next + static_cast<size_t>(shard) * g.cap, counter(w, d + 1, 0, shard));
     }
 }
 
@@ -409,6 +449,9 @@ struct DeviceScene {
     std::vector<void*> allocs;
     DevScene<R> view{};
     bool media = false;
+    uint32_t features = F_ALL;
+    uint32_t mat_types = (1u << kNumMatTypes) - 1;  // bit m: some material of type m exists
+    bool tex_basic = false;                          // only solid and checker textures
     size_t bytes = 0;
 
     template <class T>
@@ -461,7 +504,7 @@ static void build_device_scene(const FlatScene& f, DeviceScene<R>& ds) {
     }
     std::vector<MatRec<R>> mats(f.mats.size());
     for (size_t i = 0; i < mats.size(); ++i) {
-        mats[i].type = f.mats[i].type; mats[i].tex = f.mats[i].tex;
+        mats[i].type = f.mats[i].type; mats[i].tex = f.mats[i].tex; mats[i].flags = f.mats[i].flags; mats[i].pad = 0;
         for (int a = 0; a < 3; ++a) mats[i].albedo[a] = R(f.mats[i].albedo[a]);
         mats[i].fuzz = R(f.mats[i].fuzz); mats[i].ir = R(f.mats[i].ir);
     }
@@ -494,6 +537,11 @@ static void build_device_scene(const FlatScene& f, DeviceScene<R>& ds) {
     ds.view.nworld = static_cast<int32_t>(f.world.size());
     for (int a = 0; a < 3; ++a) ds.view.bg[a] = R(f.background[a]);
     ds.media = f.has_media;
+    ds.features = f.features;
+    ds.tex_basic = true;
+    for (const auto& t : f.texs) ds.tex_basic = ds.tex_basic && (t.type == TEX_SOLID || t.type == TEX_CHECKER);
+    ds.mat_types = 0;
+    for (const auto& m : f.mats) ds.mat_types |= 1u << m.type;
 }
 
 // ------------------------------------------------------------------------------------------------ renderer
@@ -548,25 +596,50 @@ size_t Renderer::scene_bytes(int fp) const {
 }
 const FlatScene& Renderer::flat() const { return impl_->flat; }
 
-template <class R, bool MEDIA>
-static int persistent_blocks(int num_cu) {
-    static int ext = 0;
-    if (!ext) {
-        int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_extend<R, MEDIA>, kBlock, 0) != hipSuccess || per_cu < 1) per_cu = 2;
-        ext = per_cu;
-    }
-    return ext * num_cu;
+template <class R, uint32_t F>
+static int extend_blocks(int num_cu) {
+    static int per_cu = 0;
+    if (!per_cu && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_extend<R, F>, kBlock, 0) != hipSuccess || per_cu < 1)) per_cu = 2;
+    return per_cu * num_cu;  // num_cu (256) is a multiple of 8: the wave count is a multiple of kShards
+}
+template <class R, uint32_t F, uint32_t M, uint32_t TF>
+static int shade_blocks(int num_cu) {
+    static int per_cu = 0;
+    if (!per_cu && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_shade<R, F, M, TF>, kBlock, 0) != hipSuccess || per_cu < 1)) per_cu = 2;
+    return per_cu * num_cu;
+}
+// Textured materials get the "solid + checker" instantiation unless the scene holds noise or image textures.
+template <class R, uint32_t F, uint32_t M>
+static void launch_shade(uint32_t mat_types, bool tex_basic, int num_cu, hipStream_t st, const DevScene<R>& S, const PassGeom& g,
+                         const Work<R>& w, int d) {
+    if (!(mat_types & (1u << M))) return;
+    constexpr bool textured = M == MAT_LAMBERTIAN || M == MAT_LIGHT || M == MAT_ISOTROPIC;
+    if (!textured || tex_basic)
+        hipLaunchKernelGGL((k_shade<R, F, M, kTexBasic>), dim3(shade_blocks<R, F, M, kTexBasic>(num_cu)), dim3(kBlock), 0, st, S, g, w, d);
+    else
+        hipLaunchKernelGGL((k_shade<R, F, M, TF_ALL>), dim3(shade_blocks<R, F, M, TF_ALL>(num_cu)), dim3(kBlock), 0, st, S, g, w, d);
+}
+// One bounce (extend + one shade launch per material type present) of the smallest kernel instantiation that
+// covers the scene's features.
+template <class R, uint32_t F>
+static void launch_bounce(uint32_t mat_types, bool tex_basic, int num_cu, hipStream_t st, const DevScene<R>& S, const PassGeom& g, const CameraRec<R>& cam,
+                          const Work<R>& w, int d, const std::function<void()>& mark) {
+    if (mark) mark();
+    hipLaunchKernelGGL((k_extend<R, F>), dim3(extend_blocks<R, F>(num_cu)), dim3(kBlock), 0, st, S, g, cam, w, d);
+    if (mark) mark();
+    launch_shade<R, F, MAT_LAMBERTIAN>(mat_types, tex_basic, num_cu, st, S, g, w, d);
+    launch_shade<R, F, MAT_METAL>(mat_types, tex_basic, num_cu, st, S, g, w, d);
+    launch_shade<R, F, MAT_DIELECTRIC>(mat_types, tex_basic, num_cu, st, S, g, w, d);
+    launch_shade<R, F, MAT_LIGHT>(mat_types, tex_basic, num_cu, st, S, g, w, d);
+    launch_shade<R, F, MAT_ISOTROPIC>(mat_types, tex_basic, num_cu, st, S, g, w, d);
+    if (mark) mark();
 }
 template <class R>
-static int shade_blocks(int num_cu) {
-    static int sh = 0;
-    if (!sh) {
-        int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_shade<R>, kBlock, 0) != hipSuccess || per_cu < 1) per_cu = 2;
-        sh = per_cu;
-    }
-    return sh * num_cu;
+static void bounce(uint32_t feat, uint32_t mat_types, bool tex_basic, int num_cu, hipStream_t st, const DevScene<R>& S, const PassGeom& g, const CameraRec<R>& cam,
+                   const Work<R>& w, int d, const std::function<void()>& mark) {
+    if ((feat & ~kFeatSpheres) == 0) launch_bounce<R, kFeatSpheres>(mat_types, tex_basic, num_cu, st, S, g, cam, w, d, mark);
+    else if ((feat & ~kFeatMesh) == 0) launch_bounce<R, kFeatMesh>(mat_types, tex_basic, num_cu, st, S, g, cam, w, d, mark);
+    else launch_bounce<R, F_ALL>(mat_types, tex_basic, num_cu, st, S, g, cam, w, d, mark);
 }
 
 template <class R>
@@ -596,13 +669,16 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     g.npix_pad = g.tiles_x * tiles_y * 64u;
     g.max_depth = p.max_depth;
     g.seed = p.seed;
-    // samples per pass: ~16M path slots per pass (memory is cheap on a 288 GB part; big passes amortise the
-    // per-depth launch tail), never more than spp.
+    // Samples per pass: ~48M path slots (memory is plentiful on a 288 GB part; big passes keep the deep,
+    // sparse bounces of a pass busy and amortise its per-depth launch tail), spread evenly over the passes.
+    const uint64_t target = 48ull << 20;
     uint32_t k = p.samples_per_pass > 0 ? static_cast<uint32_t>(p.samples_per_pass)
-                                        : std::max<uint32_t>(1u, (16u << 20) / g.npix_pad);
+                                        : static_cast<uint32_t>(std::max<uint64_t>(1, target / g.npix_pad));
     k = std::min<uint32_t>(k, static_cast<uint32_t>(p.spp));
-    const uint32_t Pmax = k * g.npix_pad;
     const int npasses = static_cast<int>((p.spp + k - 1) / k);
+    k = static_cast<uint32_t>((p.spp + npasses - 1) / npasses);
+    const uint32_t Pmax = k * g.npix_pad;
+    g.cap = shard_cap(Pmax);
     const int depth_slots = p.max_depth + 1;
     const size_t local_pix = static_cast<size_t>(nrows) * p.width;
 
@@ -611,12 +687,12 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     const size_t o_paths = off; off += al(sizeof(PathRec<R>) * Pmax);
     const size_t o_hits = off; off += al(sizeof(HitRecD<R>) * Pmax);
     const size_t o_res = off; off += al(sizeof(ResRec<R>) * Pmax);
-    const size_t o_q0 = off; off += al(4ull * Pmax);
-    const size_t o_q1 = off; off += al(4ull * Pmax);
-    size_t o_mq[kNumMatTypes];
-    for (int m = 0; m < kNumMatTypes; ++m) { o_mq[m] = off; off += al(4ull * Pmax); }
-    const size_t cnt_words = static_cast<size_t>(npasses) * depth_slots * kCStride;
+    const size_t o_a0 = off; off += al(4ull * kShards * g.cap);
+    const size_t o_a1 = off; off += al(4ull * kShards * g.cap);
+    const size_t o_mq = off; off += al(4ull * kMatSegs * g.cap);
+    const size_t cnt_words = static_cast<size_t>(depth_slots) * kQueueKinds * kShards * kCounterStride;
     const size_t o_cnt = off; off += al(4ull * cnt_words);
+    const size_t o_seg = off; off += al(sizeof(unsigned long long));
     const size_t o_acc = off; off += al(sizeof(double) * 3 * local_pix);
     const size_t o_rgb = off; off += al(3 * local_pix);
     char* base = static_cast<char*>(I.workspace(off));
@@ -625,10 +701,11 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     w.paths = reinterpret_cast<PathRec<R>*>(base + o_paths);
     w.hits = reinterpret_cast<HitRecD<R>*>(base + o_hits);
     w.res = reinterpret_cast<ResRec<R>*>(base + o_res);
-    w.queue[0] = reinterpret_cast<uint32_t*>(base + o_q0);
-    w.queue[1] = reinterpret_cast<uint32_t*>(base + o_q1);
-    for (int m = 0; m < kNumMatTypes; ++m) w.mq[m] = reinterpret_cast<uint32_t*>(base + o_mq[m]);
-    uint32_t* counters = reinterpret_cast<uint32_t*>(base + o_cnt);
+    w.active[0] = reinterpret_cast<uint32_t*>(base + o_a0);
+    w.active[1] = reinterpret_cast<uint32_t*>(base + o_a1);
+    w.mq = reinterpret_cast<uint32_t*>(base + o_mq);
+    w.counters = reinterpret_cast<uint32_t*>(base + o_cnt);
+    w.segments = reinterpret_cast<unsigned long long*>(base + o_seg);
     w.acc = reinterpret_cast<double*>(base + o_acc);
     uint8_t* drgb = reinterpret_cast<uint8_t*>(base + o_rgb);
 
@@ -643,7 +720,6 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
 
     const bool prof = (p.flags & RT_PROFILE) != 0;
     std::vector<hipEvent_t> evs;
-
     for (auto& e : I.ev)
         if (!e) HIP_OK(hipEventCreate(&e));
     if (prof) {  // event pool created before the timed region
@@ -653,24 +729,17 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     size_t ev_next = 0;
     auto mark = [&]() { HIP_OK(hipEventRecord(evs[ev_next++], stream)); };
     HIP_OK(hipEventRecord(I.ev[0], stream));
-    HIP_OK(hipMemsetAsync(counters, 0, 4ull * cnt_words, stream));
+    HIP_OK(hipMemsetAsync(w.segments, 0, sizeof(unsigned long long), stream));
     HIP_OK(hipMemsetAsync(w.acc, 0, sizeof(double) * 3 * local_pix, stream));
-    const int ext_blocks = ds.media ? persistent_blocks<R, true>(I.num_cu) : persistent_blocks<R, false>(I.num_cu);
-    const int sh_blocks = shade_blocks<R>(I.num_cu);
+    if (p.max_depth == 0) HIP_OK(hipMemsetAsync(w.res, 0, sizeof(ResRec<R>) * Pmax, stream));  // engine.h:451-452
     for (int pass = 0; pass < npasses; ++pass) {
         g.sample_base = static_cast<uint32_t>(pass) * k;
         g.k = std::min<uint32_t>(k, static_cast<uint32_t>(p.spp) - g.sample_base);
         g.P = g.k * g.npix_pad;
-        w.counters = counters + static_cast<size_t>(pass) * depth_slots * kCStride;
-        hipLaunchKernelGGL(k_gen<R>, dim3((g.P + 255) / 256), dim3(256), 0, stream, g, cam, w);
-        for (int d = 0; d < p.max_depth; ++d) {
-            if (prof) mark();
-            if (ds.media) hipLaunchKernelGGL((k_extend<R, true>), dim3(ext_blocks), dim3(kBlock), 0, stream, ds.view, w, d);
-            else hipLaunchKernelGGL((k_extend<R, false>), dim3(ext_blocks), dim3(kBlock), 0, stream, ds.view, w, d);
-            if (prof) mark();
-            hipLaunchKernelGGL(k_shade<R>, dim3(sh_blocks), dim3(kBlock), 0, stream, ds.view, w, d, p.max_depth);
-            if (prof) mark();
-        }
+        g.live = g.k * static_cast<uint32_t>(local_pix);
+        HIP_OK(hipMemsetAsync(w.counters, 0, 4ull * cnt_words, stream));
+        for (int d = 0; d < p.max_depth; ++d)
+            bounce<R>(ds.features, ds.mat_types, ds.tex_basic, I.num_cu, stream, ds.view, g, cam, w, d, prof ? std::function<void()>(mark) : std::function<void()>());
         hipLaunchKernelGGL(k_accum<R>, dim3((g.npix_pad + 255) / 256), dim3(256), 0, stream, g, w);
     }
     HIP_OK(hipGetLastError());
@@ -680,17 +749,14 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     const hipMemcpyKind kind_rgb = (p.flags & RT_OUT_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
     if (out_rgb) HIP_OK(hipMemcpyAsync(out_rgb, drgb, 3 * local_pix, kind_rgb, stream));
     if (out_acc) HIP_OK(hipMemcpyAsync(out_acc, w.acc, sizeof(double) * 3 * local_pix, kind_rgb, stream));
-    std::vector<uint32_t> hc(cnt_words);
-    HIP_OK(hipMemcpyAsync(hc.data(), counters, 4ull * cnt_words, hipMemcpyDeviceToHost, stream));
+    unsigned long long segs = 0;
+    HIP_OK(hipMemcpyAsync(&segs, w.segments, sizeof segs, hipMemcpyDeviceToHost, stream));
     HIP_OK(hipStreamSynchronize(stream));
     float ms = 0;
     HIP_OK(hipEventElapsedTime(&ms, I.ev[0], I.ev[1]));
     stats.ms = ms;
     stats.passes = npasses;
     stats.samples_per_pass = static_cast<int>(k);
-    uint64_t segs = 0;
-    for (int pass = 0; pass < npasses; ++pass)
-        for (int d = 0; d < p.max_depth; ++d) segs += hc[(static_cast<size_t>(pass) * depth_slots + d) * kCStride + kCQueue];
     stats.segments = segs;
     stats.primary = static_cast<uint64_t>(local_pix) * static_cast<uint64_t>(p.spp);
     if (prof) {

@@ -87,19 +87,29 @@ struct ObjRec {
     R p[4];         // TRANSLATE: offset xyz; ROTATE_Y: sin, cos; MEDIUM: neg_inv_density
 };
 constexpr int kMaxXformChain = 2;  // translate(rotate_y(X)) is the deepest chain in the reference scenes
+// Scene features: kernels are instantiated for feature subsets (spheres only / meshes / everything).
+enum Feature : uint32_t { F_SPHERE = 1u, F_TRI = 2u, F_RECT = 4u, F_BOX = 8u, F_XFORM = 16u, F_MEDIA = 32u, F_ALL = 63u };
+constexpr uint32_t kFeatSpheres = F_SPHERE;
+constexpr uint32_t kFeatMesh = F_SPHERE | F_TRI | F_RECT | F_MEDIA;
 
 // ---------------------------------------------------------------------------------------------- shading
 enum MatType : uint32_t { MAT_LAMBERTIAN = 0, MAT_METAL = 1, MAT_DIELECTRIC = 2, MAT_LIGHT = 3, MAT_ISOTROPIC = 4 };
 constexpr int kNumMatTypes = 5;
+enum MatFlags : uint32_t { MATF_NEEDS_UV = 1u };  // its texture tree samples u,v (image / barycentric image)
 template <class R>
 struct MatRec {
     uint32_t type;
     int32_t tex;    // lambertian / diffuse_light / isotropic
+    uint32_t flags;
+    uint32_t pad;
     R albedo[3];    // metal
     R fuzz;         // metal (already clamped to <= 1, material.h:47)
     R ir;           // dielectric
 };
 enum TexType : uint32_t { TEX_SOLID = 0, TEX_CHECKER = 1, TEX_NOISE = 2, TEX_IMAGE = 3, TEX_BARY_IMAGE = 4 };
+// Texture kinds present (shade kernels are instantiated for "solid + checker" and "all").
+enum TexFeature : uint32_t { TF_SOLID = 1u, TF_CHECKER = 2u, TF_NOISE = 4u, TF_IMAGE = 8u, TF_ALL = 15u };
+constexpr uint32_t kTexBasic = TF_SOLID | TF_CHECKER;
 template <class R>
 struct TexRec {
     uint32_t type;

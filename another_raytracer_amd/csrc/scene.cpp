@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <functional>
 #include <limits>
 #include <stdexcept>
 
@@ -786,10 +787,19 @@ struct Compiler {
 FlatScene compile_scene(const SceneGraph& g) {
     FlatScene f;
     if (g.world.empty()) throw std::runtime_error("Invalid input scene!");  // engine.h:32-36
+    // does a texture tree sample u,v? (image / barycentric image, possibly under a checker)
+    std::function<bool(int)> uses_uv = [&](int t) -> bool {
+        if (t < 0) return false;
+        const Texture& x = g.textures[t];
+        if (x.type == TEX_IMAGE || x.type == TEX_BARY_IMAGE) return true;
+        if (x.type == TEX_CHECKER) return uses_uv(x.even) || uses_uv(x.odd);
+        return false;
+    };
     for (const Material& m : g.materials) {
         MatRec<double> r{};
         r.type = m.type;
         r.tex = m.tex;
+        r.flags = uses_uv(m.tex) ? MATF_NEEDS_UV : 0u;
         for (int a = 0; a < 3; ++a) r.albedo[a] = m.albedo[a];
         r.fuzz = m.fuzz;
         r.ir = m.ir;
@@ -828,6 +838,10 @@ FlatScene compile_scene(const SceneGraph& g) {
     for (int w : g.world) c.top(w);
     for (int a = 0; a < 3; ++a) f.background[a] = g.background[a];
     if (f.max_bvh_depth > kMaxBvhDepth) throw std::runtime_error("bvh deeper than the traversal stack");
+    f.features = (f.spheres.empty() ? 0u : F_SPHERE) | (f.tris.empty() ? 0u : F_TRI) | (f.rects.empty() ? 0u : F_RECT) |
+                 (f.boxes.empty() ? 0u : F_BOX) | (f.has_media ? F_MEDIA : 0u);
+    for (const auto& o : f.objs)
+        if (o.kind == OBJ_TRANSLATE || o.kind == OBJ_ROTATE_Y) f.features |= F_XFORM;
     return f;
 }
 

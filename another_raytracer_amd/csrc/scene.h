@@ -167,6 +167,7 @@ struct FlatScene {
     std::vector<uint8_t> texels;
     double background[3] = {0, 0, 0};
     bool has_media = false;
+    uint32_t features = 0;               // layout.h Feature bits present in the scene
     int max_bvh_depth = 0;
 };
 FlatScene compile_scene(const SceneGraph& g);

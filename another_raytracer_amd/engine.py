@@ -54,7 +54,7 @@ class engine:
 
     def __init__(self, cam, mode=engine_mode.single, width=tracer_constants.image_width,
                  height=tracer_constants.image_height, samples_per_pixel=tracer_constants.samples_per_pixel,
-                 max_depth=tracer_constants.max_depth, device=0, seed=0, precision="f32", samples_per_pass=0):
+                 max_depth=tracer_constants.max_depth, device=0, seed=0, precision="f64", samples_per_pass=0):
         self.cam, self.m = cam, mode
         self.width, self.height = int(width), int(height)
         self.samples_per_pixel, self.max_depth = int(samples_per_pixel), int(max_depth)

@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=1024)
     ap.add_argument("--max-depth", type=int, default=50)
-    ap.add_argument("--precision", default="f32", choices=["f32", "f64"])
+    ap.add_argument("--precision", default="f64", choices=["f32", "f64"])
     ap.add_argument("--band-rows", type=int, default=16)
     ap.add_argument("--samples-per-pass", type=int, default=0)
     ap.add_argument("--no-profile", action="store_true", help="skip per-launch HIP events (no roofline)")
