@@ -6,6 +6,14 @@ instead of falling back to anything (there is no CPU fallback in the product).
 import ctypes
 import os
 
+try:
+    # torch-ROCm ships its own libamdhip64.so.7.  Importing torch first makes libart's DT_NEEDED on the same SONAME bind
+    # to that already-loaded runtime, so a process that uses both has ONE HIP runtime (device pointers, streams and
+    # events are shared).  Loaded the other way round, torch cannot initialise its GPUs.
+    import torch  # noqa: F401
+except ImportError:
+    pass
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libart.so")
 

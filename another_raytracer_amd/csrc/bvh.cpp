@@ -1,4 +1,4 @@
-// bvh.cpp — binned SAH builder (see bvh.h).
+// bvh.cpp — binned SAH binary tree, collapsed into the 4-wide node array of layout.h (see bvh.h).
 #include "bvh.h"
 
 #include <algorithm>
@@ -30,44 +30,49 @@ void grow(AABBd& a, const AABBd& b) {
     }
 }
 
+struct BNode {  // binary SAH tree node (host only)
+    AABBd box;
+    int left = -1, right = -1;   // inner: children in `tree`
+    int32_t leaf = 0;            // leaf: encoded primref range (< 0)
+    bool is_leaf() const { return left < 0; }
+};
+
 struct Builder {
     const std::vector<AABBd>& boxes;
     const std::vector<uint32_t>& refs;
-    std::vector<BvhNode>& nodes;
     std::vector<uint32_t>& primrefs;
     std::vector<uint32_t> idx;
     std::vector<Vec3> cent;
-    int max_depth = 0;
+    std::vector<BNode> tree;
 
-    int32_t leaf(int b, int e) {
+    int make_leaf_node(int b, int e, const AABBd& box) {
         if (e - b > 127) throw std::runtime_error("bvh leaf too large (depth limit reached)");
         uint32_t first = static_cast<uint32_t>(primrefs.size());
         if (first + static_cast<uint32_t>(e - b) > 0xFFFFFFu) throw std::runtime_error("too many primitives for the bvh encoding");
         for (int i = b; i < e; ++i) primrefs.push_back(refs[idx[i]]);
-        return make_leaf(first, static_cast<uint32_t>(e - b));
+        BNode n;
+        n.box = box;
+        n.leaf = make_leaf(first, static_cast<uint32_t>(e - b));
+        tree.push_back(n);
+        return static_cast<int>(tree.size()) - 1;
     }
 
-    // Returns the child code for idx[b, e) and its box.
-    int32_t build(int b, int e, int depth, AABBd& box) {
-        box = empty_box();
-        AABBd cb = empty_box();
+    int build(int b, int e, int depth) {
+        AABBd box = empty_box(), cb = empty_box();
         for (int i = b; i < e; ++i) {
             grow(box, boxes[idx[i]]);
             const Vec3& c = cent[idx[i]];
             grow(cb, AABBd{c, c});
         }
         const int n = e - b;
-        if (n == 1) return leaf(b, e);
-        if (depth >= kMaxBvhDepth - 1) return leaf(b, e);
+        if (n == 1 || depth >= kMaxBvhDepth - 1) return make_leaf_node(b, e, box);
 
-        // binned SAH over the widest centroid axis
-        int axis = 0;
+        int axis = 0;  // binned SAH over the widest centroid axis
         double ext[3];
         for (int k = 0; k < 3; ++k) ext[k] = cb.mx[k] - cb.mn[k];
         if (ext[1] > ext[axis]) axis = 1;
         if (ext[2] > ext[axis]) axis = 2;
         int mid = -1;
-        double best = std::numeric_limits<double>::infinity();
         if (ext[axis] > 0) {
             AABBd bin_box[kBins];
             int bin_n[kBins] = {0};
@@ -95,6 +100,7 @@ struct Builder {
             acc = empty_box();
             cnt = 0;
             int best_split = -1;
+            double best = std::numeric_limits<double>::infinity();
             const double parent = std::max(area(box), 1e-300);
             for (int i = 1; i < kBins; ++i) {
                 grow(acc, bin_box[i - 1]);
@@ -107,40 +113,82 @@ struct Builder {
                 }
             }
             if (best_split > 0) {
-                if (n <= kMaxLeafPrims && kCostIntersect * n <= best) return leaf(b, e);
+                if (n <= kMaxLeafPrims && kCostIntersect * n <= best) return make_leaf_node(b, e, box);
                 auto it = std::partition(idx.begin() + b, idx.begin() + e, [&](uint32_t p) { return bin_of(p) < best_split; });
                 mid = static_cast<int>(it - idx.begin());
             }
         }
         if (mid <= b || mid >= e) {  // degenerate centroids: object median
-            if (n <= kMaxLeafPrims) return leaf(b, e);
+            if (n <= kMaxLeafPrims) return make_leaf_node(b, e, box);
             mid = b + n / 2;
             std::nth_element(idx.begin() + b, idx.begin() + mid, idx.begin() + e,
                              [&](uint32_t x, uint32_t y) { return cent[x][axis] < cent[y][axis]; });
         }
-        const int32_t me = static_cast<int32_t>(nodes.size());
-        nodes.push_back(BvhNode{});
-        max_depth = std::max(max_depth, depth + 1);
-        AABBd lb, rb;
-        int32_t l = build(b, mid, depth + 1, lb);
-        int32_t r = build(mid, e, depth + 1, rb);
-        set_node(me, l, lb, r, rb);
+        const int me = static_cast<int>(tree.size());
+        tree.push_back(BNode{});
+        const int l = build(b, mid, depth + 1);
+        const int r = build(mid, e, depth + 1);
+        tree[me].box = box;
+        tree[me].left = l;
+        tree[me].right = r;
         return me;
     }
-
-    void set_node(int32_t me, int32_t l, const AABBd& lb, int32_t r, const AABBd& rb) {
-        float llo[3], lhi[3], rlo[3], rhi[3];
-        conservative_box(lb, llo, lhi);
-        conservative_box(rb, rlo, rhi);
-        BvhNode& nd = nodes[me];
-        nd.lx0 = llo[0]; nd.lx1 = lhi[0]; nd.ly0 = llo[1]; nd.ly1 = lhi[1];
-        nd.rx0 = rlo[0]; nd.rx1 = rhi[0]; nd.ry0 = rlo[1]; nd.ry1 = rhi[1];
-        nd.lz0 = llo[2]; nd.lz1 = lhi[2]; nd.rz0 = rlo[2]; nd.rz1 = rhi[2];
-        nd.left = l;
-        nd.right = r;
-        nd.pad0 = nd.pad1 = 0;
-    }
 };
+
+// Emits the 4-wide node for binary inner node `bn` (children pulled up greedily by largest surface area) and returns
+// its index; `stack` receives the worst-case traversal stack use below and including it.
+int32_t collapse(const std::vector<BNode>& tree, int bn, std::vector<BvhNode>& out, int& stack, int& depth) {
+    std::vector<int> kids = {tree[bn].left, tree[bn].right};
+    while (kids.size() < 4) {
+        int best = -1;
+        double best_a = -1;
+        for (size_t i = 0; i < kids.size(); ++i)
+            if (!tree[kids[i]].is_leaf() && area(tree[kids[i]].box) > best_a) {
+                best_a = area(tree[kids[i]].box);
+                best = static_cast<int>(i);
+            }
+        if (best < 0) break;
+        const int k = kids[best];
+        kids[best] = tree[k].left;
+        kids.push_back(tree[k].right);
+    }
+    const int32_t me = static_cast<int32_t>(out.size());
+    out.push_back(BvhNode{});
+    int child_stack = 0, child_depth = 0;
+    int32_t code[4];
+    float lo[4][3], hi[4][3];
+    for (int c = 0; c < 4; ++c) {
+        if (c >= static_cast<int>(kids.size())) {
+            code[c] = kNodeEmpty;
+            for (int k = 0; k < 3; ++k) {
+                lo[c][k] = std::numeric_limits<float>::max();
+                hi[c][k] = -std::numeric_limits<float>::max();
+            }
+            continue;
+        }
+        const BNode& k = tree[kids[c]];
+        conservative_box(k.box, lo[c], hi[c]);
+        if (k.is_leaf()) {
+            code[c] = k.leaf;
+        } else {
+            int s = 0, dd = 0;
+            code[c] = collapse(tree, kids[c], out, s, dd);
+            child_stack = std::max(child_stack, s);
+            child_depth = std::max(child_depth, dd);
+        }
+    }
+    BvhNode& n = out[me];
+    for (int c = 0; c < 4; ++c) {
+        n.lox[c] = lo[c][0]; n.hix[c] = hi[c][0];
+        n.loy[c] = lo[c][1]; n.hiy[c] = hi[c][1];
+        n.loz[c] = lo[c][2]; n.hiz[c] = hi[c][2];
+        n.child[c] = code[c];
+        n.pad[c] = 0;
+    }
+    stack = static_cast<int>(kids.size()) - 1 + child_stack;  // pushes on the worst root-to-leaf path
+    depth = 1 + child_depth;
+    return me;
+}
 
 }  // namespace
 
@@ -158,26 +206,39 @@ void conservative_box(const AABBd& b, float lo[3], float hi[3]) {
 }
 
 int32_t build_sah_bvh(const std::vector<AABBd>& boxes, const std::vector<uint32_t>& refs, std::vector<BvhNode>& nodes,
-                      std::vector<uint32_t>& primrefs, int& max_depth) {
+                      std::vector<uint32_t>& primrefs, int& max_depth, int& max_stack) {
     if (boxes.empty() || boxes.size() != refs.size()) throw std::runtime_error("bad bvh input");
-    Builder bl{boxes, refs, nodes, primrefs, {}, {}, 0};
+    Builder bl{boxes, refs, primrefs, {}, {}, {}};
     bl.idx.resize(boxes.size());
     bl.cent.resize(boxes.size());
     for (size_t i = 0; i < boxes.size(); ++i) {
         bl.idx[i] = static_cast<uint32_t>(i);
         for (int k = 0; k < 3; ++k) bl.cent[i][k] = 0.5 * (boxes[i].mn[k] + boxes[i].mx[k]);
     }
-    AABBd rootbox;
-    const int32_t root_slot = static_cast<int32_t>(nodes.size());
-    int32_t c = bl.build(0, static_cast<int>(boxes.size()), 0, rootbox);
-    if (c < 0) {  // the whole set is one leaf: root node with the leaf on both sides (tested once per side)
+    const int root = bl.build(0, static_cast<int>(boxes.size()), 0);
+    if (bl.tree[root].is_leaf()) {  // a single leaf: a root node with one real child
+        const int32_t me = static_cast<int32_t>(nodes.size());
         nodes.push_back(BvhNode{});
-        bl.set_node(root_slot, c, rootbox, c, rootbox);
-        bl.max_depth = std::max(bl.max_depth, 1);
-        c = root_slot;
+        float lo[3], hi[3];
+        conservative_box(bl.tree[root].box, lo, hi);
+        BvhNode& n = nodes[me];
+        for (int c = 0; c < 4; ++c) {
+            const bool real = c == 0;
+            n.lox[c] = real ? lo[0] : std::numeric_limits<float>::max(); n.hix[c] = real ? hi[0] : -std::numeric_limits<float>::max();
+            n.loy[c] = real ? lo[1] : std::numeric_limits<float>::max(); n.hiy[c] = real ? hi[1] : -std::numeric_limits<float>::max();
+            n.loz[c] = real ? lo[2] : std::numeric_limits<float>::max(); n.hiz[c] = real ? hi[2] : -std::numeric_limits<float>::max();
+            n.child[c] = real ? bl.tree[root].leaf : kNodeEmpty;
+            n.pad[c] = 0;
+        }
+        max_depth = 1;
+        max_stack = 0;
+        return me;
     }
-    max_depth = bl.max_depth;
-    return c;
+    int stack = 0, depth = 0;
+    const int32_t r = collapse(bl.tree, root, nodes, stack, depth);
+    max_depth = depth;
+    max_stack = stack;
+    return r;
 }
 
 }  // namespace art

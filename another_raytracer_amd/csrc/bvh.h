@@ -14,9 +14,10 @@
 
 namespace art {
 
-// Appends nodes/primrefs for one BVH and returns its root node index.  max_depth receives the tree depth.
+// Appends nodes/primrefs for one BVH and returns its root node index.  max_depth receives the 4-wide tree depth,
+// max_stack the worst-case number of traversal stack entries (sum of (children - 1) along a root-to-leaf path).
 int32_t build_sah_bvh(const std::vector<AABBd>& boxes, const std::vector<uint32_t>& refs, std::vector<BvhNode>& nodes,
-                      std::vector<uint32_t>& primrefs, int& max_depth);
+                      std::vector<uint32_t>& primrefs, int& max_depth, int& max_stack);
 
 // f32 box rounded outward + relative pad (the conservative box the traversal tests).
 void conservative_box(const AABBd& b, float lo[3], float hi[3]);

@@ -210,15 +210,37 @@ __device__ __forceinline__ bool hit_prim(const DevScene<R>& S, uint32_t ref, con
 }
 
 // ------------------------------------------------------------------------------------------------ BVH traversal
-// While-while traversal of the two-child f32 node array with a per-lane stack in LDS (stk[k * kBlock] is entry k of
-// this lane).  Box tests are f32 and conservative (boxes padded at build time, interval widened here); leaves run the
-// exact R tests and shrink tmax, so the closest hit equals the reference's bvh_node::hit (bvh.cpp:44-52) up to ties.
+// While-while traversal of the 4-wide f32 node array with a per-lane stack in LDS (stk[k * kBlock] is entry k of this
+// lane; the stack is a dynamic LDS array sized to the scene's worst-case depth).  Each node visit tests its four child
+// boxes at once, goes to the nearest hit child and pushes the other hit children far-to-near.  Box tests are f32 and
+// conservative (boxes padded at build time, interval widened here); leaves run the exact R tests and shrink tmax, so
+// the closest hit equals the reference's bvh_node::hit (bvh.cpp:44-52) up to exact-t ties.
 constexpr int kBlock = 256;
 
 __device__ __forceinline__ float f_lo(double t) { return t == -__builtin_inf() ? -__builtin_inff() : static_cast<float>(t) * (1.0f - 2e-6f) - 1e-30f; }
 __device__ __forceinline__ float f_lo(float t) { return t * (1.0f - 2e-6f) - 1e-30f; }
 __device__ __forceinline__ float f_hi(double t) { return t == __builtin_inf() ? __builtin_inff() : static_cast<float>(t) * (1.0f + 2e-6f) + 1e-30f; }
 __device__ __forceinline__ float f_hi(float t) { return t * (1.0f + 2e-6f) + 1e-30f; }
+
+// slab entry distance of one child box, +inf when the box is missed (or the slot is empty)
+__device__ __forceinline__ float slab(float lox, float hix, float loy, float hiy, float loz, float hiz, int32_t child, float ix, float iy,
+                                      float iz, float oix, float oiy, float oiz, float tminf, float tmaxf) {
+    const float x0 = lox * ix - oix, x1 = hix * ix - oix;
+    const float y0 = loy * iy - oiy, y1 = hiy * iy - oiy;
+    const float z0 = loz * iz - oiz, z1 = hiz * iz - oiz;
+    const float lo = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), tminf));
+    const float hi = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), tmaxf));
+    return (lo <= hi && child != kNodeEmpty) ? lo : __builtin_inff();
+}
+__device__ __forceinline__ void cas(float& ka, int32_t& ca, float& kb, int32_t& cb) {
+    const bool s = kb < ka;
+    const float k = s ? kb : ka;
+    const int32_t c = s ? cb : ca;
+    kb = s ? ka : kb;
+    cb = s ? ca : cb;
+    ka = k;
+    ca = c;
+}
 
 template <class R, uint32_t F>
 __device__ __forceinline__ bool traverse(const DevScene<R>& S, int32_t root, const Ray<R>& r, R tmin, R tmax, int32_t* stk, R& t,
@@ -234,31 +256,24 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, int32_t root, con
     for (;;) {
         while (node >= 0) {
             const float4* np = reinterpret_cast<const float4*>(S.nodes + node);
-            const float4 a = np[0], b = np[1], c = np[2];
-            const int4 ch = reinterpret_cast<const int4*>(np)[3];
-            const float l0x = a.x * ix - oix, l1x = a.y * ix - oix, l0y = a.z * iy - oiy, l1y = a.w * iy - oiy;
-            const float l0z = c.x * iz - oiz, l1z = c.y * iz - oiz;
-            const float r0x = b.x * ix - oix, r1x = b.y * ix - oix, r0y = b.z * iy - oiy, r1y = b.w * iy - oiy;
-            const float r0z = c.z * iz - oiz, r1z = c.w * iz - oiz;
-            const float llo = fmaxf(fmaxf(fminf(l0x, l1x), fminf(l0y, l1y)), fmaxf(fminf(l0z, l1z), tminf));
-            const float lhi = fminf(fminf(fmaxf(l0x, l1x), fmaxf(l0y, l1y)), fminf(fmaxf(l0z, l1z), tmaxf));
-            const float rlo = fmaxf(fmaxf(fminf(r0x, r1x), fminf(r0y, r1y)), fmaxf(fminf(r0z, r1z), tminf));
-            const float rhi = fminf(fminf(fmaxf(r0x, r1x), fmaxf(r0y, r1y)), fminf(fmaxf(r0z, r1z), tmaxf));
-            const bool hl = llo <= lhi, hr = rlo <= rhi;
-            if (!hl && !hr) {
-                node = sp > 0 ? stk[(--sp) * kBlock] : kNodeEmpty;
-            } else {
-                int32_t first = hl ? ch.x : ch.y;
-                if (hl && hr) {
-                    int32_t second = ch.y;
-                    if (rlo < llo) {
-                        first = ch.y;
-                        second = ch.x;
-                    }
-                    stk[(sp++) * kBlock] = second;
-                }
-                node = first;
-            }
+            const float4 lx = np[0], hx = np[1], ly = np[2], hy = np[3], lz = np[4], hz = np[5];
+            const int4 ch = reinterpret_cast<const int4*>(np)[6];
+            float k0 = slab(lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, ch.x, ix, iy, iz, oix, oiy, oiz, tminf, tmaxf);
+            float k1 = slab(lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, ch.y, ix, iy, iz, oix, oiy, oiz, tminf, tmaxf);
+            float k2 = slab(lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, ch.z, ix, iy, iz, oix, oiy, oiz, tminf, tmaxf);
+            float k3 = slab(lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, ch.w, ix, iy, iz, oix, oiy, oiz, tminf, tmaxf);
+            int32_t c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
+            // sorting network: ascending entry distance, misses (+inf) last
+            cas(k0, c0, k1, c1);
+            cas(k2, c2, k3, c3);
+            cas(k0, c0, k2, c2);
+            cas(k1, c1, k3, c3);
+            cas(k1, c1, k2, c2);
+            const float inf = __builtin_inff();
+            if (k3 < inf) stk[(sp++) * kBlock] = c3;
+            if (k2 < inf) stk[(sp++) * kBlock] = c2;
+            if (k1 < inf) stk[(sp++) * kBlock] = c1;
+            node = k0 < inf ? c0 : (sp > 0 ? stk[(--sp) * kBlock] : kNodeEmpty);
         }
         if (node == kNodeEmpty) break;
         const uint32_t first = leaf_first(node), cnt = leaf_count(node);

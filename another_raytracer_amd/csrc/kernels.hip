@@ -157,6 +157,7 @@ struct PassGeom {
     uint32_t P;                 // k * npix_pad path slots
     uint32_t cap;               // shard capacity
     uint32_t live;              // k * rows * W: slots that are real pixels (depth-0 segments)
+    uint32_t stack;             // LDS traversal stack entries per lane
     int32_t max_depth;
     uint64_t seed;
 };
@@ -197,6 +198,36 @@ __device__ __forceinline__ void wave_append(bool pred, uint32_t val, uint32_t* s
     if (pred) {
         const uint32_t off = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(mask >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(mask), 0u));
         shard_buf[base + off] = val;
+    }
+}
+
+// Appends every lane with mtype in [0, kNumMatTypes) to its material queue (this wave's shard) with ONE vector atomic:
+// lane m reserves the slots of material m, so the wave pays one atomic round trip instead of one per material.
+template <class R>
+__device__ __forceinline__ void append_by_material(int mtype, uint32_t q, const Work<R>& w, const PassGeom& g, int d, int shard) {
+    uint64_t masks[kNumMatTypes];
+    uint64_t any = 0;
+#pragma unroll
+    for (int m = 0; m < kNumMatTypes; ++m) {
+        masks[m] = __ballot(mtype == m);
+        any |= masks[m];
+    }
+    if (any == 0) return;
+    const int lane = static_cast<int>(__lane_id());
+    uint64_t my_mask = 0;
+#pragma unroll
+    for (int m = 0; m < kNumMatTypes; ++m)
+        if (lane == m) my_mask = masks[m];
+    uint32_t base = 0;
+    if (lane < kNumMatTypes && my_mask != 0) base = atomicAdd(counter(w, d, 1 + lane, shard), static_cast<uint32_t>(__popcll(my_mask)));
+    base = __shfl(base, mtype >= 0 ? mtype : 0);  // all lanes: lanes 0..4 own the reservations
+    if (mtype >= 0) {
+        uint64_t mine = masks[0];
+#pragma unroll
+        for (int m = 1; m < kNumMatTypes; ++m)
+            if (mtype == m) mine = masks[m];
+        const uint32_t off = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(mine >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(mine), 0u));
+        w.mq[static_cast<size_t>(mtype * kShards + shard) * g.cap + base + off] = q;
     }
 }
 
@@ -262,7 +293,7 @@ __device__ __forceinline__ void gen_ray(const PassGeom& g, const CameraRec<R>& c
 
 template <class R, uint32_t F>
 __global__ __launch_bounds__(kBlock) void k_extend(DevScene<R> S, PassGeom g, CameraRec<R> cam, Work<R> w, int d) {
-    __shared__ int32_t stack[kStackDepth * kBlock];
+    extern __shared__ int32_t stack[];  // g.stack entries x kBlock lanes (sized per scene at launch)
     __shared__ uint32_t pre[kBlock + 1];
     int32_t* stk = stack + threadIdx.x;
     // input: depth 0 = every slot (identity; padding slots are skipped), deeper = the kShards active shards
@@ -324,9 +355,7 @@ __global__ __launch_bounds__(kBlock) void k_extend(DevScene<R> S, PassGeom g, Ca
                 store_res(w.res, q, st.L);
             }
         }
-#pragma unroll
-        for (int m = 0; m < kNumMatTypes; ++m)
-            wave_append(mtype == m, q, w.mq + static_cast<size_t>(m * kShards + shard) * g.cap, counter(w, d, 1 + m, shard));
+        append_by_material(mtype, q, w, g, d, shard);
     }
 }
 
@@ -450,6 +479,7 @@ struct DeviceScene {
     DevScene<R> view{};
     bool media = false;
     uint32_t features = F_ALL;
+    int max_stack = kMaxStackDepth;
     uint32_t mat_types = (1u << kNumMatTypes) - 1;  // bit m: some material of type m exists
     bool tex_basic = false;                          // only solid and checker textures
     size_t bytes = 0;
@@ -538,6 +568,7 @@ static void build_device_scene(const FlatScene& f, DeviceScene<R>& ds) {
     for (int a = 0; a < 3; ++a) ds.view.bg[a] = R(f.background[a]);
     ds.media = f.has_media;
     ds.features = f.features;
+    ds.max_stack = f.max_stack;
     ds.tex_basic = true;
     for (const auto& t : f.texs) ds.tex_basic = ds.tex_basic && (t.type == TEX_SOLID || t.type == TEX_CHECKER);
     ds.mat_types = 0;
@@ -596,10 +627,11 @@ size_t Renderer::scene_bytes(int fp) const {
 }
 const FlatScene& Renderer::flat() const { return impl_->flat; }
 
+// Persistent extend grid for a given dynamic LDS stack: every block the CUs can hold at once.
 template <class R, uint32_t F>
-static int extend_blocks(int num_cu) {
-    static int per_cu = 0;
-    if (!per_cu && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_extend<R, F>, kBlock, 0) != hipSuccess || per_cu < 1)) per_cu = 2;
+static int extend_blocks(int num_cu, size_t lds) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_extend<R, F>, kBlock, lds) != hipSuccess || per_cu < 1) per_cu = 1;
     return per_cu * num_cu;  // num_cu (256) is a multiple of 8: the wave count is a multiple of kShards
 }
 template <class R, uint32_t F, uint32_t M, uint32_t TF>
@@ -625,7 +657,14 @@ template <class R, uint32_t F>
 static void launch_bounce(uint32_t mat_types, bool tex_basic, int num_cu, hipStream_t st, const DevScene<R>& S, const PassGeom& g, const CameraRec<R>& cam,
                           const Work<R>& w, int d, const std::function<void()>& mark) {
     if (mark) mark();
-    hipLaunchKernelGGL((k_extend<R, F>), dim3(extend_blocks<R, F>(num_cu)), dim3(kBlock), 0, st, S, g, cam, w, d);
+    const size_t lds = sizeof(int32_t) * g.stack * kBlock;
+    static int blocks = 0;
+    static size_t blocks_lds = ~size_t(0);
+    if (lds != blocks_lds) {
+        blocks = extend_blocks<R, F>(num_cu, lds);
+        blocks_lds = lds;
+    }
+    hipLaunchKernelGGL((k_extend<R, F>), dim3(blocks), dim3(kBlock), lds, st, S, g, cam, w, d);
     if (mark) mark();
     launch_shade<R, F, MAT_LAMBERTIAN>(mat_types, tex_basic, num_cu, st, S, g, w, d);
     launch_shade<R, F, MAT_METAL>(mat_types, tex_basic, num_cu, st, S, g, w, d);
@@ -669,6 +708,7 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     g.npix_pad = g.tiles_x * tiles_y * 64u;
     g.max_depth = p.max_depth;
     g.seed = p.seed;
+    g.stack = static_cast<uint32_t>(std::max(1, ds.max_stack));
     // Samples per pass: ~48M path slots (memory is plentiful on a 288 GB part; big passes keep the deep,
     // sparse bounces of a pass busy and amortise its per-depth launch tail), spread evenly over the passes.
     const uint64_t target = 48ull << 20;

@@ -58,23 +58,25 @@ struct BoxRec {         // box.cpp: six rects in a fixed order (face index 0..5 
 };
 
 // ---------------------------------------------------------------------------------------------- BVH
-// Two-child node, 64 B = one cache line, fetched as four 16-B loads.  Child boxes are rounded outward to
-// f32 and padded, so f32 traversal is conservative; leaf tests run in R.
-//   child >= 0 : inner node index;   child < 0 : leaf ~((count << 24) | first_primref_slot);   -1 : empty
-struct BvhNode {
-    float lx0, lx1, ly0, ly1;   // left  child box x/y
-    float rx0, rx1, ry0, ry1;   // right child box x/y
-    float lz0, lz1, rz0, rz1;   // z of both
-    int32_t left, right, pad0, pad1;
+// Four-child node, 128 B = two cache lines, fetched as eight 16-B loads; the four child boxes are stored SoA so one
+// node visit tests all four with float4 arithmetic.  Child boxes are rounded outward to f32 and padded, so f32
+// traversal is conservative; leaf tests run in R.
+//   child >= 0 : inner node index;   child < 0 : leaf ~((count << 24) | first_primref_slot);   -1 : empty slot
+struct alignas(16) BvhNode {
+    float lox[4], hix[4];
+    float loy[4], hiy[4];
+    float loz[4], hiz[4];
+    int32_t child[4];
+    int32_t pad[4];
 };
-static_assert(sizeof(BvhNode) == 64, "BvhNode must be one 64-B line");
+static_assert(sizeof(BvhNode) == 128, "BvhNode must be two 64-B lines");
 constexpr int32_t kNodeEmpty = -1;
 ART_HD int32_t make_leaf(uint32_t first, uint32_t count) { return ~static_cast<int32_t>((count << 24) | first); }
 ART_HD uint32_t leaf_first(int32_t c) { return static_cast<uint32_t>(~c) & 0xFFFFFFu; }
 ART_HD uint32_t leaf_count(int32_t c) { return (static_cast<uint32_t>(~c) >> 24) & 0x7Fu; }
 constexpr int kMaxLeafPrims = 4;
-constexpr int kMaxBvhDepth = 30;   // traversal stack (LDS) depth is kStackDepth >= kMaxBvhDepth + 1
-constexpr int kStackDepth = 32;
+constexpr int kMaxBvhDepth = 30;     // binary SAH tree depth cap
+constexpr int kMaxStackDepth = 64;   // per-lane LDS traversal stack entries (sized per scene: FlatScene::max_stack)
 
 // ---------------------------------------------------------------------------------------------- objects
 enum ObjKind : int32_t { OBJ_PRIM = 0, OBJ_BVH = 1, OBJ_TRANSLATE = 2, OBJ_ROTATE_Y = 3, OBJ_MEDIUM = 4 };

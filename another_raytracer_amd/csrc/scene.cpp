@@ -736,10 +736,11 @@ struct Compiler {
                 std::vector<uint32_t> refs;
                 std::vector<AABBd> boxes;
                 gather(idx, refs, boxes);
-                int depth = 0;
+                int depth = 0, stack = 0;
                 o.kind = OBJ_BVH;
-                o.a = build_sah_bvh(boxes, refs, f.nodes, f.primrefs, depth);
+                o.a = build_sah_bvh(boxes, refs, f.nodes, f.primrefs, depth, stack);
                 f.max_bvh_depth = std::max(f.max_bvh_depth, depth);
+                f.max_stack = std::max(f.max_stack, stack);
                 return add_obj(o);
             }
             case N_TRANSLATE:
@@ -837,7 +838,7 @@ FlatScene compile_scene(const SceneGraph& g) {
     Compiler c{g, f};
     for (int w : g.world) c.top(w);
     for (int a = 0; a < 3; ++a) f.background[a] = g.background[a];
-    if (f.max_bvh_depth > kMaxBvhDepth) throw std::runtime_error("bvh deeper than the traversal stack");
+    if (f.max_stack > kMaxStackDepth) throw std::runtime_error("bvh needs a deeper traversal stack than kMaxStackDepth");
     f.features = (f.spheres.empty() ? 0u : F_SPHERE) | (f.tris.empty() ? 0u : F_TRI) | (f.rects.empty() ? 0u : F_RECT) |
                  (f.boxes.empty() ? 0u : F_BOX) | (f.has_media ? F_MEDIA : 0u);
     for (const auto& o : f.objs)

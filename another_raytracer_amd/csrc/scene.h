@@ -168,7 +168,8 @@ struct FlatScene {
     double background[3] = {0, 0, 0};
     bool has_media = false;
     uint32_t features = 0;               // layout.h Feature bits present in the scene
-    int max_bvh_depth = 0;
+    int max_bvh_depth = 0;               // 4-wide tree depth
+    int max_stack = 0;                   // worst-case traversal stack entries (sizes the LDS stack)
 };
 FlatScene compile_scene(const SceneGraph& g);
 
