@@ -15,7 +15,7 @@ except ImportError:
     pass
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libart.so")
+LIB_PATH = os.environ.get("ART_LIB") or os.path.join(_HERE, "libart.so")  # ART_LIB: A/B another build
 
 RT_OK = 0
 RT_FP32, RT_FP64 = 0, 1

@@ -29,6 +29,10 @@
 #include "device.h"
 #include "renderer.h"
 
+#ifndef ART_EXTEND_MIN_WAVES
+#define ART_EXTEND_MIN_WAVES 1  // __launch_bounds__ minimum waves per SIMD for k_extend (register budget knob)
+#endif
+
 namespace art {
 
 #define HIP_OK(x)                                                                                         \
@@ -292,7 +296,7 @@ __device__ __forceinline__ void gen_ray(const PassGeom& g, const CameraRec<R>& c
 }
 
 template <class R, uint32_t F>
-__global__ __launch_bounds__(kBlock) void k_extend(DevScene<R> S, PassGeom g, CameraRec<R> cam, Work<R> w, int d) {
+__global__ __launch_bounds__(kBlock, ART_EXTEND_MIN_WAVES) void k_extend(DevScene<R> S, PassGeom g, CameraRec<R> cam, Work<R> w, int d) {
     extern __shared__ int32_t stack[];  // g.stack entries x kBlock lanes (sized per scene at launch)
     __shared__ uint32_t pre[kBlock + 1];
     int32_t* stk = stack + threadIdx.x;
