@@ -8,6 +8,7 @@
 
 #include <cfloat>
 #include <cstdint>
+#include <type_traits>
 
 #include "layout.h"
 
@@ -101,8 +102,9 @@ struct DevScene {
     const PerlinRec<R>* perlins;
     const ImageRec* images;
     const uint8_t* texels;
+    const uint8_t* lds_image;   // layout.h LDS scene image (nullptr unless the scene qualifies)
+    uint32_t lds_nodes, lds_slots, lds_mov;  // filled entries per plane group
     int32_t nworld;
-    int32_t pad;
     R bg[3];
 };
 
@@ -111,13 +113,11 @@ constexpr uint32_t kMediumHit = 0xFFFFFFFFu;  // hit.prim value of a constant_me
 // ------------------------------------------------------------------------------------------------ primitives
 // sphere.h:39-65 / moving_sphere.h:41-58 (root selection only; the surface is rebuilt in shade).
 template <class R>
-__device__ __forceinline__ bool hit_sphere(const SphereRec<R>& s, const Ray<R>& r, R tmin, R tmax, R& t) {
-    V3<R> center = ld3(s.c);
-    if (s.flags & SPH_MOVING) center = center + ((r.tm - s.t0) / s.dt) * ld3(s.d);
+__device__ __forceinline__ bool hit_sphere_at(V3<R> center, R radius, const Ray<R>& r, R tmin, R tmax, R& t) {
     const V3<R> oc = r.o - center;
     const R a = len2(r.d);
     const R half_b = dot(oc, r.d);
-    const R c = len2(oc) - s.r * s.r;
+    const R c = len2(oc) - radius * radius;
     const R disc = half_b * half_b - a * c;
     if (disc < R(0)) return false;
     const R sqrtd = sqrt(disc);
@@ -128,6 +128,15 @@ __device__ __forceinline__ bool hit_sphere(const SphereRec<R>& s, const Ray<R>& 
     }
     t = root;
     return true;
+}
+// moving_sphere.h:72-74 center(time) = center0 + ((time - time0) / (time1 - time0)) * (center1 - center0)
+template <class R>
+__device__ __forceinline__ V3<R> moving_center(V3<R> c0, V3<R> d, R t0, R dt, R tm) { return c0 + ((tm - t0) / dt) * d; }
+template <class R>
+__device__ __forceinline__ bool hit_sphere(const SphereRec<R>& s, const Ray<R>& r, R tmin, R tmax, R& t) {
+    V3<R> center = ld3(s.c);
+    if (s.flags & SPH_MOVING) center = moving_center(center, ld3(s.d), s.t0, s.dt, r.tm);
+    return hit_sphere_at(center, s.r, r, tmin, tmax, t);
 }
 
 // triangle.h:22-88 (geometric test, unnormalised normal).
@@ -210,7 +219,7 @@ __device__ __forceinline__ bool hit_prim(const DevScene<R>& S, uint32_t ref, con
 }
 
 // ------------------------------------------------------------------------------------------------ BVH traversal
-// While-while traversal of the 4-wide f32 node array with a per-lane stack in LDS (stk[k * kBlock] is entry k of this
+// While-while traversal of the 4-wide f32 node array with a per-lane stack in LDS (stk[k * B] is entry k of this
 // lane; the stack is a dynamic LDS array sized to the scene's worst-case depth).  Each node visit tests its four child
 // boxes at once, goes to the nearest hit child and pushes the other hit children far-to-near.  Box tests are f32 and
 // conservative (boxes padded at build time, interval widened here); leaves run the exact R tests and shrink tmax, so
@@ -242,9 +251,30 @@ __device__ __forceinline__ void cas(float& ka, int32_t& ca, float& kb, int32_t& 
     ca = c;
 }
 
-template <class R, uint32_t F>
-__device__ __forceinline__ bool traverse(const DevScene<R>& S, int32_t root, const Ray<R>& r, R tmin, R tmax, int32_t* stk, R& t,
-                                         uint32_t& prim, uint32_t& face) {
+// Leaf slot test of the LDS scene image (layout.h): the same root selection as hit_sphere on the same f64 values.
+__device__ __forceinline__ bool hit_lds_slot(const uint8_t* lds, uint32_t slot, const Ray<double>& r, double tmin, double tmax,
+                                             double& t, uint32_t& prim) {
+    const double2* sp = reinterpret_cast<const double2*>(lds + kLdsOffSph) + slot;
+    const double2 a = sp[0], b = sp[kLdsSlotCap];
+    const uint32_t code = reinterpret_cast<const uint32_t*>(lds + kLdsOffRef)[slot];
+    V3<double> center{a.x, a.y, b.x};
+    const uint32_t mv = code >> kLdsRefMovShift;
+    if (mv) {
+        const double2* mp = reinterpret_cast<const double2*>(lds + kLdsOffMov) + (mv - 1);
+        const double2 m0 = mp[0], m1 = mp[kLdsMovCap], m2 = mp[2 * kLdsMovCap];
+        center = moving_center(center, V3<double>{m0.x, m0.y, m1.x}, m1.y, m2.x, r.tm);
+    }
+    prim = make_primref(PRIM_SPHERE, code & kLdsRefIndexMask);
+    return hit_sphere_at(center, b.y, r, tmin, tmax, t);
+}
+
+// Traversal stack entry: node/leaf codes, 16 bits in the LDS-scene variant (layout.h lds_leaf), 32 bits otherwise.
+template <bool L> using StackT = typename std::conditional<L, int16_t, int32_t>::type;
+
+// B: lanes per block (LDS stack stride).  L: nodes and leaf spheres come from the LDS scene image at `lds`.
+template <class R, uint32_t F, int B, bool L>
+__device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* lds, int32_t root, const Ray<R>& r, R tmin, R tmax,
+                                         StackT<L>* stk, R& t, uint32_t& prim, uint32_t& face) {
     const float ox = static_cast<float>(r.o.x), oy = static_cast<float>(r.o.y), oz = static_cast<float>(r.o.z);
     const float ix = 1.0f / static_cast<float>(r.d.x), iy = 1.0f / static_cast<float>(r.d.y), iz = 1.0f / static_cast<float>(r.d.z);
     const float oix = ox * ix, oiy = oy * iy, oiz = oz * iz;
@@ -255,9 +285,18 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, int32_t root, con
     int32_t node = root;
     for (;;) {
         while (node >= 0) {
-            const float4* np = reinterpret_cast<const float4*>(S.nodes + node);
-            const float4 lx = np[0], hx = np[1], ly = np[2], hy = np[3], lz = np[4], hz = np[5];
-            const int4 ch = reinterpret_cast<const int4*>(np)[6];
+            float4 lx, hx, ly, hy, lz, hz;
+            int4 ch;
+            if constexpr (L) {
+                const float4* np = reinterpret_cast<const float4*>(lds + kLdsOffNodes) + node;
+                lx = np[0]; hx = np[kLdsNodeCap]; ly = np[2 * kLdsNodeCap]; hy = np[3 * kLdsNodeCap];
+                lz = np[4 * kLdsNodeCap]; hz = np[5 * kLdsNodeCap];
+                ch = reinterpret_cast<const int4*>(np)[6 * kLdsNodeCap];
+            } else {
+                const float4* np = reinterpret_cast<const float4*>(S.nodes + node);
+                lx = np[0]; hx = np[1]; ly = np[2]; hy = np[3]; lz = np[4]; hz = np[5];
+                ch = reinterpret_cast<const int4*>(np)[6];
+            }
             float k0 = slab(lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, ch.x, ix, iy, iz, oix, oiy, oiz, tminf, tmaxf);
             float k1 = slab(lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, ch.y, ix, iy, iz, oix, oiy, oiz, tminf, tmaxf);
             float k2 = slab(lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, ch.z, ix, iy, iz, oix, oiy, oiz, tminf, tmaxf);
@@ -270,18 +309,32 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, int32_t root, con
             cas(k1, c1, k3, c3);
             cas(k1, c1, k2, c2);
             const float inf = __builtin_inff();
-            if (k3 < inf) stk[(sp++) * kBlock] = c3;
-            if (k2 < inf) stk[(sp++) * kBlock] = c2;
-            if (k1 < inf) stk[(sp++) * kBlock] = c1;
-            node = k0 < inf ? c0 : (sp > 0 ? stk[(--sp) * kBlock] : kNodeEmpty);
+            if (k3 < inf) stk[(sp++) * B] = static_cast<StackT<L>>(c3);
+            if (k2 < inf) stk[(sp++) * B] = static_cast<StackT<L>>(c2);
+            if (k1 < inf) stk[(sp++) * B] = static_cast<StackT<L>>(c1);
+            node = k0 < inf ? c0 : (sp > 0 ? stk[(--sp) * B] : kNodeEmpty);
         }
         if (node == kNodeEmpty) break;
-        const uint32_t first = leaf_first(node), cnt = leaf_count(node);
+        uint32_t first, cnt;
+        if constexpr (L) {
+            const uint32_t x = ~static_cast<uint32_t>(node);
+            first = x & ((1u << kLdsLeafShift) - 1);
+            cnt = x >> kLdsLeafShift;
+        } else {
+            first = leaf_first(node);
+            cnt = leaf_count(node);
+        }
         for (uint32_t k = 0; k < cnt; ++k) {
-            const uint32_t ref = S.primrefs[first + k];
             R tt;
-            uint32_t fc = 0;
-            if (hit_prim<R, F>(S, ref, r, tmin, tmax, tt, fc)) {
+            uint32_t fc = 0, ref;
+            bool h;
+            if constexpr (L) {
+                h = hit_lds_slot(lds, first + k, r, tmin, tmax, tt, ref);
+            } else {
+                ref = S.primrefs[first + k];
+                h = hit_prim<R, F>(S, ref, r, tmin, tmax, tt, fc);
+            }
+            if (h) {
                 tmax = tt;
                 t = tt;
                 prim = ref;
@@ -290,7 +343,7 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, int32_t root, con
                 tmaxf = f_hi(tt);
             }
         }
-        node = sp > 0 ? stk[(--sp) * kBlock] : kNodeEmpty;
+        node = sp > 0 ? stk[(--sp) * B] : kNodeEmpty;
     }
     return hit;
 }
@@ -312,9 +365,9 @@ __device__ __forceinline__ Ray<R> xform_in(const ObjRec<R>& o, const Ray<R>& r) 
 }
 
 // Any non-medium object: prim, BVH, or a translate/rotate_y chain (<= kMaxXformChain) over one of them.
-template <class R, uint32_t F>
-__device__ __forceinline__ bool hit_object(const DevScene<R>& S, int32_t oi, Ray<R> r, R tmin, R tmax, int32_t* stk, R& t, uint32_t& prim,
-                                           uint32_t& face) {
+template <class R, uint32_t F, int B, bool L>
+__device__ __forceinline__ bool hit_object(const DevScene<R>& S, const uint8_t* lds, int32_t oi, Ray<R> r, R tmin, R tmax, StackT<L>* stk,
+                                           R& t, uint32_t& prim, uint32_t& face) {
     if (F & F_XFORM) {
 #pragma unroll
         for (int c = 0; c < kMaxXformChain; ++c) {
@@ -329,18 +382,18 @@ __device__ __forceinline__ bool hit_object(const DevScene<R>& S, int32_t oi, Ray
         prim = static_cast<uint32_t>(o.a);
         return hit_prim<R, F>(S, prim, r, tmin, tmax, t, face);
     }
-    return traverse<R, F>(S, o.a, r, tmin, tmax, stk, t, prim, face);
+    return traverse<R, F, B, L>(S, lds, o.a, r, tmin, tmax, stk, t, prim, face);
 }
 
 // constant_medium.h:37-82.  Consumes one uniform when the clamped interval is non-empty.
-template <class R, uint32_t F>
-__device__ __forceinline__ bool hit_medium(const DevScene<R>& S, const ObjRec<R>& m, const Ray<R>& r, R tmin, R tmax, int32_t* stk,
-                                           uint64_t& rng, R& t) {
+template <class R, uint32_t F, int B, bool L>
+__device__ __forceinline__ bool hit_medium(const DevScene<R>& S, const uint8_t* lds, const ObjRec<R>& m, const Ray<R>& r, R tmin, R tmax,
+                                           StackT<L>* stk, uint64_t& rng, R& t) {
     const R inf = R(__builtin_inf());
     R t1, t2;
     uint32_t p, f;
-    if (!hit_object<R, F>(S, m.a, r, -inf, inf, stk, t1, p, f)) return false;
-    if (!hit_object<R, F>(S, m.a, r, t1 + R(0.0001), inf, stk, t2, p, f)) return false;
+    if (!hit_object<R, F, B, L>(S, lds, m.a, r, -inf, inf, stk, t1, p, f)) return false;
+    if (!hit_object<R, F, B, L>(S, lds, m.a, r, t1 + R(0.0001), inf, stk, t2, p, f)) return false;
     if (t1 < tmin) t1 = tmin;
     if (t2 > tmax) t2 = tmax;
     if (t1 >= t2) return false;
@@ -357,8 +410,9 @@ __device__ __forceinline__ bool hit_medium(const DevScene<R>& S, const ObjRec<R>
 struct HitOut {
     uint32_t prim, obj;  // obj: world slot | box face << 16
 };
-template <class R, uint32_t F>
-__device__ __forceinline__ bool trace_world(const DevScene<R>& S, const Ray<R>& r, int32_t* stk, uint64_t& rng, R& t, HitOut& h) {
+template <class R, uint32_t F, int B, bool L>
+__device__ __forceinline__ bool trace_world(const DevScene<R>& S, const uint8_t* lds, const Ray<R>& r, StackT<L>* stk, uint64_t& rng, R& t,
+                                            HitOut& h) {
     R closest = R(__builtin_inf());
     bool any = false;
     for (int w = 0; w < S.nworld; ++w) {
@@ -366,7 +420,7 @@ __device__ __forceinline__ bool trace_world(const DevScene<R>& S, const Ray<R>& 
         const ObjRec<R>& o = S.objs[oi];
         R tt;
         if ((F & F_MEDIA) && o.kind == OBJ_MEDIUM) {
-            if (hit_medium<R, F>(S, o, r, R(0.001), closest, stk, rng, tt)) {
+            if (hit_medium<R, F, B, L>(S, lds, o, r, R(0.001), closest, stk, rng, tt)) {
                 closest = tt;
                 any = true;
                 h.prim = kMediumHit;
@@ -374,7 +428,7 @@ __device__ __forceinline__ bool trace_world(const DevScene<R>& S, const Ray<R>& 
             }
         } else {
             uint32_t prim = 0, face = 0;
-            if (hit_object<R, F>(S, oi, r, R(0.001), closest, stk, tt, prim, face)) {
+            if (hit_object<R, F, B, L>(S, lds, oi, r, R(0.001), closest, stk, tt, prim, face)) {
                 closest = tt;
                 any = true;
                 h.prim = prim;

@@ -23,6 +23,7 @@
 #include <cstdio>
 #include <cstring>
 #include <stdexcept>
+#include <type_traits>
 #include <string>
 #include <vector>
 
@@ -235,22 +236,20 @@ __device__ __forceinline__ void append_by_material(int mtype, uint32_t q, const 
     }
 }
 
-// Block-wide exclusive prefix of n <= kBlock shard counts into pre[0..n] (pre[n] = total).
+// Exclusive prefix of the n <= 64 shard counts v (held by threads 0..n-1) into pre[0..n] (pre[n] = total), by one wave
+// scan; independent of the block size.
 __device__ __forceinline__ void block_prefix(uint32_t* pre, int n, uint32_t v) {
     const int t = threadIdx.x;
-    pre[t] = t < n ? v : 0u;
-    __syncthreads();
-    for (int off = 1; off < kBlock; off <<= 1) {
-        const uint32_t x = t >= off ? pre[t - off] : 0u;
-        __syncthreads();
-        pre[t] += x;
-        __syncthreads();
+    if (t < 64) {
+        uint32_t x = t < n ? v : 0u;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(x, off);
+            if (t >= off) x += y;
+        }
+        if (t < n) pre[t + 1] = x;
+        if (t == 0) pre[0] = 0u;
     }
-    // inclusive -> exclusive, shifted by one: pre[i] = sum of the first i counts
-    const uint32_t inc = pre[t];
-    __syncthreads();
-    if (t < n) pre[t + 1] = inc;
-    if (t == 0) pre[0] = 0u;
     __syncthreads();
 }
 // Segment of item i: largest s with pre[s] <= i (pre strictly describes n segments).
@@ -295,11 +294,43 @@ __device__ __forceinline__ void gen_ray(const PassGeom& g, const CameraRec<R>& c
     st.rng = rng;
 }
 
-template <class R, uint32_t F>
-__global__ __launch_bounds__(kBlock, ART_EXTEND_MIN_WAVES) void k_extend(DevScene<R> S, PassGeom g, CameraRec<R> cam, Work<R> w, int d) {
-    extern __shared__ int32_t stack[];  // g.stack entries x kBlock lanes (sized per scene at launch)
-    __shared__ uint32_t pre[kBlock + 1];
-    int32_t* stk = stack + threadIdx.x;
+#ifndef ART_LDS_BLOCK
+#define ART_LDS_BLOCK 1024
+#endif
+// Blocks of the LDS-scene variant: one block per CU holds the scene image once for 16 waves (4 per SIMD).
+constexpr int kBlockL = ART_LDS_BLOCK;
+
+// Copies the filled part of every plane of the LDS scene image (layout.h) into LDS.
+template <int B>
+__device__ __forceinline__ void load_lds_image(const uint8_t* image, uint8_t* lds, uint32_t nodes, uint32_t slots, uint32_t mov) {
+    const uint4* src = reinterpret_cast<const uint4*>(image);
+    uint4* dst = reinterpret_cast<uint4*>(lds);
+    auto copy = [&](uint32_t off, uint32_t n16) {
+        for (uint32_t i = threadIdx.x; i < n16; i += B) dst[off / 16 + i] = src[off / 16 + i];
+    };
+#pragma unroll
+    for (uint32_t j = 0; j < 7; ++j) copy(kLdsOffNodes + j * kLdsNodeCap * 16, nodes);
+#pragma unroll
+    for (uint32_t c = 0; c < 2; ++c) copy(kLdsOffSph + c * kLdsSlotCap * 16, slots);
+#pragma unroll
+    for (uint32_t c = 0; c < 3; ++c) copy(kLdsOffMov + c * kLdsMovCap * 16, mov);
+    copy(kLdsOffRef, (slots * 4 + 15) / 16);
+}
+
+// L: the scene is LDS-resident (DevScene::lds_image, spheres-only f64): nodes and leaf spheres are read from LDS.
+template <class R, uint32_t F, bool L>
+__global__ __launch_bounds__(L ? kBlockL : kBlock, L ? 1 : ART_EXTEND_MIN_WAVES) void k_extend(DevScene<R> S, PassGeom g, CameraRec<R> cam,
+                                                                                                 Work<R> w, int d) {
+    constexpr int B = L ? kBlockL : kBlock;
+    // dynamic LDS: [scene image (L only)][traversal stack: g.stack entries x B lanes] (sized per scene at launch)
+    extern __shared__ __align__(16) uint8_t smem[];
+    __shared__ uint32_t pre[kShards + 1];
+    const uint8_t* lds = smem;
+    StackT<L>* stk = reinterpret_cast<StackT<L>*>(smem + (L ? kLdsImageBytes : 0u)) + threadIdx.x;
+    if constexpr (L) {
+        load_lds_image<B>(S.lds_image, smem, S.lds_nodes, S.lds_slots, S.lds_mov);
+        __syncthreads();
+    }
     // input: depth 0 = every slot (identity; padding slots are skipped), deeper = the kShards active shards
     uint32_t count;
     if (d == 0) {
@@ -310,8 +341,8 @@ __global__ __launch_bounds__(kBlock, ART_EXTEND_MIN_WAVES) void k_extend(DevScen
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(w.segments, static_cast<unsigned long long>(d == 0 ? g.live : count));
     const uint32_t* in = w.active[d & 1];
-    const uint32_t wave = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
-    const uint32_t nwaves = gridDim.x * (kBlock / 64);
+    const uint32_t wave = blockIdx.x * (B / 64) + (threadIdx.x >> 6);
+    const uint32_t nwaves = gridDim.x * (B / 64);
     const int shard = static_cast<int>(wave % kShards);
     for (uint32_t b = wave; b * 64u < count; b += nwaves) {
         const uint32_t i = b * 64u + __lane_id();
@@ -334,7 +365,7 @@ __global__ __launch_bounds__(kBlock, ART_EXTEND_MIN_WAVES) void k_extend(DevScen
         if (live) {
             R t;
             HitOut h{0, 0};
-            if (trace_world<R, F>(S, st.ray, stk, st.rng, t, h)) {
+            if (trace_world<R, F, B, L>(S, lds, st.ray, stk, st.rng, t, h)) {
                 w.hits[q] = HitRecD<R>{t, h.prim, h.obj};
                 uint32_t m;
                 if ((F & F_MEDIA) && h.prim == kMediumHit) {
@@ -405,7 +436,7 @@ __device__ __forceinline__ bool scatter(const DevScene<R>& S, const MatRec<R>& m
 // Input: the kShards shards of material queue M at depth d (the extend stage sorted hits by material type).
 template <class R, uint32_t F, uint32_t M, uint32_t TF>
 __global__ __launch_bounds__(kBlock) void k_shade(DevScene<R> S, PassGeom g, Work<R> w, int d) {
-    __shared__ uint32_t pre[kBlock + 1];
+    __shared__ uint32_t pre[kShards + 1];
     block_prefix(pre, kShards, threadIdx.x < kShards ? *counter(w, d, 1 + static_cast<int>(M), threadIdx.x) : 0u);
     const uint32_t total = pre[kShards];
     const uint32_t* in = w.mq + static_cast<size_t>(M) * kShards * g.cap;
@@ -486,6 +517,7 @@ struct DeviceScene {
     int max_stack = kMaxStackDepth;
     uint32_t mat_types = (1u << kNumMatTypes) - 1;  // bit m: some material of type m exists
     bool tex_basic = false;                          // only solid and checker textures
+    bool lds_scene = false;                          // view.lds_image holds the layout.h LDS scene image
     size_t bytes = 0;
 
     template <class T>
@@ -508,6 +540,63 @@ template <class R, class D>
 static void cvt_sphere(const SphereRec<D>& s, SphereRec<R>& o) {
     for (int a = 0; a < 3; ++a) { o.c[a] = R(s.c[a]); o.d[a] = R(s.d[a]); }
     o.r = R(s.r); o.t0 = R(s.t0); o.dt = R(s.dt); o.mat = s.mat; o.flags = s.flags;
+}
+
+constexpr size_t kLdsPerCu = 160 * 1024;  // gfx950
+
+// LDS bytes of one k_extend block: scene image (L) + per-lane stack + the shard prefix.
+static size_t extend_lds_bytes(bool L, uint32_t stack) {
+    return L ? kLdsImageBytes + sizeof(int16_t) * stack * kBlockL : sizeof(int32_t) * stack * kBlock;
+}
+
+// Builds the layout.h LDS scene image when the f64 scene qualifies: spheres only, every BVH node and leaf slot within
+// the plane capacities, and image + stack within one CU's LDS.  Returns an empty vector otherwise.
+static std::vector<uint8_t> lds_scene_image(const FlatScene& f, uint32_t& nmov) {
+    std::vector<uint8_t> img;
+    nmov = 0;
+    const int stack = std::max(1, f.max_stack);
+    if ((f.features & ~kFeatSpheres) != 0 || f.nodes.empty() || f.nodes.size() > kLdsNodeCap || f.primrefs.size() > kLdsSlotCap ||
+        f.spheres.size() > kLdsRefIndexMask || extend_lds_bytes(true, static_cast<uint32_t>(stack)) + 4 * (kShards + 1) > kLdsPerCu)
+        return img;
+    for (uint32_t ref : f.primrefs) {
+        if (primref_type(ref) != PRIM_SPHERE) return img;
+        if (f.spheres[primref_index(ref)].flags & SPH_MOVING) ++nmov;
+    }
+    if (nmov > kLdsMovCap) return img;
+    for (const BvhNode& b : f.nodes)
+        for (int c = 0; c < 4; ++c)
+            if (b.child[c] < 0 && b.child[c] != kNodeEmpty && leaf_count(b.child[c]) > kLdsLeafMaxCount) return img;
+    img.assign(kLdsImageBytes, 0);
+    auto put = [&](uint32_t off, const void* v, size_t n) { std::memcpy(img.data() + off, v, n); };
+    for (size_t n = 0; n < f.nodes.size(); ++n) {
+        const BvhNode& b = f.nodes[n];
+        const float* planes[6] = {b.lox, b.hix, b.loy, b.hiy, b.loz, b.hiz};
+        for (uint32_t j = 0; j < 6; ++j) put(kLdsOffNodes + (j * kLdsNodeCap + static_cast<uint32_t>(n)) * 16, planes[j], 16);
+        int32_t child[4];
+        for (int c = 0; c < 4; ++c)
+            child[c] = (b.child[c] >= 0 || b.child[c] == kNodeEmpty) ? b.child[c] : lds_leaf(leaf_first(b.child[c]), leaf_count(b.child[c]));
+        put(kLdsOffNodes + (6 * kLdsNodeCap + static_cast<uint32_t>(n)) * 16, child, 16);
+    }
+    uint32_t m = 0;
+    for (size_t slot = 0; slot < f.primrefs.size(); ++slot) {
+        const uint32_t idx = primref_index(f.primrefs[slot]);
+        const auto& sp = f.spheres[idx];
+        const double p0[2] = {sp.c[0], sp.c[1]}, p1[2] = {sp.c[2], sp.r};
+        const uint32_t sl = static_cast<uint32_t>(slot);
+        put(kLdsOffSph + sl * 16, p0, 16);
+        put(kLdsOffSph + (kLdsSlotCap + sl) * 16, p1, 16);
+        uint32_t code = idx;
+        if (sp.flags & SPH_MOVING) {
+            const double m0[2] = {sp.d[0], sp.d[1]}, m1[2] = {sp.d[2], sp.t0}, m2[2] = {sp.dt, 0.0};
+            put(kLdsOffMov + m * 16, m0, 16);
+            put(kLdsOffMov + (kLdsMovCap + m) * 16, m1, 16);
+            put(kLdsOffMov + (2 * kLdsMovCap + m) * 16, m2, 16);
+            code |= (m + 1) << kLdsRefMovShift;
+            ++m;
+        }
+        put(kLdsOffRef + sl * 4, &code, 4);
+    }
+    return img;
 }
 
 template <class R>
@@ -568,6 +657,17 @@ static void build_device_scene(const FlatScene& f, DeviceScene<R>& ds) {
     ds.view.perlins = ds.upload(per);
     ds.view.images = ds.upload(f.images);
     ds.view.texels = ds.upload(f.texels);
+    if (std::is_same<R, double>::value) {
+        uint32_t nmov = 0;
+        const std::vector<uint8_t> img = lds_scene_image(f, nmov);
+        if (!img.empty()) {
+            ds.view.lds_image = ds.upload(img);
+            ds.view.lds_nodes = static_cast<uint32_t>(f.nodes.size());
+            ds.view.lds_slots = static_cast<uint32_t>(f.primrefs.size());
+            ds.view.lds_mov = nmov;
+            ds.lds_scene = true;
+        }
+    }
     ds.view.nworld = static_cast<int32_t>(f.world.size());
     for (int a = 0; a < 3; ++a) ds.view.bg[a] = R(f.background[a]);
     ds.media = f.has_media;
@@ -631,11 +731,11 @@ size_t Renderer::scene_bytes(int fp) const {
 }
 const FlatScene& Renderer::flat() const { return impl_->flat; }
 
-// Persistent extend grid for a given dynamic LDS stack: every block the CUs can hold at once.
-template <class R, uint32_t F>
+// Persistent extend grid for a given dynamic LDS size: every block the CUs can hold at once.
+template <class R, uint32_t F, bool L>
 static int extend_blocks(int num_cu, size_t lds) {
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_extend<R, F>, kBlock, lds) != hipSuccess || per_cu < 1) per_cu = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_extend<R, F, L>, L ? kBlockL : kBlock, lds) != hipSuccess || per_cu < 1) per_cu = 1;
     return per_cu * num_cu;  // num_cu (256) is a multiple of 8: the wave count is a multiple of kShards
 }
 template <class R, uint32_t F, uint32_t M, uint32_t TF>
@@ -657,18 +757,31 @@ static void launch_shade(uint32_t mat_types, bool tex_basic, int num_cu, hipStre
 }
 // One bounce (extend + one shade launch per material type present) of the smallest kernel instantiation that
 // covers the scene's features.
-template <class R, uint32_t F>
-static void launch_bounce(uint32_t mat_types, bool tex_basic, int num_cu, hipStream_t st, const DevScene<R>& S, const PassGeom& g, const CameraRec<R>& cam,
-                          const Work<R>& w, int d, const std::function<void()>& mark) {
-    if (mark) mark();
-    const size_t lds = sizeof(int32_t) * g.stack * kBlock;
+template <class R, uint32_t F, bool L>
+static void launch_extend(int num_cu, hipStream_t st, const DevScene<R>& S, const PassGeom& g, const CameraRec<R>& cam, const Work<R>& w, int d) {
+    const size_t lds = extend_lds_bytes(L, g.stack);
     static int blocks = 0;
     static size_t blocks_lds = ~size_t(0);
     if (lds != blocks_lds) {
-        blocks = extend_blocks<R, F>(num_cu, lds);
+        if (lds > 64 * 1024) HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_extend<R, F, L>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                        static_cast<int>(lds)));
+        blocks = extend_blocks<R, F, L>(num_cu, lds);
         blocks_lds = lds;
     }
-    hipLaunchKernelGGL((k_extend<R, F>), dim3(blocks), dim3(kBlock), lds, st, S, g, cam, w, d);
+    hipLaunchKernelGGL((k_extend<R, F, L>), dim3(blocks), dim3(L ? kBlockL : kBlock), lds, st, S, g, cam, w, d);
+}
+// One bounce (extend + one shade launch per material type present) of the smallest kernel instantiation that
+// covers the scene's features.
+template <class R, uint32_t F>
+static void launch_bounce(uint32_t mat_types, bool tex_basic, bool lds_scene, int num_cu, hipStream_t st, const DevScene<R>& S, const PassGeom& g,
+                          const CameraRec<R>& cam, const Work<R>& w, int d, const std::function<void()>& mark) {
+    if (mark) mark();
+    if constexpr (F == kFeatSpheres && std::is_same<R, double>::value) {
+        if (lds_scene) launch_extend<R, F, true>(num_cu, st, S, g, cam, w, d);
+        else launch_extend<R, F, false>(num_cu, st, S, g, cam, w, d);
+    } else {
+        launch_extend<R, F, false>(num_cu, st, S, g, cam, w, d);
+    }
     if (mark) mark();
     launch_shade<R, F, MAT_LAMBERTIAN>(mat_types, tex_basic, num_cu, st, S, g, w, d);
     launch_shade<R, F, MAT_METAL>(mat_types, tex_basic, num_cu, st, S, g, w, d);
@@ -678,11 +791,15 @@ static void launch_bounce(uint32_t mat_types, bool tex_basic, int num_cu, hipStr
     if (mark) mark();
 }
 template <class R>
-static void bounce(uint32_t feat, uint32_t mat_types, bool tex_basic, int num_cu, hipStream_t st, const DevScene<R>& S, const PassGeom& g, const CameraRec<R>& cam,
-                   const Work<R>& w, int d, const std::function<void()>& mark) {
-    if ((feat & ~kFeatSpheres) == 0) launch_bounce<R, kFeatSpheres>(mat_types, tex_basic, num_cu, st, S, g, cam, w, d, mark);
-    else if ((feat & ~kFeatMesh) == 0) launch_bounce<R, kFeatMesh>(mat_types, tex_basic, num_cu, st, S, g, cam, w, d, mark);
-    else launch_bounce<R, F_ALL>(mat_types, tex_basic, num_cu, st, S, g, cam, w, d, mark);
+static void bounce(const DeviceScene<R>& ds, bool allow_lds, int num_cu, hipStream_t st, const PassGeom& g, const CameraRec<R>& cam, const Work<R>& w, int d,
+                   const std::function<void()>& mark) {
+    const uint32_t feat = ds.features;
+    if ((feat & ~kFeatSpheres) == 0)
+        launch_bounce<R, kFeatSpheres>(ds.mat_types, ds.tex_basic, ds.lds_scene && allow_lds, num_cu, st, ds.view, g, cam, w, d, mark);
+    else if ((feat & ~kFeatMesh) == 0)
+        launch_bounce<R, kFeatMesh>(ds.mat_types, ds.tex_basic, false, num_cu, st, ds.view, g, cam, w, d, mark);
+    else
+        launch_bounce<R, F_ALL>(ds.mat_types, ds.tex_basic, false, num_cu, st, ds.view, g, cam, w, d, mark);
 }
 
 template <class R>
@@ -783,7 +900,7 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
         g.live = g.k * static_cast<uint32_t>(local_pix);
         HIP_OK(hipMemsetAsync(w.counters, 0, 4ull * cnt_words, stream));
         for (int d = 0; d < p.max_depth; ++d)
-            bounce<R>(ds.features, ds.mat_types, ds.tex_basic, I.num_cu, stream, ds.view, g, cam, w, d, prof ? std::function<void()>(mark) : std::function<void()>());
+            bounce<R>(ds, (p.flags & RT_GLOBAL_SCENE) == 0, I.num_cu, stream, g, cam, w, d, prof ? std::function<void()>(mark) : std::function<void()>());
         hipLaunchKernelGGL(k_accum<R>, dim3((g.npix_pad + 255) / 256), dim3(256), 0, stream, g, w);
     }
     HIP_OK(hipGetLastError());
@@ -802,6 +919,7 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     stats.passes = npasses;
     stats.samples_per_pass = static_cast<int>(k);
     stats.segments = segs;
+    stats.lds_scene = (ds.lds_scene && (p.flags & RT_GLOBAL_SCENE) == 0 && (ds.features & ~kFeatSpheres) == 0) ? 1 : 0;
     stats.primary = static_cast<uint64_t>(local_pix) * static_cast<uint64_t>(p.spp);
     if (prof) {
         double ext_ms = 0, sh_ms = 0;

@@ -4,7 +4,7 @@
 // (engine/hittable.h:25-29, rendering/material.h:10-17, rendering/texture.h:11-14).  Here the same graph is
 // compiled (scene.cpp: compile()) into typed arrays:
 //   * primitives   per-type AoS records (SphereRec, TriRec, RectRec, BoxRec), addressed by a 32-bit prim ref
-//   * BVH          one flat array of 64-B two-child nodes (f32, conservatively rounded boxes) per scene
+//   * BVH          one flat array of 128-B four-child nodes (f32, conservatively rounded boxes) per scene
 //   * objects      the top-level hittable_list (world) as ObjRec: PRIM | BVH | XFORM (translate/rotate_y) | MEDIUM
 //   * materials    MatRec, textures TexRec, perlin tables, image texel pool
 // Every record exists in an f64 and an f32 instantiation (template R); the BVH is always f32.
@@ -77,6 +77,29 @@ ART_HD uint32_t leaf_count(int32_t c) { return (static_cast<uint32_t>(~c) >> 24)
 constexpr int kMaxLeafPrims = 4;
 constexpr int kMaxBvhDepth = 30;     // binary SAH tree depth cap
 constexpr int kMaxStackDepth = 64;   // per-lane LDS traversal stack entries (sized per scene: FlatScene::max_stack)
+
+// ---------------------------------------------------------------------------------------------- LDS scene image
+// A spheres-only f64 scene whose BVH4 and leaf spheres fit one CU's LDS (the random-spheres benchmark scene: 234
+// nodes, 874 leaf slots) is traversed entirely out of LDS: k_extend copies this image into LDS once per block, so the
+// node and sphere fetches of the traversal never touch the vector-memory (TA/L1) path that bounds the global variant.
+// Every plane is an array of 16-B entries, so lanes fetching different nodes/spheres spread over the 16 four-bank slots
+// of the ds_read_b128 bank row, and the plane strides are compile-time (DS immediate offsets, no address VALU).
+constexpr uint32_t kLdsNodeCap = 256;   // BVH4 nodes: 7 planes (lox, hix, loy, hiy, loz, hiz as float4; child as int4)
+constexpr uint32_t kLdsSlotCap = 1024;  // leaf slots (= primref array entries): 2 planes (cx, cy), (cz, r) as double2
+constexpr uint32_t kLdsMovCap = 512;    // moving spheres: 3 planes (dx, dy), (dz, t0), (dt, 0) as double2
+constexpr uint32_t kLdsOffNodes = 0;
+constexpr uint32_t kLdsOffSph = kLdsOffNodes + 7 * kLdsNodeCap * 16;
+constexpr uint32_t kLdsOffMov = kLdsOffSph + 2 * kLdsSlotCap * 16;
+constexpr uint32_t kLdsOffRef = kLdsOffMov + 3 * kLdsMovCap * 16;  // u32 per slot: sphere index | (moving index + 1) << 20
+constexpr uint32_t kLdsImageBytes = kLdsOffRef + kLdsSlotCap * 4;
+constexpr uint32_t kLdsRefMovShift = 20;
+// Child codes in the image: inner node n as is, leaf ~((count << 10) | first), empty -1 -- all fit the 16-bit LDS
+// traversal stack entries of this variant (halving the stack is what lets 1024 lanes share one image).
+constexpr uint32_t kLdsLeafShift = 10;
+constexpr uint32_t kLdsLeafMaxCount = 31;
+ART_HD int32_t lds_leaf(uint32_t first, uint32_t count) { return ~static_cast<int32_t>((count << kLdsLeafShift) | first); }
+constexpr uint32_t kLdsRefIndexMask = (1u << kLdsRefMovShift) - 1;
+static_assert(kLdsImageBytes % 16 == 0, "LDS image is copied in 16-B pieces");
 
 // ---------------------------------------------------------------------------------------------- objects
 enum ObjKind : int32_t { OBJ_PRIM = 0, OBJ_BVH = 1, OBJ_TRANSLATE = 2, OBJ_ROTATE_Y = 3, OBJ_MEDIUM = 4 };

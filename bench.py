@@ -50,6 +50,7 @@ def parse():
     ap.add_argument("--band-rows", type=int, default=16)
     ap.add_argument("--samples-per-pass", type=int, default=0)
     ap.add_argument("--no-profile", action="store_true", help="skip per-launch HIP events (no roofline)")
+    ap.add_argument("--global-scene", action="store_true", help="force the global-memory extend kernel (A/B vs LDS scene)")
     ap.add_argument("--cpu-baseline-spp", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -118,6 +119,7 @@ def main():
                      samples_per_pixel=args.spp, max_depth=args.max_depth, device=dev.index, precision=args.precision,
                      samples_per_pass=args.samples_per_pass)
     eng.set_scene(world_scene.objects, world_scene.background)
+    eng.global_scene = args.global_scene
     rows = band_rows_of(args.height, args.band_rows, world, rank)
     local = torch.empty((len(rows), args.width, 3), dtype=torch.uint8, device=dev)
     profile = not args.no_profile

@@ -49,6 +49,7 @@ extern "C" {
 /* rt_params.flags */
 #define RT_OUT_DEVICE 1     /* out_rgb8 / out_accum are device pointers (on the scene's device) */
 #define RT_PROFILE 2        /* time every extend/shade launch with HIP events (rt_stats.*_ms) */
+#define RT_GLOBAL_SCENE 4   /* never use the LDS-resident scene variant of the extend kernel (A/B and parity tests) */
 
 typedef struct rt_scene rt_scene;
 typedef struct rt_graph rt_graph;
@@ -74,7 +75,7 @@ typedef struct rt_params {
     int32_t band_count;         /*   is rendered here when band % band_count == band_index; (H, 1, 0) = whole image */
     int32_t band_index;
     int32_t samples_per_pass;   /* 0 = auto (~16M path slots per pass) */
-    int32_t flags;              /* RT_OUT_DEVICE | RT_PROFILE */
+    int32_t flags;              /* RT_OUT_DEVICE | RT_PROFILE | RT_GLOBAL_SCENE */
     void* stream;               /* hipStream_t to run on, or NULL for the scene's own stream */
     double background[3];       /* engine::set_scene(world, background) (engine.h:24-28): returned on a miss */
 } rt_params;
@@ -85,7 +86,8 @@ typedef struct rt_stats {
     double ms;                  /* device time, first kernel -> finalized RGB8 (HIP events) */
     double extend_ms, shade_ms; /* RT_PROFILE only: summed launch durations */
     uint64_t extend_launches, shade_launches;
-    int32_t passes, samples_per_pass, local_rows, pad;
+    int32_t passes, samples_per_pass, local_rows;
+    int32_t lds_scene;          /* 1: the extend kernel read the scene from LDS (spheres-only scene that fits), 0: from HBM */
 } rt_stats;
 
 typedef struct rt_scene_info {  /* scene_manager.h:6-14 */
