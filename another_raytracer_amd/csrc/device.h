@@ -103,7 +103,6 @@ struct DevScene {
     const ImageRec* images;
     const uint8_t* texels;
     const uint8_t* lds_image;   // layout.h LDS scene image (nullptr unless the scene qualifies)
-    uint32_t lds_nodes, lds_slots, lds_mov;  // filled entries per plane group
     int32_t nworld;
     R bg[3];
 };
@@ -220,7 +219,8 @@ __device__ __forceinline__ bool hit_prim(const DevScene<R>& S, uint32_t ref, con
 
 // ------------------------------------------------------------------------------------------------ BVH traversal
 // While-while traversal of the 4-wide f32 node array with a per-lane stack in LDS (stk[k * B] is entry k of this
-// lane; the stack is a dynamic LDS array sized to the scene's worst-case depth).  Each node visit tests its four child
+// lane; the stack is a dynamic LDS array of the scene's worst-case depth + 2 rows: stk[-B] is a kNodeEmpty sentinel and
+// the last row takes the discarded write of a branchless push).  Each node visit tests its four child
 // boxes at once, goes to the nearest hit child and pushes the other hit children far-to-near.  Box tests are f32 and
 // conservative (boxes padded at build time, interval widened here); leaves run the exact R tests and shrink tmax, so
 // the closest hit equals the reference's bvh_node::hit (bvh.cpp:44-52) up to exact-t ties.
@@ -231,15 +231,30 @@ __device__ __forceinline__ float f_lo(float t) { return t * (1.0f - 2e-6f) - 1e-
 __device__ __forceinline__ float f_hi(double t) { return t == __builtin_inf() ? __builtin_inff() : static_cast<float>(t) * (1.0f + 2e-6f) + 1e-30f; }
 __device__ __forceinline__ float f_hi(float t) { return t * (1.0f + 2e-6f) + 1e-30f; }
 
-// slab entry distance of one child box, +inf when the box is missed (or the slot is empty)
-__device__ __forceinline__ float slab(float lox, float hix, float loy, float hiy, float loz, float hiz, int32_t child, float ix, float iy,
-                                      float iz, float oix, float oiy, float oiz, float tminf, float tmaxf) {
-    const float x0 = lox * ix - oix, x1 = hix * ix - oix;
-    const float y0 = loy * iy - oiy, y1 = hiy * iy - oiy;
-    const float z0 = loz * iz - oiz, z1 = hiz * iz - oiz;
+// Slab entry distances of the four child boxes of a node, +inf when a box is missed (or the slot is empty).  The plane
+// distances are single-rounding FMAs fma(plane, 1/d, -o/d), two children per v_pk_fma_f32; one rounding is no worse
+// than the mul+sub the box padding was sized for, so the test stays conservative.
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float slab_key(float x0, float x1, float y0, float y1, float z0, float z1, int32_t child, float tminf, float tmaxf) {
     const float lo = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), tminf));
     const float hi = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), tmaxf));
     return (lo <= hi && child != kNodeEmpty) ? lo : __builtin_inff();
+}
+__device__ __forceinline__ void slab4(const float4& lx, const float4& hx, const float4& ly, const float4& hy, const float4& lz, const float4& hz,
+                                      const int4& ch, float ix, float iy, float iz, float oix, float oiy, float oiz, float tminf, float tmaxf,
+                                      float& k0, float& k1, float& k2, float& k3) {
+    const f2v vx = {ix, ix}, vy = {iy, iy}, vz = {iz, iz};
+    const f2v nx = {-oix, -oix}, ny = {-oiy, -oiy}, nz = {-oiz, -oiz};
+    const f2v x0a = __builtin_elementwise_fma(f2v{lx.x, lx.y}, vx, nx), x0b = __builtin_elementwise_fma(f2v{lx.z, lx.w}, vx, nx);
+    const f2v x1a = __builtin_elementwise_fma(f2v{hx.x, hx.y}, vx, nx), x1b = __builtin_elementwise_fma(f2v{hx.z, hx.w}, vx, nx);
+    const f2v y0a = __builtin_elementwise_fma(f2v{ly.x, ly.y}, vy, ny), y0b = __builtin_elementwise_fma(f2v{ly.z, ly.w}, vy, ny);
+    const f2v y1a = __builtin_elementwise_fma(f2v{hy.x, hy.y}, vy, ny), y1b = __builtin_elementwise_fma(f2v{hy.z, hy.w}, vy, ny);
+    const f2v z0a = __builtin_elementwise_fma(f2v{lz.x, lz.y}, vz, nz), z0b = __builtin_elementwise_fma(f2v{lz.z, lz.w}, vz, nz);
+    const f2v z1a = __builtin_elementwise_fma(f2v{hz.x, hz.y}, vz, nz), z1b = __builtin_elementwise_fma(f2v{hz.z, hz.w}, vz, nz);
+    k0 = slab_key(x0a.x, x1a.x, y0a.x, y1a.x, z0a.x, z1a.x, ch.x, tminf, tmaxf);
+    k1 = slab_key(x0a.y, x1a.y, y0a.y, y1a.y, z0a.y, z1a.y, ch.y, tminf, tmaxf);
+    k2 = slab_key(x0b.x, x1b.x, y0b.x, y1b.x, z0b.x, z1b.x, ch.z, tminf, tmaxf);
+    k3 = slab_key(x0b.y, x1b.y, y0b.y, y1b.y, z0b.y, z1b.y, ch.w, tminf, tmaxf);
 }
 __device__ __forceinline__ void cas(float& ka, int32_t& ca, float& kb, int32_t& cb) {
     const bool s = kb < ka;
@@ -297,10 +312,8 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                 lx = np[0]; hx = np[1]; ly = np[2]; hy = np[3]; lz = np[4]; hz = np[5];
                 ch = reinterpret_cast<const int4*>(np)[6];
             }
-            float k0 = slab(lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, ch.x, ix, iy, iz, oix, oiy, oiz, tminf, tmaxf);
-            float k1 = slab(lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, ch.y, ix, iy, iz, oix, oiy, oiz, tminf, tmaxf);
-            float k2 = slab(lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, ch.z, ix, iy, iz, oix, oiy, oiz, tminf, tmaxf);
-            float k3 = slab(lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, ch.w, ix, iy, iz, oix, oiy, oiz, tminf, tmaxf);
+            float k0, k1, k2, k3;
+            slab4(lx, hx, ly, hy, lz, hz, ch, ix, iy, iz, oix, oiy, oiz, tminf, tmaxf, k0, k1, k2, k3);
             int32_t c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
             // sorting network: ascending entry distance, misses (+inf) last
             cas(k0, c0, k1, c1);
@@ -308,11 +321,19 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
             cas(k0, c0, k2, c2);
             cas(k1, c1, k3, c3);
             cas(k1, c1, k2, c2);
+            // branchless pushes (far to near): every write lands at or below the final top, which the stack's spare row
+            // covers; the pop reads the entry under the top, the per-lane sentinel row (kNodeEmpty) when the stack is empty
             const float inf = __builtin_inff();
-            if (k3 < inf) stk[(sp++) * B] = static_cast<StackT<L>>(c3);
-            if (k2 < inf) stk[(sp++) * B] = static_cast<StackT<L>>(c2);
-            if (k1 < inf) stk[(sp++) * B] = static_cast<StackT<L>>(c1);
-            node = k0 < inf ? c0 : (sp > 0 ? stk[(--sp) * B] : kNodeEmpty);
+            stk[sp * B] = static_cast<StackT<L>>(c3);
+            sp += k3 < inf;
+            stk[sp * B] = static_cast<StackT<L>>(c2);
+            sp += k2 < inf;
+            stk[sp * B] = static_cast<StackT<L>>(c1);
+            sp += k1 < inf;
+            const int32_t top = stk[(sp - 1) * B];
+            const bool near = k0 < inf;
+            node = near ? c0 : top;
+            sp -= (!near && sp > 0) ? 1 : 0;
         }
         if (node == kNodeEmpty) break;
         uint32_t first, cnt;
@@ -343,7 +364,8 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                 tmaxf = f_hi(tt);
             }
         }
-        node = sp > 0 ? stk[(--sp) * B] : kNodeEmpty;
+        node = stk[(sp - 1) * B];
+        sp -= sp > 0 ? 1 : 0;
     }
     return hit;
 }

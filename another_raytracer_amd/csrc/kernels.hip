@@ -149,6 +149,7 @@ constexpr int kShards = 32;
 constexpr int kCounterStride = 32;                   // words between counters (128 B)
 constexpr int kQueueKinds = 1 + kNumMatTypes;        // 0: active (extend input), 1..5: material queues
 constexpr int kMatSegs = kNumMatTypes * kShards;     // shade input segments
+constexpr uint64_t kMaxPassSlots = 1ull << 31;       // slot ids and batch offsets stay well inside u32
 // + 2 batches per material kernel: the kNumMatTypes shade launches of one depth all append to the same next-queue shards
 __host__ __device__ inline uint32_t shard_cap(uint32_t P) { return 64u * ((((P + 63u) / 64u) + kShards - 1) / kShards + 2 * kNumMatTypes); }
 
@@ -162,7 +163,7 @@ struct PassGeom {
     uint32_t P;                 // k * npix_pad path slots
     uint32_t cap;               // shard capacity
     uint32_t live;              // k * rows * W: slots that are real pixels (depth-0 segments)
-    uint32_t stack;             // LDS traversal stack entries per lane
+    uint32_t stack;             // LDS traversal stack rows per lane (stack_rows)
     int32_t max_depth;
     uint64_t seed;
 };
@@ -300,21 +301,25 @@ __device__ __forceinline__ void gen_ray(const PassGeom& g, const CameraRec<R>& c
 // Blocks of the LDS-scene variant: one block per CU holds the scene image once for 16 waves (4 per SIMD).
 constexpr int kBlockL = ART_LDS_BLOCK;
 
-// Copies the filled part of every plane of the LDS scene image (layout.h) into LDS.
+// Copies the LDS scene image (layout.h) into LDS in one round: every lane issues all of its 16-B loads before its
+// first store, so the block pays one global-load latency instead of one per plane.
 template <int B>
-__device__ __forceinline__ void load_lds_image(const uint8_t* image, uint8_t* lds, uint32_t nodes, uint32_t slots, uint32_t mov) {
+__device__ __forceinline__ void load_lds_image(const uint8_t* image, uint8_t* lds) {
+    constexpr uint32_t n16 = kLdsImageBytes / 16;
+    constexpr int per = static_cast<int>((n16 + B - 1) / B);
     const uint4* src = reinterpret_cast<const uint4*>(image);
     uint4* dst = reinterpret_cast<uint4*>(lds);
-    auto copy = [&](uint32_t off, uint32_t n16) {
-        for (uint32_t i = threadIdx.x; i < n16; i += B) dst[off / 16 + i] = src[off / 16 + i];
-    };
+    uint4 v[per];
 #pragma unroll
-    for (uint32_t j = 0; j < 7; ++j) copy(kLdsOffNodes + j * kLdsNodeCap * 16, nodes);
+    for (int j = 0; j < per; ++j) {
+        const uint32_t i = threadIdx.x + static_cast<uint32_t>(j) * B;
+        if (i < n16) v[j] = src[i];
+    }
 #pragma unroll
-    for (uint32_t c = 0; c < 2; ++c) copy(kLdsOffSph + c * kLdsSlotCap * 16, slots);
-#pragma unroll
-    for (uint32_t c = 0; c < 3; ++c) copy(kLdsOffMov + c * kLdsMovCap * 16, mov);
-    copy(kLdsOffRef, (slots * 4 + 15) / 16);
+    for (int j = 0; j < per; ++j) {
+        const uint32_t i = threadIdx.x + static_cast<uint32_t>(j) * B;
+        if (i < n16) dst[i] = v[j];
+    }
 }
 
 // L: the scene is LDS-resident (DevScene::lds_image, spheres-only f64): nodes and leaf spheres are read from LDS.
@@ -326,11 +331,10 @@ __global__ __launch_bounds__(L ? kBlockL : kBlock, L ? 1 : ART_EXTEND_MIN_WAVES)
     extern __shared__ __align__(16) uint8_t smem[];
     __shared__ uint32_t pre[kShards + 1];
     const uint8_t* lds = smem;
-    StackT<L>* stk = reinterpret_cast<StackT<L>*>(smem + (L ? kLdsImageBytes : 0u)) + threadIdx.x;
-    if constexpr (L) {
-        load_lds_image<B>(S.lds_image, smem, S.lds_nodes, S.lds_slots, S.lds_mov);
-        __syncthreads();
-    }
+    // row 0 of the stack region is this lane's sentinel (device.h traverse), entries start at row 1
+    StackT<L>* stk = reinterpret_cast<StackT<L>*>(smem + (L ? kLdsImageBytes : 0u)) + B + threadIdx.x;
+    stk[-B] = static_cast<StackT<L>>(kNodeEmpty);
+
     // input: depth 0 = every slot (identity; padding slots are skipped), deeper = the kShards active shards
     uint32_t count;
     if (d == 0) {
@@ -340,6 +344,12 @@ __global__ __launch_bounds__(L ? kBlockL : kBlock, L ? 1 : ART_EXTEND_MIN_WAVES)
         count = pre[kShards];
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(w.segments, static_cast<unsigned long long>(d == 0 ? g.live : count));
+    if constexpr (L) {
+        // deep bounces have few paths: blocks without a batch leave before paying for the image
+        if (static_cast<uint64_t>(blockIdx.x) * B >= count) return;
+        load_lds_image<B>(S.lds_image, smem);
+        __syncthreads();
+    }
     const uint32_t* in = w.active[d & 1];
     const uint32_t wave = blockIdx.x * (B / 64) + (threadIdx.x >> 6);
     const uint32_t nwaves = gridDim.x * (B / 64);
@@ -544,7 +554,9 @@ static void cvt_sphere(const SphereRec<D>& s, SphereRec<R>& o) {
 
 constexpr size_t kLdsPerCu = 160 * 1024;  // gfx950
 
-// LDS bytes of one k_extend block: scene image (L) + per-lane stack + the shard prefix.
+// Traversal stack rows per lane: the worst-case depth + the sentinel row + the spare row of branchless pushes.
+static uint32_t stack_rows(int max_stack) { return static_cast<uint32_t>(std::max(1, max_stack)) + 2u; }
+// LDS bytes of one k_extend block: scene image (L) + per-lane stack.
 static size_t extend_lds_bytes(bool L, uint32_t stack) {
     return L ? kLdsImageBytes + sizeof(int16_t) * stack * kBlockL : sizeof(int32_t) * stack * kBlock;
 }
@@ -554,9 +566,8 @@ static size_t extend_lds_bytes(bool L, uint32_t stack) {
 static std::vector<uint8_t> lds_scene_image(const FlatScene& f, uint32_t& nmov) {
     std::vector<uint8_t> img;
     nmov = 0;
-    const int stack = std::max(1, f.max_stack);
     if ((f.features & ~kFeatSpheres) != 0 || f.nodes.empty() || f.nodes.size() > kLdsNodeCap || f.primrefs.size() > kLdsSlotCap ||
-        f.spheres.size() > kLdsRefIndexMask || extend_lds_bytes(true, static_cast<uint32_t>(stack)) + 4 * (kShards + 1) > kLdsPerCu)
+        f.spheres.size() > kLdsRefIndexMask || extend_lds_bytes(true, stack_rows(f.max_stack)) + 4 * (kShards + 1) > kLdsPerCu)
         return img;
     for (uint32_t ref : f.primrefs) {
         if (primref_type(ref) != PRIM_SPHERE) return img;
@@ -662,9 +673,6 @@ static void build_device_scene(const FlatScene& f, DeviceScene<R>& ds) {
         const std::vector<uint8_t> img = lds_scene_image(f, nmov);
         if (!img.empty()) {
             ds.view.lds_image = ds.upload(img);
-            ds.view.lds_nodes = static_cast<uint32_t>(f.nodes.size());
-            ds.view.lds_slots = static_cast<uint32_t>(f.primrefs.size());
-            ds.view.lds_mov = nmov;
             ds.lds_scene = true;
         }
     }
@@ -829,10 +837,14 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     g.npix_pad = g.tiles_x * tiles_y * 64u;
     g.max_depth = p.max_depth;
     g.seed = p.seed;
-    g.stack = static_cast<uint32_t>(std::max(1, ds.max_stack));
-    // Samples per pass: ~48M path slots (memory is plentiful on a 288 GB part; big passes keep the deep,
-    // sparse bounces of a pass busy and amortise its per-depth launch tail), spread evenly over the passes.
-    const uint64_t target = 48ull << 20;
+    g.stack = stack_rows(ds.max_stack);
+    // Samples per pass: as many path slots as half of the free HBM holds (plus the workspace this renderer already
+    // owns).  Every pass pays max_depth bounces of fixed launch/tail cost whatever its size, so on a 288 GB part the
+    // 1080p x 1024 spp frame runs in 3 passes instead of ~40 (5.6 -> 6.9 Gsamples/s measured); spread evenly.
+    const size_t slot_bytes = sizeof(PathRec<R>) + sizeof(HitRecD<R>) + sizeof(ResRec<R>) + 4u * (2u + kNumMatTypes) + 8u;
+    size_t free_b = 0, total_b = 0;
+    HIP_OK(hipMemGetInfo(&free_b, &total_b));
+    const uint64_t target = std::min<uint64_t>((free_b + I.ws_bytes) / 2 / slot_bytes, kMaxPassSlots);  // fixed point: no regrowth
     uint32_t k = p.samples_per_pass > 0 ? static_cast<uint32_t>(p.samples_per_pass)
                                         : static_cast<uint32_t>(std::max<uint64_t>(1, target / g.npix_pad));
     k = std::min<uint32_t>(k, static_cast<uint32_t>(p.spp));

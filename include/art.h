@@ -74,7 +74,7 @@ typedef struct rt_params {
     int32_t band_rows;          /* row-interleaved partition: global row y belongs to band (y / band_rows) and */
     int32_t band_count;         /*   is rendered here when band % band_count == band_index; (H, 1, 0) = whole image */
     int32_t band_index;
-    int32_t samples_per_pass;   /* 0 = auto (~16M path slots per pass) */
+    int32_t samples_per_pass;   /* 0 = auto: the largest pass whose path state fits half of the free device memory */
     int32_t flags;              /* RT_OUT_DEVICE | RT_PROFILE | RT_GLOBAL_SCENE */
     void* stream;               /* hipStream_t to run on, or NULL for the scene's own stream */
     double background[3];       /* engine::set_scene(world, background) (engine.h:24-28): returned on a miss */
