@@ -268,18 +268,19 @@ __device__ __forceinline__ void cas(float& ka, int32_t& ca, float& kb, int32_t& 
 
 // Leaf slot test of the LDS scene image (layout.h): the same root selection as hit_sphere on the same f64 values.
 __device__ __forceinline__ bool hit_lds_slot(const uint8_t* lds, uint32_t slot, const Ray<double>& r, double tmin, double tmax,
-                                             double& t, uint32_t& prim) {
+                                             double& t, uint32_t& prim, uint32_t& mt) {
     const double2* sp = reinterpret_cast<const double2*>(lds + kLdsOffSph) + slot;
     const double2 a = sp[0], b = sp[kLdsSlotCap];
     const uint32_t code = reinterpret_cast<const uint32_t*>(lds + kLdsOffRef)[slot];
     V3<double> center{a.x, a.y, b.x};
-    const uint32_t mv = code >> kLdsRefMovShift;
+    const uint32_t mv = (code >> kLdsRefMovShift) & ((1u << (kLdsRefMatShift - kLdsRefMovShift)) - 1);
     if (mv) {
         const double2* mp = reinterpret_cast<const double2*>(lds + kLdsOffMov) + (mv - 1);
         const double2 m0 = mp[0], m1 = mp[kLdsMovCap], m2 = mp[2 * kLdsMovCap];
         center = moving_center(center, V3<double>{m0.x, m0.y, m1.x}, m1.y, m2.x, r.tm);
     }
     prim = make_primref(PRIM_SPHERE, code & kLdsRefIndexMask);
+    mt = code >> kLdsRefMatShift;
     return hit_sphere_at(center, b.y, r, tmin, tmax, t);
 }
 
@@ -289,7 +290,7 @@ template <bool L> using StackT = typename std::conditional<L, int16_t, int32_t>:
 // B: lanes per block (LDS stack stride).  L: nodes and leaf spheres come from the LDS scene image at `lds`.
 template <class R, uint32_t F, int B, bool L>
 __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* lds, int32_t root, const Ray<R>& r, R tmin, R tmax,
-                                         StackT<L>* stk, R& t, uint32_t& prim, uint32_t& face) {
+                                         StackT<L>* stk, R& t, uint32_t& prim, uint32_t& face, uint32_t& mt) {
     const float ox = static_cast<float>(r.o.x), oy = static_cast<float>(r.o.y), oz = static_cast<float>(r.o.z);
     const float ix = 1.0f / static_cast<float>(r.d.x), iy = 1.0f / static_cast<float>(r.d.y), iz = 1.0f / static_cast<float>(r.d.z);
     const float oix = ox * ix, oiy = oy * iy, oiz = oz * iz;
@@ -347,10 +348,10 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
         }
         for (uint32_t k = 0; k < cnt; ++k) {
             R tt;
-            uint32_t fc = 0, ref;
+            uint32_t fc = 0, ref, m = kMatUnknown;
             bool h;
             if constexpr (L) {
-                h = hit_lds_slot(lds, first + k, r, tmin, tmax, tt, ref);
+                h = hit_lds_slot(lds, first + k, r, tmin, tmax, tt, ref, m);
             } else {
                 ref = S.primrefs[first + k];
                 h = hit_prim<R, F>(S, ref, r, tmin, tmax, tt, fc);
@@ -360,6 +361,7 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                 t = tt;
                 prim = ref;
                 face = fc;
+                mt = m;
                 hit = true;
                 tmaxf = f_hi(tt);
             }
@@ -389,7 +391,7 @@ __device__ __forceinline__ Ray<R> xform_in(const ObjRec<R>& o, const Ray<R>& r) 
 // Any non-medium object: prim, BVH, or a translate/rotate_y chain (<= kMaxXformChain) over one of them.
 template <class R, uint32_t F, int B, bool L>
 __device__ __forceinline__ bool hit_object(const DevScene<R>& S, const uint8_t* lds, int32_t oi, Ray<R> r, R tmin, R tmax, StackT<L>* stk,
-                                           R& t, uint32_t& prim, uint32_t& face) {
+                                           R& t, uint32_t& prim, uint32_t& face, uint32_t& mt) {
     if (F & F_XFORM) {
 #pragma unroll
         for (int c = 0; c < kMaxXformChain; ++c) {
@@ -402,9 +404,10 @@ __device__ __forceinline__ bool hit_object(const DevScene<R>& S, const uint8_t* 
     const ObjRec<R>& o = S.objs[oi];
     if (o.kind == OBJ_PRIM) {
         prim = static_cast<uint32_t>(o.a);
+        mt = kMatUnknown;
         return hit_prim<R, F>(S, prim, r, tmin, tmax, t, face);
     }
-    return traverse<R, F, B, L>(S, lds, o.a, r, tmin, tmax, stk, t, prim, face);
+    return traverse<R, F, B, L>(S, lds, o.a, r, tmin, tmax, stk, t, prim, face, mt);
 }
 
 // constant_medium.h:37-82.  Consumes one uniform when the clamped interval is non-empty.
@@ -413,9 +416,9 @@ __device__ __forceinline__ bool hit_medium(const DevScene<R>& S, const uint8_t* 
                                            StackT<L>* stk, uint64_t& rng, R& t) {
     const R inf = R(__builtin_inf());
     R t1, t2;
-    uint32_t p, f;
-    if (!hit_object<R, F, B, L>(S, lds, m.a, r, -inf, inf, stk, t1, p, f)) return false;
-    if (!hit_object<R, F, B, L>(S, lds, m.a, r, t1 + R(0.0001), inf, stk, t2, p, f)) return false;
+    uint32_t p, f, mt;
+    if (!hit_object<R, F, B, L>(S, lds, m.a, r, -inf, inf, stk, t1, p, f, mt)) return false;
+    if (!hit_object<R, F, B, L>(S, lds, m.a, r, t1 + R(0.0001), inf, stk, t2, p, f, mt)) return false;
     if (t1 < tmin) t1 = tmin;
     if (t2 > tmax) t2 = tmax;
     if (t1 >= t2) return false;
@@ -431,6 +434,7 @@ __device__ __forceinline__ bool hit_medium(const DevScene<R>& S, const uint8_t* 
 // The world hittable_list (hittable_list.cpp:5-19): objects in order, t_max = closest so far.
 struct HitOut {
     uint32_t prim, obj;  // obj: world slot | box face << 16
+    uint32_t mt;         // material type when the hit came from the LDS scene image, else kMatUnknown
 };
 template <class R, uint32_t F, int B, bool L>
 __device__ __forceinline__ bool trace_world(const DevScene<R>& S, const uint8_t* lds, const Ray<R>& r, StackT<L>* stk, uint64_t& rng, R& t,
@@ -447,14 +451,16 @@ __device__ __forceinline__ bool trace_world(const DevScene<R>& S, const uint8_t*
                 any = true;
                 h.prim = kMediumHit;
                 h.obj = static_cast<uint32_t>(w);
+                h.mt = kMatUnknown;
             }
         } else {
-            uint32_t prim = 0, face = 0;
-            if (hit_object<R, F, B, L>(S, lds, oi, r, R(0.001), closest, stk, tt, prim, face)) {
+            uint32_t prim = 0, face = 0, mt = kMatUnknown;
+            if (hit_object<R, F, B, L>(S, lds, oi, r, R(0.001), closest, stk, tt, prim, face, mt)) {
                 closest = tt;
                 any = true;
                 h.prim = prim;
                 h.obj = static_cast<uint32_t>(w) | (face << 16);
+                h.mt = mt;
             }
         }
     }

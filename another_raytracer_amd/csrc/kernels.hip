@@ -374,24 +374,28 @@ __global__ __launch_bounds__(L ? kBlockL : kBlock, L ? 1 : ART_EXTEND_MIN_WAVES)
         }
         if (live) {
             R t;
-            HitOut h{0, 0};
+            HitOut h{0, 0, kMatUnknown};
             if (trace_world<R, F, B, L>(S, lds, st.ray, stk, st.rng, t, h)) {
                 w.hits[q] = HitRecD<R>{t, h.prim, h.obj};
-                uint32_t m;
-                if ((F & F_MEDIA) && h.prim == kMediumHit) {
-                    m = static_cast<uint32_t>(S.objs[S.world[h.obj & 0xFFFFu]].b);
-                } else if (F == F_SPHERE) {
-                    m = S.spheres[primref_index(h.prim)].mat;
+                if (L && h.mt != kMatUnknown) {
+                    mtype = static_cast<int>(h.mt);  // from the LDS image: no dependent global loads
                 } else {
-                    const uint32_t idx = primref_index(h.prim);
-                    switch (primref_type(h.prim)) {
-                        case PRIM_SPHERE: m = S.spheres[idx].mat; break;
-                        case PRIM_TRIANGLE: m = S.tris[idx].mat; break;
-                        case PRIM_RECT: m = S.rects[idx].mat; break;
-                        default: m = S.boxes[idx].mat; break;
+                    uint32_t m;
+                    if ((F & F_MEDIA) && h.prim == kMediumHit) {
+                        m = static_cast<uint32_t>(S.objs[S.world[h.obj & 0xFFFFu]].b);
+                    } else if (F == F_SPHERE) {
+                        m = S.spheres[primref_index(h.prim)].mat;
+                    } else {
+                        const uint32_t idx = primref_index(h.prim);
+                        switch (primref_type(h.prim)) {
+                            case PRIM_SPHERE: m = S.spheres[idx].mat; break;
+                            case PRIM_TRIANGLE: m = S.tris[idx].mat; break;
+                            case PRIM_RECT: m = S.rects[idx].mat; break;
+                            default: m = S.boxes[idx].mat; break;
+                        }
                     }
+                    mtype = static_cast<int>(S.mats[m].type);
                 }
-                mtype = static_cast<int>(S.mats[m].type);
                 if (d == 0) store_path(w.paths, q, st);
                 else if (F & F_MEDIA) store_rng(w.paths, q, st.rng);
             } else {  // engine.h:455-456: miss -> background
@@ -596,7 +600,7 @@ static std::vector<uint8_t> lds_scene_image(const FlatScene& f, uint32_t& nmov) 
         const uint32_t sl = static_cast<uint32_t>(slot);
         put(kLdsOffSph + sl * 16, p0, 16);
         put(kLdsOffSph + (kLdsSlotCap + sl) * 16, p1, 16);
-        uint32_t code = idx;
+        uint32_t code = idx | (f.mats[sp.mat].type << kLdsRefMatShift);
         if (sp.flags & SPH_MOVING) {
             const double m0[2] = {sp.d[0], sp.d[1]}, m1[2] = {sp.d[2], sp.t0}, m2[2] = {sp.dt, 0.0};
             put(kLdsOffMov + m * 16, m0, 16);

@@ -90,15 +90,19 @@ constexpr uint32_t kLdsMovCap = 512;    // moving spheres: 3 planes (dx, dy), (d
 constexpr uint32_t kLdsOffNodes = 0;
 constexpr uint32_t kLdsOffSph = kLdsOffNodes + 7 * kLdsNodeCap * 16;
 constexpr uint32_t kLdsOffMov = kLdsOffSph + 2 * kLdsSlotCap * 16;
-constexpr uint32_t kLdsOffRef = kLdsOffMov + 3 * kLdsMovCap * 16;  // u32 per slot: sphere index | (moving index + 1) << 20
+// u32 per slot: sphere index (19 bits) | (moving index + 1) << 19 (10 bits) | material type << 29 (3 bits)
+constexpr uint32_t kLdsOffRef = kLdsOffMov + 3 * kLdsMovCap * 16;
 constexpr uint32_t kLdsImageBytes = kLdsOffRef + kLdsSlotCap * 4;
-constexpr uint32_t kLdsRefMovShift = 20;
+constexpr uint32_t kLdsRefMovShift = 19;
+constexpr uint32_t kLdsRefMatShift = 29;
+constexpr uint32_t kMatUnknown = 0xFFu;  // HitOut::mt when the hit did not come from the LDS image
 // Child codes in the image: inner node n as is, leaf ~((count << 10) | first), empty -1 -- all fit the 16-bit LDS
 // traversal stack entries of this variant (halving the stack is what lets 1024 lanes share one image).
 constexpr uint32_t kLdsLeafShift = 10;
 constexpr uint32_t kLdsLeafMaxCount = 31;
 ART_HD int32_t lds_leaf(uint32_t first, uint32_t count) { return ~static_cast<int32_t>((count << kLdsLeafShift) | first); }
 constexpr uint32_t kLdsRefIndexMask = (1u << kLdsRefMovShift) - 1;
+static_assert(kLdsMovCap + 1 < (1u << (kLdsRefMatShift - kLdsRefMovShift)), "moving index field");
 static_assert(kLdsImageBytes % 16 == 0, "LDS image is copied in 16-B pieces");
 
 // ---------------------------------------------------------------------------------------------- objects
