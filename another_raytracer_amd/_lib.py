@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("ART_LIB") or os.path.join(_HERE, "libart.so")  # ART_
 
 RT_OK = 0
 RT_FP32, RT_FP64 = 0, 1
-RT_OUT_DEVICE, RT_PROFILE, RT_GLOBAL_SCENE = 1, 2, 4
+RT_OUT_DEVICE, RT_PROFILE, RT_GLOBAL_SCENE, RT_SPLIT_SHADE = 1, 2, 4, 8
 ERRORS = {-1: "RT_E_INVALID", -2: "RT_E_SCENE", -3: "RT_E_DEVICE", -4: "RT_E_INTERNAL"}
 
 
@@ -42,7 +42,7 @@ class rt_stats(ctypes.Structure):
                 ("extend_ms", ctypes.c_double), ("shade_ms", ctypes.c_double),
                 ("extend_launches", ctypes.c_uint64), ("shade_launches", ctypes.c_uint64),
                 ("passes", ctypes.c_int32), ("samples_per_pass", ctypes.c_int32), ("local_rows", ctypes.c_int32),
-                ("lds_scene", ctypes.c_int32)]
+                ("extend_variant", ctypes.c_int32)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

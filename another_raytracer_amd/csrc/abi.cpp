@@ -189,7 +189,7 @@ int rt_render(rt_scene* s, const rt_camera* cam, const rt_params* p, uint8_t* ou
             stats->passes = st.passes;
             stats->samples_per_pass = st.samples_per_pass;
             stats->local_rows = st.local_rows;
-            stats->lds_scene = st.lds_scene;
+            stats->extend_variant = st.extend_variant;
         }
         return RT_OK;
     });

@@ -108,6 +108,17 @@ __device__ __forceinline__ void store_path(PathRec<double>* P, uint32_t q, const
     p.g = make_double2(s.T.z, s.L.x);
     p.h = make_double2(s.L.y, s.L.z);
 }
+// throughput and radiance only (line 1 of the f64 record)
+__device__ __forceinline__ void load_tl(const PathRec<float>* P, uint32_t q, PathState<float>& s) {
+    const float4 tl = P[q].tl, lr = P[q].lr;
+    s.T = mk(tl.x, tl.y, tl.z);
+    s.L = mk(tl.w, lr.x, lr.y);
+}
+__device__ __forceinline__ void load_tl(const PathRec<double>* P, uint32_t q, PathState<double>& s) {
+    const double2 f = P[q].f, g = P[q].g, h = P[q].h;
+    s.T = mk(f.x, f.y, g.x);
+    s.L = mk(g.y, h.x, h.y);
+}
 __device__ __forceinline__ void store_rng(PathRec<double>* P, uint32_t q, uint64_t rng) {
     P[q].e.y = __longlong_as_double(static_cast<long long>(rng));
 }
@@ -295,119 +306,6 @@ __device__ __forceinline__ void gen_ray(const PassGeom& g, const CameraRec<R>& c
     st.rng = rng;
 }
 
-#ifndef ART_LDS_BLOCK
-#define ART_LDS_BLOCK 1024
-#endif
-// Blocks of the LDS-scene variant: one block per CU holds the scene image once for 16 waves (4 per SIMD).
-constexpr int kBlockL = ART_LDS_BLOCK;
-
-// Copies the LDS scene image (layout.h) into LDS in one round: every lane issues all of its 16-B loads before its
-// first store, so the block pays one global-load latency instead of one per plane.
-template <int B>
-__device__ __forceinline__ void load_lds_image(const uint8_t* image, uint8_t* lds) {
-    constexpr uint32_t n16 = kLdsImageBytes / 16;
-    constexpr int per = static_cast<int>((n16 + B - 1) / B);
-    const uint4* src = reinterpret_cast<const uint4*>(image);
-    uint4* dst = reinterpret_cast<uint4*>(lds);
-    uint4 v[per];
-#pragma unroll
-    for (int j = 0; j < per; ++j) {
-        const uint32_t i = threadIdx.x + static_cast<uint32_t>(j) * B;
-        if (i < n16) v[j] = src[i];
-    }
-#pragma unroll
-    for (int j = 0; j < per; ++j) {
-        const uint32_t i = threadIdx.x + static_cast<uint32_t>(j) * B;
-        if (i < n16) dst[i] = v[j];
-    }
-}
-
-// L: the scene is LDS-resident (DevScene::lds_image, spheres-only f64): nodes and leaf spheres are read from LDS.
-template <class R, uint32_t F, bool L>
-__global__ __launch_bounds__(L ? kBlockL : kBlock, L ? 1 : ART_EXTEND_MIN_WAVES) void k_extend(DevScene<R> S, PassGeom g, CameraRec<R> cam,
-                                                                                                 Work<R> w, int d) {
-    constexpr int B = L ? kBlockL : kBlock;
-    // dynamic LDS: [scene image (L only)][traversal stack: g.stack entries x B lanes] (sized per scene at launch)
-    extern __shared__ __align__(16) uint8_t smem[];
-    __shared__ uint32_t pre[kShards + 1];
-    const uint8_t* lds = smem;
-    // row 0 of the stack region is this lane's sentinel (device.h traverse), entries start at row 1
-    StackT<L>* stk = reinterpret_cast<StackT<L>*>(smem + (L ? kLdsImageBytes : 0u)) + B + threadIdx.x;
-    stk[-B] = static_cast<StackT<L>>(kNodeEmpty);
-
-    // input: depth 0 = every slot (identity; padding slots are skipped), deeper = the kShards active shards
-    uint32_t count;
-    if (d == 0) {
-        count = g.P;
-    } else {
-        block_prefix(pre, kShards, threadIdx.x < kShards ? *counter(w, d, 0, threadIdx.x) : 0u);
-        count = pre[kShards];
-    }
-    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(w.segments, static_cast<unsigned long long>(d == 0 ? g.live : count));
-    if constexpr (L) {
-        // deep bounces have few paths: blocks without a batch leave before paying for the image
-        if (static_cast<uint64_t>(blockIdx.x) * B >= count) return;
-        load_lds_image<B>(S.lds_image, smem);
-        __syncthreads();
-    }
-    const uint32_t* in = w.active[d & 1];
-    const uint32_t wave = blockIdx.x * (B / 64) + (threadIdx.x >> 6);
-    const uint32_t nwaves = gridDim.x * (B / 64);
-    const int shard = static_cast<int>(wave % kShards);
-    for (uint32_t b = wave; b * 64u < count; b += nwaves) {
-        const uint32_t i = b * 64u + __lane_id();
-        int mtype = -1;
-        uint32_t q = 0;
-        bool live = i < count;
-        PathState<R> st;
-        if (live) {
-            if (d == 0) {
-                q = i;
-                int lx, ly;
-                live = slot_pixel(g, i % g.npix_pad, lx, ly);
-                if (live) gen_ray(g, cam, q, lx, ly, st);
-            } else {
-                const int s = find_segment(pre, kShards, i);
-                q = in[s * g.cap + (i - pre[s])];
-                load_path(w.paths, q, st, false);
-            }
-        }
-        if (live) {
-            R t;
-            HitOut h{0, 0, kMatUnknown};
-            if (trace_world<R, F, B, L>(S, lds, st.ray, stk, st.rng, t, h)) {
-                w.hits[q] = HitRecD<R>{t, h.prim, h.obj};
-                if (L && h.mt != kMatUnknown) {
-                    mtype = static_cast<int>(h.mt);  // from the LDS image: no dependent global loads
-                } else {
-                    uint32_t m;
-                    if ((F & F_MEDIA) && h.prim == kMediumHit) {
-                        m = static_cast<uint32_t>(S.objs[S.world[h.obj & 0xFFFFu]].b);
-                    } else if (F == F_SPHERE) {
-                        m = S.spheres[primref_index(h.prim)].mat;
-                    } else {
-                        const uint32_t idx = primref_index(h.prim);
-                        switch (primref_type(h.prim)) {
-                            case PRIM_SPHERE: m = S.spheres[idx].mat; break;
-                            case PRIM_TRIANGLE: m = S.tris[idx].mat; break;
-                            case PRIM_RECT: m = S.rects[idx].mat; break;
-                            default: m = S.boxes[idx].mat; break;
-                        }
-                    }
-                    mtype = static_cast<int>(S.mats[m].type);
-                }
-                if (d == 0) store_path(w.paths, q, st);
-                else if (F & F_MEDIA) store_rng(w.paths, q, st.rng);
-            } else {  // engine.h:455-456: miss -> background
-                if (d != 0) load_path(w.paths, q, st, true);
-                st.L = st.L + st.T * mk(S.bg[0], S.bg[1], S.bg[2]);
-                store_res(w.res, q, st.L);
-            }
-        }
-        append_by_material(mtype, q, w, g, d, shard);
-    }
-}
-
 // material.h scatter() for one hit of material type M (compile time: one shade kernel per material type, so a wave
 // never carries another material's code or registers); returns false when the path ends here.
 template <class R, uint32_t M, uint32_t TF>
@@ -445,6 +343,155 @@ __device__ __forceinline__ bool scatter(const DevScene<R>& S, const MatRec<R>& m
         return true;
     }
     return false;  // diffuse_light (material.h:106-110)
+}
+
+// Emission + scatter of one hit whose material type is only known at run time (the fused extend variant): the
+// same scatter<R, M, TF> the split k_shade kernels run, dispatched per lane.  Returns true when the path continues
+// (st then holds the scattered ray and the updated throughput).
+template <class R, uint32_t F, uint32_t TF>
+__device__ __forceinline__ bool shade_hit(const DevScene<R>& S, const HitOut& h, R t, bool last, PathState<R>& st) {
+    Surf<R> s;
+    world_surface<R, F, (TF & TF_IMAGE) != 0>(S, h, st.ray, t, s);
+    const MatRec<R>& mat = S.mats[s.mat];
+    const uint32_t mtype = mat.type;
+    if (mtype == MAT_LIGHT) {  // material.h:114-116; diffuse_light never scatters
+        st.L = st.L + st.T * tex_value<R, TF>(S, mat.tex, s.u, s.v, s.p);
+        return false;
+    }
+    if (last) return false;
+    V3<R> att, dir;
+    bool cont;
+    if (mtype == MAT_LAMBERTIAN) cont = scatter<R, MAT_LAMBERTIAN, TF>(S, mat, s, st, att, dir);
+    else if (mtype == MAT_METAL) cont = scatter<R, MAT_METAL, TF>(S, mat, s, st, att, dir);
+    else cont = scatter<R, MAT_DIELECTRIC, TF>(S, mat, s, st, att, dir);
+    if (!cont) return false;
+    st.T = st.T * att;
+    st.ray.o = s.p;
+    st.ray.d = dir;
+    return true;
+}
+
+#ifndef ART_LDS_BLOCK
+#define ART_LDS_BLOCK 1024
+#endif
+// Blocks of the LDS-scene variant: one block per CU holds the scene image once for 16 waves (4 per SIMD).
+constexpr int kBlockL = ART_LDS_BLOCK;
+
+// Copies the LDS scene image (layout.h) into LDS in one round: every lane issues all of its 16-B loads before its
+// first store, so the block pays one global-load latency instead of one per plane.
+template <int B>
+__device__ __forceinline__ void load_lds_image(const uint8_t* image, uint8_t* lds) {
+    constexpr uint32_t n16 = kLdsImageBytes / 16;
+    constexpr int per = static_cast<int>((n16 + B - 1) / B);
+    const uint4* src = reinterpret_cast<const uint4*>(image);
+    uint4* dst = reinterpret_cast<uint4*>(lds);
+    uint4 v[per];
+#pragma unroll
+    for (int j = 0; j < per; ++j) {
+        const uint32_t i = threadIdx.x + static_cast<uint32_t>(j) * B;
+        if (i < n16) v[j] = src[i];
+    }
+#pragma unroll
+    for (int j = 0; j < per; ++j) {
+        const uint32_t i = threadIdx.x + static_cast<uint32_t>(j) * B;
+        if (i < n16) dst[i] = v[j];
+    }
+}
+
+// L: the scene is LDS-resident (DevScene::lds_image, spheres-only f64): nodes and leaf spheres are read from LDS.
+// FUSE (L scenes with solid/checker textures, no media): every hit is shaded in place (shade_hit) and goes straight to
+// the next depth's active queue -- no hit record, no material queues, no k_shade launches, one path-record round trip
+// per bounce.
+template <class R, uint32_t F, bool L, bool FUSE>
+__global__ __launch_bounds__(L ? kBlockL : kBlock, L ? 1 : ART_EXTEND_MIN_WAVES) void k_extend(DevScene<R> S, PassGeom g, CameraRec<R> cam,
+                                                                                                 Work<R> w, int d) {
+    constexpr int B = L ? kBlockL : kBlock;
+    // dynamic LDS: [scene image (L only)][traversal stack: g.stack entries x B lanes] (sized per scene at launch)
+    extern __shared__ __align__(16) uint8_t smem[];
+    __shared__ uint32_t pre[kShards + 1];
+    const uint8_t* lds = smem;
+    // row 0 of the stack region is this lane's sentinel (device.h traverse), entries start at row 1
+    StackT<L>* stk = reinterpret_cast<StackT<L>*>(smem + (L ? kLdsImageBytes : 0u)) + B + threadIdx.x;
+    stk[-B] = static_cast<StackT<L>>(kNodeEmpty);
+
+    // input: depth 0 = every slot (identity; padding slots are skipped), deeper = the kShards active shards
+    uint32_t count;
+    if (d == 0) {
+        count = g.P;
+    } else {
+        block_prefix(pre, kShards, threadIdx.x < kShards ? *counter(w, d, 0, threadIdx.x) : 0u);
+        count = pre[kShards];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(w.segments, static_cast<unsigned long long>(d == 0 ? g.live : count));
+    if constexpr (L) {
+        // deep bounces have few paths: blocks without a batch leave before paying for the image
+        if (static_cast<uint64_t>(blockIdx.x) * B >= count) return;
+        load_lds_image<B>(S.lds_image, smem);
+        __syncthreads();
+    }
+    const uint32_t* in = w.active[d & 1];
+    const uint32_t wave = blockIdx.x * (B / 64) + (threadIdx.x >> 6);
+    const uint32_t nwaves = gridDim.x * (B / 64);
+    const int shard = static_cast<int>(wave % kShards);
+    for (uint32_t b = wave; b * 64u < count; b += nwaves) {
+        const uint32_t i = b * 64u + __lane_id();
+        int mtype = -1;
+        bool cont = false;  // FUSE: the path continues at depth d + 1
+        uint32_t q = 0;
+        bool live = i < count;
+        PathState<R> st;
+        if (live) {
+            if (d == 0) {
+                q = i;
+                int lx, ly;
+                live = slot_pixel(g, i % g.npix_pad, lx, ly);
+                if (live) gen_ray(g, cam, q, lx, ly, st);
+            } else {
+                const int s = find_segment(pre, kShards, i);
+                q = in[s * g.cap + (i - pre[s])];
+                load_path(w.paths, q, st, false);
+            }
+        }
+        if (live) {
+            R t;
+            HitOut h{0, 0, kMatUnknown};
+            if (FUSE && trace_world<R, F, B, L>(S, lds, st.ray, stk, st.rng, t, h)) {
+                if (d != 0) load_tl(w.paths, q, st);
+                cont = shade_hit<R, F, kTexBasic>(S, h, t, d + 1 >= g.max_depth, st);
+                if (cont) store_path(w.paths, q, st);
+                else store_res(w.res, q, st.L);
+            } else if (!FUSE && trace_world<R, F, B, L>(S, lds, st.ray, stk, st.rng, t, h)) {
+                w.hits[q] = HitRecD<R>{t, h.prim, h.obj};
+                if (L && h.mt != kMatUnknown) {
+                    mtype = static_cast<int>(h.mt);  // from the LDS image: no dependent global loads
+                } else {
+                    uint32_t m;
+                    if ((F & F_MEDIA) && h.prim == kMediumHit) {
+                        m = static_cast<uint32_t>(S.objs[S.world[h.obj & 0xFFFFu]].b);
+                    } else if (F == F_SPHERE) {
+                        m = S.spheres[primref_index(h.prim)].mat;
+                    } else {
+                        const uint32_t idx = primref_index(h.prim);
+                        switch (primref_type(h.prim)) {
+                            case PRIM_SPHERE: m = S.spheres[idx].mat; break;
+                            case PRIM_TRIANGLE: m = S.tris[idx].mat; break;
+                            case PRIM_RECT: m = S.rects[idx].mat; break;
+                            default: m = S.boxes[idx].mat; break;
+                        }
+                    }
+                    mtype = static_cast<int>(S.mats[m].type);
+                }
+                if (d == 0) store_path(w.paths, q, st);
+                else if (F & F_MEDIA) store_rng(w.paths, q, st.rng);
+            } else {  // engine.h:455-456: miss -> background
+                if (d != 0) load_path(w.paths, q, st, true);
+                st.L = st.L + st.T * mk(S.bg[0], S.bg[1], S.bg[2]);
+                store_res(w.res, q, st.L);
+            }
+        }
+        if constexpr (FUSE) wave_append(cont, q, w.active[(d + 1) & 1] + static_cast<size_t>(shard) * g.cap, counter(w, d + 1, 0, shard));
+        else append_by_material(mtype, q, w, g, d, shard);
+    }
 }
 
 // Input: the kShards shards of material queue M at depth d (the extend stage sorted hits by material type).
@@ -744,10 +791,11 @@ size_t Renderer::scene_bytes(int fp) const {
 const FlatScene& Renderer::flat() const { return impl_->flat; }
 
 // Persistent extend grid for a given dynamic LDS size: every block the CUs can hold at once.
-template <class R, uint32_t F, bool L>
+template <class R, uint32_t F, bool L, bool FUSE>
 static int extend_blocks(int num_cu, size_t lds) {
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_extend<R, F, L>, L ? kBlockL : kBlock, lds) != hipSuccess || per_cu < 1) per_cu = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_extend<R, F, L, FUSE>, L ? kBlockL : kBlock, lds) != hipSuccess || per_cu < 1)
+        per_cu = 1;
     return per_cu * num_cu;  // num_cu (256) is a multiple of 8: the wave count is a multiple of kShards
 }
 template <class R, uint32_t F, uint32_t M, uint32_t TF>
@@ -769,49 +817,63 @@ static void launch_shade(uint32_t mat_types, bool tex_basic, int num_cu, hipStre
 }
 // One bounce (extend + one shade launch per material type present) of the smallest kernel instantiation that
 // covers the scene's features.
-template <class R, uint32_t F, bool L>
+template <class R, uint32_t F, bool L, bool FUSE>
 static void launch_extend(int num_cu, hipStream_t st, const DevScene<R>& S, const PassGeom& g, const CameraRec<R>& cam, const Work<R>& w, int d) {
     const size_t lds = extend_lds_bytes(L, g.stack);
     static int blocks = 0;
     static size_t blocks_lds = ~size_t(0);
     if (lds != blocks_lds) {
-        if (lds > 64 * 1024) HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_extend<R, F, L>), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                        static_cast<int>(lds)));
-        blocks = extend_blocks<R, F, L>(num_cu, lds);
+        if (lds > 64 * 1024)
+            HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_extend<R, F, L, FUSE>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       static_cast<int>(lds)));
+        blocks = extend_blocks<R, F, L, FUSE>(num_cu, lds);
         blocks_lds = lds;
     }
-    hipLaunchKernelGGL((k_extend<R, F, L>), dim3(blocks), dim3(L ? kBlockL : kBlock), lds, st, S, g, cam, w, d);
+    hipLaunchKernelGGL((k_extend<R, F, L, FUSE>), dim3(blocks), dim3(L ? kBlockL : kBlock), lds, st, S, g, cam, w, d);
 }
-// One bounce (extend + one shade launch per material type present) of the smallest kernel instantiation that
-// covers the scene's features.
+// Extend variant of one bounce: 0 = HBM scene, 1 = LDS scene, 2 = LDS scene with fused shading (no k_shade launches).
+enum ExtendVariant { EXT_GLOBAL = 0, EXT_LDS = 1, EXT_FUSED = 2 };
+
+// One bounce (extend + one shade launch per material type present, unless fused) of the smallest kernel
+// instantiation that covers the scene's features.
 template <class R, uint32_t F>
-static void launch_bounce(uint32_t mat_types, bool tex_basic, bool lds_scene, int num_cu, hipStream_t st, const DevScene<R>& S, const PassGeom& g,
+static void launch_bounce(uint32_t mat_types, bool tex_basic, int variant, int num_cu, hipStream_t st, const DevScene<R>& S, const PassGeom& g,
                           const CameraRec<R>& cam, const Work<R>& w, int d, const std::function<void()>& mark) {
     if (mark) mark();
     if constexpr (F == kFeatSpheres && std::is_same<R, double>::value) {
-        if (lds_scene) launch_extend<R, F, true>(num_cu, st, S, g, cam, w, d);
-        else launch_extend<R, F, false>(num_cu, st, S, g, cam, w, d);
+        if (variant == EXT_FUSED) launch_extend<R, F, true, true>(num_cu, st, S, g, cam, w, d);
+        else if (variant == EXT_LDS) launch_extend<R, F, true, false>(num_cu, st, S, g, cam, w, d);
+        else launch_extend<R, F, false, false>(num_cu, st, S, g, cam, w, d);
     } else {
-        launch_extend<R, F, false>(num_cu, st, S, g, cam, w, d);
+        launch_extend<R, F, false, false>(num_cu, st, S, g, cam, w, d);
     }
     if (mark) mark();
-    launch_shade<R, F, MAT_LAMBERTIAN>(mat_types, tex_basic, num_cu, st, S, g, w, d);
-    launch_shade<R, F, MAT_METAL>(mat_types, tex_basic, num_cu, st, S, g, w, d);
-    launch_shade<R, F, MAT_DIELECTRIC>(mat_types, tex_basic, num_cu, st, S, g, w, d);
-    launch_shade<R, F, MAT_LIGHT>(mat_types, tex_basic, num_cu, st, S, g, w, d);
-    launch_shade<R, F, MAT_ISOTROPIC>(mat_types, tex_basic, num_cu, st, S, g, w, d);
+    if (variant != EXT_FUSED) {
+        launch_shade<R, F, MAT_LAMBERTIAN>(mat_types, tex_basic, num_cu, st, S, g, w, d);
+        launch_shade<R, F, MAT_METAL>(mat_types, tex_basic, num_cu, st, S, g, w, d);
+        launch_shade<R, F, MAT_DIELECTRIC>(mat_types, tex_basic, num_cu, st, S, g, w, d);
+        launch_shade<R, F, MAT_LIGHT>(mat_types, tex_basic, num_cu, st, S, g, w, d);
+        launch_shade<R, F, MAT_ISOTROPIC>(mat_types, tex_basic, num_cu, st, S, g, w, d);
+    }
     if (mark) mark();
 }
+// Extend variant for this scene and these flags (RT_GLOBAL_SCENE / RT_SPLIT_SHADE force the general kernels).
 template <class R>
-static void bounce(const DeviceScene<R>& ds, bool allow_lds, int num_cu, hipStream_t st, const PassGeom& g, const CameraRec<R>& cam, const Work<R>& w, int d,
-                   const std::function<void()>& mark) {
+static int extend_variant(const DeviceScene<R>& ds, int flags) {
+    if (!ds.lds_scene || (flags & RT_GLOBAL_SCENE) || (ds.features & ~kFeatSpheres) != 0) return EXT_GLOBAL;
+    const bool fusable = ds.tex_basic && (ds.mat_types & (1u << MAT_ISOTROPIC)) == 0;
+    return (fusable && !(flags & RT_SPLIT_SHADE)) ? EXT_FUSED : EXT_LDS;
+}
+template <class R>
+static void bounce(const DeviceScene<R>& ds, int variant, int num_cu, hipStream_t st, const PassGeom& g, const CameraRec<R>& cam, const Work<R>& w,
+                   int d, const std::function<void()>& mark) {
     const uint32_t feat = ds.features;
     if ((feat & ~kFeatSpheres) == 0)
-        launch_bounce<R, kFeatSpheres>(ds.mat_types, ds.tex_basic, ds.lds_scene && allow_lds, num_cu, st, ds.view, g, cam, w, d, mark);
+        launch_bounce<R, kFeatSpheres>(ds.mat_types, ds.tex_basic, variant, num_cu, st, ds.view, g, cam, w, d, mark);
     else if ((feat & ~kFeatMesh) == 0)
-        launch_bounce<R, kFeatMesh>(ds.mat_types, ds.tex_basic, false, num_cu, st, ds.view, g, cam, w, d, mark);
+        launch_bounce<R, kFeatMesh>(ds.mat_types, ds.tex_basic, EXT_GLOBAL, num_cu, st, ds.view, g, cam, w, d, mark);
     else
-        launch_bounce<R, F_ALL>(ds.mat_types, ds.tex_basic, false, num_cu, st, ds.view, g, cam, w, d, mark);
+        launch_bounce<R, F_ALL>(ds.mat_types, ds.tex_basic, EXT_GLOBAL, num_cu, st, ds.view, g, cam, w, d, mark);
 }
 
 template <class R>
@@ -895,6 +957,7 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     cam.time0 = R(camd.time0);
     cam.time1 = R(camd.time1);
 
+    const int variant = extend_variant(ds, p.flags);
     const bool prof = (p.flags & RT_PROFILE) != 0;
     std::vector<hipEvent_t> evs;
     for (auto& e : I.ev)
@@ -916,7 +979,7 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
         g.live = g.k * static_cast<uint32_t>(local_pix);
         HIP_OK(hipMemsetAsync(w.counters, 0, 4ull * cnt_words, stream));
         for (int d = 0; d < p.max_depth; ++d)
-            bounce<R>(ds, (p.flags & RT_GLOBAL_SCENE) == 0, I.num_cu, stream, g, cam, w, d, prof ? std::function<void()>(mark) : std::function<void()>());
+            bounce<R>(ds, variant, I.num_cu, stream, g, cam, w, d, prof ? std::function<void()>(mark) : std::function<void()>());
         hipLaunchKernelGGL(k_accum<R>, dim3((g.npix_pad + 255) / 256), dim3(256), 0, stream, g, w);
     }
     HIP_OK(hipGetLastError());
@@ -935,7 +998,7 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     stats.passes = npasses;
     stats.samples_per_pass = static_cast<int>(k);
     stats.segments = segs;
-    stats.lds_scene = (ds.lds_scene && (p.flags & RT_GLOBAL_SCENE) == 0 && (ds.features & ~kFeatSpheres) == 0) ? 1 : 0;
+    stats.extend_variant = variant;
     stats.primary = static_cast<uint64_t>(local_pix) * static_cast<uint64_t>(p.spp);
     if (prof) {
         double ext_ms = 0, sh_ms = 0;

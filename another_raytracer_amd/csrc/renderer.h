@@ -24,7 +24,7 @@ struct RenderStats {
     double ms = 0, extend_ms = 0, shade_ms = 0;
     uint64_t extend_launches = 0, shade_launches = 0;
     int passes = 0, samples_per_pass = 0, local_rows = 0;
-    int lds_scene = 0;
+    int extend_variant = 0;
 };
 
 class Renderer {

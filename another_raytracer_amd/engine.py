@@ -10,7 +10,7 @@ import enum
 
 import numpy as np
 
-from ._lib import RT_FP32, RT_FP64, RT_GLOBAL_SCENE, RT_OUT_DEVICE, RT_PROFILE, check, dvec, lib, rt_camera, rt_params, rt_stats
+from ._lib import RT_FP32, RT_FP64, RT_GLOBAL_SCENE, RT_OUT_DEVICE, RT_PROFILE, RT_SPLIT_SHADE, check, dvec, lib, rt_camera, rt_params, rt_stats
 from .scene import compile_world
 
 
@@ -65,6 +65,8 @@ class engine:
         self.samples_per_pass = int(samples_per_pass)
         # True forces the global-memory extend kernel even when the scene fits the LDS-resident variant (A/B, tests)
         self.global_scene = False
+        # True keeps shading in separate per-material k_shade launches even when it could be fused (A/B, tests)
+        self.split_shade = False
         self.world = None
         self.background = (0.0, 0.0, 0.0)
         self._scene = None
@@ -97,7 +99,8 @@ class engine:
         if self.m == engine_mode.adaptive:
             raise NotImplementedError("engine_mode.adaptive (engine.h:151-333) is SURVEY §8(f) row 1; use single, "
                                       "parallel_stripes or parallel_images (all render every pixel)")
-        flags = (RT_PROFILE if profile else 0) | (RT_GLOBAL_SCENE if self.global_scene else 0)
+        flags = ((RT_PROFILE if profile else 0) | (RT_GLOBAL_SCENE if self.global_scene else 0)
+                 | (RT_SPLIT_SHADE if self.split_shade else 0))
         p = self.params(band_rows, band_count, band_index, flags, stream)
         rows = check(lib.rt_local_rows(ctypes.byref(p), None), "rt_local_rows")
         nbytes = rows * self.width * 3

@@ -51,6 +51,7 @@ def parse():
     ap.add_argument("--samples-per-pass", type=int, default=0)
     ap.add_argument("--no-profile", action="store_true", help="skip per-launch HIP events (no roofline)")
     ap.add_argument("--global-scene", action="store_true", help="force the global-memory extend kernel (A/B vs LDS scene)")
+    ap.add_argument("--split-shade", action="store_true", help="keep per-material k_shade launches (A/B vs fused shading)")
     ap.add_argument("--cpu-baseline-spp", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -120,6 +121,7 @@ def main():
                      samples_per_pass=args.samples_per_pass)
     eng.set_scene(world_scene.objects, world_scene.background)
     eng.global_scene = args.global_scene
+    eng.split_shade = args.split_shade
     rows = band_rows_of(args.height, args.band_rows, world, rank)
     local = torch.empty((len(rows), args.width, 3), dtype=torch.uint8, device=dev)
     profile = not args.no_profile

@@ -50,6 +50,7 @@ extern "C" {
 #define RT_OUT_DEVICE 1     /* out_rgb8 / out_accum are device pointers (on the scene's device) */
 #define RT_PROFILE 2        /* time every extend/shade launch with HIP events (rt_stats.*_ms) */
 #define RT_GLOBAL_SCENE 4   /* never use the LDS-resident scene variant of the extend kernel (A/B and parity tests) */
+#define RT_SPLIT_SHADE 8    /* never fuse shading into the extend kernel: one k_shade launch per material (A/B, tests) */
 
 typedef struct rt_scene rt_scene;
 typedef struct rt_graph rt_graph;
@@ -87,7 +88,8 @@ typedef struct rt_stats {
     double extend_ms, shade_ms; /* RT_PROFILE only: summed launch durations */
     uint64_t extend_launches, shade_launches;
     int32_t passes, samples_per_pass, local_rows;
-    int32_t lds_scene;          /* 1: the extend kernel read the scene from LDS (spheres-only scene that fits), 0: from HBM */
+    int32_t extend_variant;     /* 0: scene read from HBM; 1: LDS-resident scene (spheres-only scene that fits);
+                                   2: LDS-resident scene with shading fused into the extend kernel */
 } rt_stats;
 
 typedef struct rt_scene_info {  /* scene_manager.h:6-14 */

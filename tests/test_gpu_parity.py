@@ -19,13 +19,15 @@ pytestmark = pytest.mark.gpu
 SCENES = ["c1", "1", "2", "3", "4", "5", "6", "7", "8", "cow", "dino"]
 
 
-def gpu_render(scene, W, H, spp, precision="f64", seed=0, band=None, accum=True, global_scene=False):
+def gpu_render(scene, W, H, spp, precision="f64", seed=0, band=None, accum=True, global_scene=False, split_shade=False,
+               max_depth=50):
     world = art.scene_manager().build(scene)
     cam = art.camera(world.lookfrom, world.lookat, (0, 1, 0), world.vfov, W / H, world.aperture, 10.0, 0.0, 1.0)
     eng = art.engine(cam, art.engine_mode.single, width=W, height=H, samples_per_pixel=spp, precision=precision,
-                     seed=seed)
+                     seed=seed, max_depth=max_depth)
     eng.set_scene(world.objects, world.background)
     eng.global_scene = global_scene
+    eng.split_shade = split_shade
     band_rows, band_count, band_index = band or (None, 1, 0)
     rows = H if band is None else len(eng.local_rows(band_rows, band_count, band_index))
     img = np.zeros((rows, W, 3), np.uint8)
@@ -84,17 +86,24 @@ def test_band_partition_is_bit_identical(gpu, precision):
         assert segs == full["segments"]
 
 
-def test_lds_scene_matches_global_scene(gpu):
-    # the benchmark scene qualifies for the LDS-resident extend kernel: it must reproduce the HBM variant bit for bit
+@pytest.mark.parametrize("max_depth", [1, 3, 50])
+def test_extend_variants_are_bit_identical(gpu, max_depth):
+    # the benchmark scene runs the LDS-resident extend kernel with fused shading (variant 2); it must reproduce the
+    # split-shade LDS kernel (1) and the HBM kernel (0) bit for bit, including the last-bounce cut-off
     W, H, spp = 160, 90, 8
-    lds = gpu_render("1", W, H, spp, "f64")
-    glb = gpu_render("1", W, H, spp, "f64", global_scene=True)
-    assert lds["stats"]["lds_scene"] == 1 and glb["stats"]["lds_scene"] == 0
-    assert np.array_equal(lds["acc"], glb["acc"])
-    assert np.array_equal(lds["rgb"], glb["rgb"])
-    assert lds["segments"] == glb["segments"]
-    # scenes with triangles/rects/media (or no BVH) never take it
-    assert gpu_render("cow", 32, 18, 2)["stats"]["lds_scene"] == 0
+    fused = gpu_render("1", W, H, spp, "f64", max_depth=max_depth)
+    split = gpu_render("1", W, H, spp, "f64", split_shade=True, max_depth=max_depth)
+    glb = gpu_render("1", W, H, spp, "f64", global_scene=True, max_depth=max_depth)
+    assert (fused["stats"]["extend_variant"], split["stats"]["extend_variant"], glb["stats"]["extend_variant"]) == (2, 1, 0)
+    for other in (split, glb):
+        assert np.array_equal(fused["acc"], other["acc"])
+        assert np.array_equal(fused["rgb"], other["rgb"])
+        assert fused["segments"] == other["segments"]
+
+
+def test_general_scenes_use_the_hbm_kernels(gpu):
+    # triangles/rects/media (or no BVH) never take the LDS variants
+    assert gpu_render("cow", 32, 18, 2)["stats"]["extend_variant"] == 0
 
 
 def test_statistical_parity_with_reference_config0(gpu):
