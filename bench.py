@@ -32,8 +32,19 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # k_extend algorithmic bytes per segment: queue index 4 + ray (origin, time, direction) + hit record 16
 # + material-queue entry 4.  f32 path record: ray = 32 B; f64: 64 B.
 EXTEND_BYTES = {"f32": 4 + 32 + 16 + 4, "f64": 4 + 64 + 16 + 4}
-# whole-bounce (extend + shade) path-record traffic, SURVEY.md §8(d)'s per-segment figure for this layout
-BOUNCE_BYTES = {"f32": 4 + 32 + 16 + 4 + 4 + 64 + 16 + 64 + 4, "f64": 4 + 64 + 16 + 4 + 4 + 128 + 16 + 128 + 4}
+# Fused variant (extend_variant 2: shading inside k_extend): a non-primary segment reads its queue id and
+# whole path record and, when it continues, writes the record back plus the next queue id; every path ends exactly
+# once with a radiance record.  Depth-0 (primary) segments generate their ray in registers and read nothing.
+PATH_BYTES = {"f32": 64, "f64": 128}
+RES_BYTES = {"f32": 16, "f64": 32}
+
+
+def extend_algorithmic_bytes(precision, variant, segments, primary):
+    """Algorithmic HBM bytes of all k_extend launches of the timed region."""
+    if variant == 2:
+        rec = PATH_BYTES[precision]
+        return (segments - primary) * (4 + rec + rec + 4) + primary * RES_BYTES[precision]
+    return EXTEND_BYTES[precision] * segments
 
 
 def parse():
@@ -80,15 +91,17 @@ def cpu_baseline(args):
             "cpu_model": model, "host_cpus": os.cpu_count()}
 
 
-def latest_traffic(precision, scene):
-    """Per-segment HBM bytes of k_extend from the newest committed PMC summary (profiles/*pmc*.json), or None."""
+def latest_traffic(precision, scene, variant):
+    """Per-segment HBM bytes of k_extend from the newest committed PMC summary (profiles/*pmc*.json) of this extend
+    variant, or None."""
     best = None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
         try:
             d = json.load(open(path))
         except (OSError, ValueError):
             continue
-        if d.get("precision") == precision and str(d.get("scene")) == str(scene) and d.get("extend_bytes_per_segment"):
+        if (d.get("precision") == precision and str(d.get("scene")) == str(scene) and d.get("extend_bytes_per_segment")
+                and d.get("extend_variant", 1) == variant):
             best = d
     return best
 
@@ -138,6 +151,8 @@ def main():
     segs = 0
     ext_ms = shade_ms = gpu_ms = 0.0
     ext_launches = 0
+    primary_segs = 0
+    variant = 0
     frame = None
     for _ in range(args.steps):
         frame, st = step()
@@ -146,18 +161,21 @@ def main():
         shade_ms += st["shade_ms"]
         gpu_ms += st["ms"]
         ext_launches += st["extend_launches"]
+        primary_segs += st["primary"]
+        variant = st["extend_variant"]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    stats = torch.tensor([elapsed, float(segs), ext_ms, shade_ms, float(ext_launches)], dtype=torch.float64, device=dev)
+    stats = torch.tensor([elapsed, float(segs), ext_ms, shade_ms, float(ext_launches), float(primary_segs)],
+                         dtype=torch.float64, device=dev)
     if world > 1:
         t_max = stats[:1].clone()
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
         tot = stats[1:].clone()
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         elapsed = float(t_max.item())
-        segs, ext_ms, shade_ms, ext_launches = (float(x) for x in tot.tolist())
+        segs, ext_ms, shade_ms, ext_launches, primary_segs = (float(x) for x in tot.tolist())
     if rank == 0:
         value = segs / elapsed / 1e6
         primary = args.width * args.height * args.spp * args.steps
@@ -174,17 +192,17 @@ def main():
         }
         if profile and ext_ms > 0:
             per_launch_ms = ext_ms / max(ext_launches, 1)
-            achieved = EXTEND_BYTES[args.precision] * segs / (ext_ms * 1e-3) / 1e9
-            tr = latest_traffic(args.precision, args.scene)
+            alg = extend_algorithmic_bytes(args.precision, variant, segs, primary_segs)
+            achieved = alg / (ext_ms * 1e-3) / 1e9
+            tr = latest_traffic(args.precision, args.scene, variant)
             line["roofline"] = {
                 "bound": "hbm", "kernel": "k_extend", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                 "traffic": (round(tr["extend_bytes_per_segment"] * segs / max(ext_launches, 1)) if tr else None),
-                "algorithmic_bytes_per_segment": EXTEND_BYTES[args.precision],
+                "algorithmic_bytes_per_launch": round(alg / max(ext_launches, 1)),
+                "algorithmic_bytes_per_segment": round(alg / max(segs, 1), 2), "extend_variant": variant,
                 "avg_launch_ms": round(per_launch_ms, 4), "launches": int(ext_launches),
                 "extend_ms_total": round(ext_ms, 2), "shade_ms_total": round(shade_ms, 2),
-                "bounce_bytes_per_segment": BOUNCE_BYTES[args.precision],
-                "bounce_achieved_gbs": round(BOUNCE_BYTES[args.precision] * segs / ((ext_ms + shade_ms) * 1e-3) / 1e9, 2),
             }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args)

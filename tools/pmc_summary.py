@@ -23,7 +23,7 @@ def load(d):
     return out, {k: len(v) for k, v in calls.items()}
 
 
-def main(tag, scene, prec, segments_per_step, root="gpurun_out"):
+def main(tag, scene, prec, segments_per_step, variant=2, root="gpurun_out"):
     base = os.path.join(root, f"pmc_{tag}")
     agg = defaultdict(dict)
     ncalls = {}
@@ -46,7 +46,8 @@ def main(tag, scene, prec, segments_per_step, root="gpurun_out"):
         kernels[short] = e
     ext = {k: v for k, v in kernels.items() if k.startswith("art::k_extend")}
     total = lambda key: sum(v.get(key, 0) for v in ext.values())
-    res = {"tag": tag, "scene": scene, "precision": prec, "segments": segments_per_step, "kernels": kernels,
+    res = {"tag": tag, "scene": scene, "precision": prec, "segments": segments_per_step, "extend_variant": variant,
+           "kernels": kernels,
            "note": "hbm_read_bytes_corrected = 2*FETCH_SIZE*1024 (gfx950 half-count correction), hbm_write_bytes = WRITE_SIZE*1024"}
     if segments_per_step and ext:
         res["extend_bytes_per_segment"] = (total("hbm_read_bytes_corrected") + total("hbm_write_bytes")) / segments_per_step
@@ -61,4 +62,4 @@ def main(tag, scene, prec, segments_per_step, root="gpurun_out"):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]))
+    main(sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]), int(sys.argv[5]) if len(sys.argv) > 5 else 2)
