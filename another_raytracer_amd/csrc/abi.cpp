@@ -157,6 +157,13 @@ int rt_render(rt_scene* s, const rt_camera* cam, const rt_params* p, uint8_t* ou
     std::string why;
     if (!s || !cam) return fail(RT_E_INVALID, "scene and camera must be non-NULL");
     if (!valid_params(p, why)) return fail(RT_E_INVALID, why);
+    if (p->flags & RT_ADAPTIVE) {
+        const int rows = rt_local_rows(p, nullptr);
+        if (p->width % 12 != 0 || rows % 12 != 0 || (p->band_count > 1 && p->band_rows % 12 != 0))
+            return fail(RT_E_INVALID, "for adaptive strategy image size should perfectly fit big square size for now!! (engine.h:178-179: "
+                                      "width and local rows multiples of 12, band_rows a multiple of 12 when bands are interleaved)");
+        if (out_accum) return fail(RT_E_INVALID, "adaptive mode has no per-pixel radiance sums: out_accum must be NULL");
+    }
     return guard(RT_E_DEVICE, [&] {
         if (!s->renderer) s->renderer = std::make_unique<art::Renderer>(s->flat, s->device);
         art::CameraRec<double> c = art::make_camera(cam->lookfrom, cam->lookat, cam->vup, cam->vfov, cam->aspect, cam->aperture,

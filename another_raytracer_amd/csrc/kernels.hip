@@ -177,6 +177,8 @@ struct PassGeom {
     uint32_t stack;             // LDS traversal stack rows per lane (stack_rows)
     int32_t max_depth;
     uint64_t seed;
+    const uint32_t* list;       // pixel-list mode (engine_mode::adaptive levels): slot pixel = list[qi] (local ly*W+lx)
+    uint32_t nlist;             //   for qi < nlist; nullptr = every local pixel in 8x8 tile order
 };
 template <class R>
 struct Work {
@@ -198,6 +200,13 @@ __device__ __forceinline__ int global_row(const PassGeom& g, int ly) {  // row-i
     return (ly / g.band_rows) * (g.band_rows * g.band_count) + g.band_index * g.band_rows + (ly % g.band_rows);
 }
 __device__ __forceinline__ bool slot_pixel(const PassGeom& g, uint32_t qi, int& lx, int& ly) {
+    if (g.list) {
+        if (qi >= g.nlist) return false;
+        const uint32_t p = g.list[qi];
+        ly = static_cast<int>(p / static_cast<uint32_t>(g.W));
+        lx = static_cast<int>(p - static_cast<uint32_t>(ly) * static_cast<uint32_t>(g.W));
+        return true;
+    }
     const uint32_t tile = qi >> 6, within = qi & 63u;
     lx = static_cast<int>((tile % g.tiles_x) * 8 + (within & 7u));
     ly = static_cast<int>((tile / g.tiles_x) * 8 + (within >> 3));
@@ -542,7 +551,8 @@ __global__ __launch_bounds__(256) void k_accum(PassGeom g, Work<R> w) {
     if (qi >= g.npix_pad) return;
     int lx, ly;
     if (!slot_pixel(g, qi, lx, ly)) return;
-    double* a = w.acc + 3 * (static_cast<size_t>(ly) * g.W + lx);
+    // pixel sums: per local pixel, or per list entry in pixel-list mode
+    double* a = w.acc + 3 * (g.list ? static_cast<size_t>(qi) : static_cast<size_t>(ly) * g.W + lx);
     double r = a[0], gg = a[1], b = a[2];
     for (uint32_t j = 0; j < g.k; ++j) {  // sample order == the reference's `pixel_color +=` order
         double x, y, z;
@@ -566,6 +576,141 @@ __global__ void k_finalize(const double* acc, uint8_t* rgb, uint32_t n, int spp)
         x = x < 0.0 ? 0.0 : (x > 0.999 ? 0.999 : x);
         rgb[3 * i + c] = static_cast<uint8_t>(256 * x);
     }
+}
+
+// ------------------------------------------------------------------------------------------------ adaptive mode
+// engine_mode::adaptive (engine.h:96-333) as four traced levels over the local image, whose rows group into 12-px
+// "big squares" (6-px mid and 3-px small squares inside).  Level 0 traces every big square's 4 corners; level L+1
+// traces the new corners (12 per square) of the sub-squares of every level-L square whose corner heuristic fired, and
+// level 3 the 5 remaining pixels of each subdivided small square; k_adapt_fill then interpolates every pixel no level
+// traced from the corners of the deepest square that was not subdivided.  The work image is the reference's int frame
+// (-1 = not yet written); every traced pixel's value depends only on its (pixel, sample) streams, so a corner shared by
+// two levels is traced once.
+constexpr int kBig = 12, kMid = kBig / 2, kSmall = kMid / 2;
+
+// write_color<int> (color.h:6-22) of list entry e's pixel sums into the work image.
+__global__ void k_adapt_store(const uint32_t* list, uint32_t n, const double* acc, int spp, int32_t* work) {
+    const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    const double scale = 1.0 / spp;
+    int32_t* o = work + 3 * static_cast<size_t>(list[e]);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        double x = sqrt(scale * acc[3 * static_cast<size_t>(e) + c]);
+        x = x < 0.0 ? 0.0 : (x > 0.999 ? 0.999 : x);
+        o[c] = static_cast<int32_t>(256 * x);
+    }
+}
+
+// _compute_corners_heuristic (engine.h:96-136): any squared RGB distance between neighbouring corners > 100.
+__device__ __forceinline__ bool adapt_subdivide(const int32_t* work, int W, int x, int y, int L) {
+    const int32_t* c1 = work + 3 * (static_cast<size_t>(y) * W + x);
+    const int32_t* c2 = work + 3 * (static_cast<size_t>(y) * W + x + L - 1);
+    const int32_t* c3 = work + 3 * (static_cast<size_t>(y + L - 1) * W + x);
+    const int32_t* c4 = work + 3 * (static_cast<size_t>(y + L - 1) * W + x + L - 1);
+    auto d = [](const int32_t* a, const int32_t* b) {
+        return (a[0] - b[0]) * (a[0] - b[0]) + (a[1] - b[1]) * (a[1] - b[1]) + (a[2] - b[2]) * (a[2] - b[2]);
+    };
+    return d(c1, c2) > 100 || d(c2, c4) > 100 || d(c4, c3) > 100 || d(c3, c1) > 100;
+}
+
+// Level-0 list: the four corners of every big square (ul, ur, bl, br: engine.h:223-233).
+__global__ void k_adapt_corners(uint32_t* list, int W, int sqx, uint32_t nsq) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nsq) return;
+    const uint32_t x = (s % sqx) * kBig, y = (s / sqx) * kBig;
+    list[4 * s + 0] = y * W + x;
+    list[4 * s + 1] = y * W + x + kBig - 1;
+    list[4 * s + 2] = (y + kBig - 1) * W + x;
+    list[4 * s + 3] = (y + kBig - 1) * W + x + kBig - 1;
+}
+
+// Heuristic of every level-`level` square (0: big, 1: mid, 2: small) whose parent was subdivided, and the list of
+// the pixels the next level traces.  flags[level] holds one byte per square: index big, big*4+mid, (big*4+mid)*4+small.
+__global__ void k_adapt_level(int level, int32_t* work, int W, int sqx, uint32_t nsq, uint8_t* f0, uint8_t* f1, uint8_t* f2, uint32_t* list,
+                              uint32_t* count) {
+    const uint32_t per = level == 0 ? 1u : (level == 1 ? 4u : 16u);
+    const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= nsq * per) return;
+    const uint32_t big = id / per, sub = id % per;
+    int x = static_cast<int>((big % sqx) * kBig), y = static_cast<int>((big / sqx) * kBig);
+    int L = kBig;
+    if (level >= 1) {
+        if (!f0[big]) return;
+        const uint32_t mid = level == 1 ? sub : sub / 4;
+        x += static_cast<int>(mid & 1u) * kMid;
+        y += static_cast<int>(mid >> 1) * kMid;
+        L = kMid;
+        if (level == 2) {
+            if (!f1[big * 4 + mid]) return;
+            x += static_cast<int>(sub & 1u) * kSmall;
+            y += static_cast<int>((sub >> 1) & 1u) * kSmall;
+            L = kSmall;
+        }
+    }
+    const bool split = adapt_subdivide(work, W, x, y, L);
+    (level == 0 ? f0 : (level == 1 ? f1 : f2))[id] = split ? 1 : 0;
+    if (!split) return;
+    if (level < 2) {  // the 16 corners of the 4 sub-squares minus this square's own 4 corners
+        const int h = L / 2;
+        const int xs[4] = {x, x + h - 1, x + h, x + L - 1}, ys[4] = {y, y + h - 1, y + h, y + L - 1};
+        const uint32_t base = atomicAdd(count, 12u);
+        uint32_t k = 0;
+        for (int b = 0; b < 4; ++b)
+            for (int a = 0; a < 4; ++a) {
+                if ((a == 0 || a == 3) && (b == 0 || b == 3)) continue;
+                list[base + k++] = static_cast<uint32_t>(ys[b]) * W + static_cast<uint32_t>(xs[a]);
+            }
+    } else {  // engine.h:268-278: the 5 non-corner pixels of the 3-px square
+        const uint32_t base = atomicAdd(count, 5u);
+        list[base + 0] = static_cast<uint32_t>(y) * W + x + 1;
+        list[base + 1] = static_cast<uint32_t>(y + 1) * W + x;
+        list[base + 2] = static_cast<uint32_t>(y + 1) * W + x + 1;
+        list[base + 3] = static_cast<uint32_t>(y + 1) * W + x + 2;
+        list[base + 4] = static_cast<uint32_t>(y + 2) * W + x + 1;
+    }
+}
+
+// interpolate_square (engine.h:185-219) with _interpolate (engine.h:138-149, v/t == (1/t)*v), then the u8 frame.
+__global__ void k_adapt_fill(int32_t* work, uint8_t* rgb, int W, int rows, int sqx, const uint8_t* f0, const uint8_t* f1, const uint8_t* f2) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= static_cast<uint32_t>(W) * static_cast<uint32_t>(rows)) return;
+    const int x = static_cast<int>(p % W), y = static_cast<int>(p / W);
+    int32_t* o = work + 3 * static_cast<size_t>(p);
+    if (o[0] < 0) {
+        const uint32_t big = static_cast<uint32_t>(y / kBig) * sqx + static_cast<uint32_t>(x / kBig);
+        int x1 = (x / kBig) * kBig, y1 = (y / kBig) * kBig, L = kBig;
+        if (f0[big]) {
+            const uint32_t mid = static_cast<uint32_t>(((y % kBig) / kMid) * 2 + (x % kBig) / kMid);
+            x1 += (x % kBig) / kMid * kMid;
+            y1 += (y % kBig) / kMid * kMid;
+            L = kMid;
+            if (f1[big * 4 + mid]) {
+                x1 += (x % kMid) / kSmall * kSmall;
+                y1 += (y % kMid) / kSmall * kSmall;
+                L = kSmall;
+            }
+        }
+        const int x2 = x1 + L - 1, y2 = y1 + L - 1;
+        const int32_t* q11 = work + 3 * (static_cast<size_t>(y1) * W + x1);
+        const int32_t* q12 = work + 3 * (static_cast<size_t>(y2) * W + x1);
+        const int32_t* q21 = work + 3 * (static_cast<size_t>(y1) * W + x2);
+        const int32_t* q22 = work + 3 * (static_cast<size_t>(y2) * W + x2);
+        const double ix = 1.0 / static_cast<double>(x2 - x1), iy = 1.0 / static_cast<double>(y2 - y1);
+        const double ax = x2 - x, bx = x - x1, ay = y2 - y, by = y - y1;
+        int32_t v[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const double r1 = ix * (ax * static_cast<double>(q11[c])) + ix * (bx * static_cast<double>(q21[c]));
+            const double r2 = ix * (ax * static_cast<double>(q12[c])) + ix * (bx * static_cast<double>(q22[c]));
+            v[c] = static_cast<int32_t>(iy * (ay * r1) + iy * (by * r2));
+        }
+        // written after all three reads: a neighbour never reads this pixel (only corners, which are traced)
+        o[0] = v[0]; o[1] = v[1]; o[2] = v[2];
+    }
+    (void)f2;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) rgb[3 * static_cast<size_t>(p) + c] = static_cast<uint8_t>(o[c]);
 }
 
 // ------------------------------------------------------------------------------------------------ device scene
@@ -934,7 +1079,20 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     const size_t o_seg = off; off += al(sizeof(unsigned long long));
     const size_t o_acc = off; off += al(sizeof(double) * 3 * local_pix);
     const size_t o_rgb = off; off += al(3 * local_pix);
+    // adaptive mode: int work frame, pixel list (<= 80 of every 144 pixels per level), square flags, list counter
+    const bool adapt_ws = (p.flags & RT_ADAPTIVE) != 0;
+    const size_t nsq_ws = adapt_ws ? local_pix / (kBig * kBig) : 0;
+    const size_t o_adw = off; off += adapt_ws ? al(sizeof(int32_t) * 3 * local_pix) : 0;
+    const size_t o_adl = off; off += adapt_ws ? al(4 * local_pix) : 0;
+    const size_t o_adf = off; off += adapt_ws ? al(21 * nsq_ws) : 0;
+    const size_t o_adc = off; off += adapt_ws ? al(4) : 0;
     char* base = static_cast<char*>(I.workspace(off));
+    int32_t* ad_work = reinterpret_cast<int32_t*>(base + o_adw);
+    uint32_t* ad_list = reinterpret_cast<uint32_t*>(base + o_adl);
+    uint8_t* ad_f0 = reinterpret_cast<uint8_t*>(base + o_adf);
+    uint8_t* ad_f1 = ad_f0 + nsq_ws;
+    uint8_t* ad_f2 = ad_f1 + 4 * nsq_ws;
+    uint32_t* ad_count = reinterpret_cast<uint32_t*>(base + o_adc);
 
     Work<R> w{};
     w.paths = reinterpret_cast<PathRec<R>*>(base + o_paths);
@@ -959,50 +1117,93 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
 
     const int variant = extend_variant(ds, p.flags);
     const bool prof = (p.flags & RT_PROFILE) != 0;
+    const bool adaptive = (p.flags & RT_ADAPTIVE) != 0;
+    const int levels = adaptive ? 4 : 1;
     std::vector<hipEvent_t> evs;
     for (auto& e : I.ev)
         if (!e) HIP_OK(hipEventCreate(&e));
-    if (prof) {  // event pool created before the timed region
-        evs.resize(static_cast<size_t>(npasses) * p.max_depth * 3);
+    if (prof) {  // event pool created before the timed region (a pixel-list level never needs more passes than k gives)
+        evs.resize(static_cast<size_t>(levels) * npasses * p.max_depth * 3);
         for (auto& e : evs) HIP_OK(hipEventCreate(&e));
     }
     size_t ev_next = 0;
     auto mark = [&]() { HIP_OK(hipEventRecord(evs[ev_next++], stream)); };
+    int passes_run = 0;
+    // Traces spp samples of every local pixel (list == nullptr) or of every entry of a device pixel list, into
+    // w.acc (per local pixel, or per list entry).
+    auto trace = [&](const uint32_t* list, uint32_t nlist) {
+        g.list = list;
+        g.nlist = nlist;
+        uint32_t kk = k, npix = static_cast<uint32_t>(local_pix);
+        if (list) {
+            npix = nlist;
+            g.npix_pad = (nlist + 63u) & ~63u;
+            kk = std::max<uint32_t>(1, std::min<uint32_t>(static_cast<uint32_t>(p.spp), Pmax / std::max<uint32_t>(g.npix_pad, 64u)));
+        }
+        HIP_OK(hipMemsetAsync(w.acc, 0, sizeof(double) * 3 * npix, stream));
+        for (uint32_t sb = 0; sb < static_cast<uint32_t>(p.spp); sb += kk) {
+            g.sample_base = sb;
+            g.k = std::min<uint32_t>(kk, static_cast<uint32_t>(p.spp) - sb);
+            g.P = g.k * g.npix_pad;
+            g.live = g.k * npix;
+            HIP_OK(hipMemsetAsync(w.counters, 0, 4ull * cnt_words, stream));
+            for (int d = 0; d < p.max_depth; ++d)
+                bounce<R>(ds, variant, I.num_cu, stream, g, cam, w, d, prof ? std::function<void()>(mark) : std::function<void()>());
+            hipLaunchKernelGGL(k_accum<R>, dim3((g.npix_pad + 255) / 256), dim3(256), 0, stream, g, w);
+            ++passes_run;
+        }
+    };
     HIP_OK(hipEventRecord(I.ev[0], stream));
     HIP_OK(hipMemsetAsync(w.segments, 0, sizeof(unsigned long long), stream));
-    HIP_OK(hipMemsetAsync(w.acc, 0, sizeof(double) * 3 * local_pix, stream));
     if (p.max_depth == 0) HIP_OK(hipMemsetAsync(w.res, 0, sizeof(ResRec<R>) * Pmax, stream));  // engine.h:451-452
-    for (int pass = 0; pass < npasses; ++pass) {
-        g.sample_base = static_cast<uint32_t>(pass) * k;
-        g.k = std::min<uint32_t>(k, static_cast<uint32_t>(p.spp) - g.sample_base);
-        g.P = g.k * g.npix_pad;
-        g.live = g.k * static_cast<uint32_t>(local_pix);
-        HIP_OK(hipMemsetAsync(w.counters, 0, 4ull * cnt_words, stream));
-        for (int d = 0; d < p.max_depth; ++d)
-            bounce<R>(ds, variant, I.num_cu, stream, g, cam, w, d, prof ? std::function<void()>(mark) : std::function<void()>());
-        hipLaunchKernelGGL(k_accum<R>, dim3((g.npix_pad + 255) / 256), dim3(256), 0, stream, g, w);
+    uint64_t traced = local_pix;
+    if (!adaptive) {
+        trace(nullptr, 0);
+        const uint32_t npix = static_cast<uint32_t>(local_pix);
+        hipLaunchKernelGGL(k_finalize, dim3((npix + 255) / 256), dim3(256), 0, stream, w.acc, drgb, npix, p.spp);
+    } else {
+        // engine.h:151-333: levels 0..3 (k_adapt_* above); the list sizes come back to the host between levels
+        const int sqx = p.width / kBig;
+        const uint32_t nsq = static_cast<uint32_t>(sqx) * static_cast<uint32_t>(nrows / kBig);
+        HIP_OK(hipMemsetAsync(ad_work, 0xFF, sizeof(int32_t) * 3 * local_pix, stream));  // the reference's -1 frame
+        hipLaunchKernelGGL(k_adapt_corners, dim3((nsq + 255) / 256), dim3(256), 0, stream, ad_list, p.width, sqx, nsq);
+        uint32_t n = 4 * nsq;
+        traced = 0;
+        for (int level = 0;; ++level) {
+            trace(ad_list, n);
+            hipLaunchKernelGGL(k_adapt_store, dim3((n + 255) / 256), dim3(256), 0, stream, ad_list, n, w.acc, p.spp, ad_work);
+            traced += n;
+            if (level == 3) break;
+            const uint32_t per = level == 0 ? 1u : (level == 1 ? 4u : 16u);
+            HIP_OK(hipMemsetAsync(ad_count, 0, 4, stream));
+            hipLaunchKernelGGL(k_adapt_level, dim3((nsq * per + 255) / 256), dim3(256), 0, stream, level, ad_work, p.width, sqx, nsq, ad_f0,
+                               ad_f1, ad_f2, ad_list, ad_count);
+            HIP_OK(hipMemcpyAsync(&n, ad_count, 4, hipMemcpyDeviceToHost, stream));
+            HIP_OK(hipStreamSynchronize(stream));
+            if (n == 0) break;
+        }
+        const uint32_t npix = static_cast<uint32_t>(local_pix);
+        hipLaunchKernelGGL(k_adapt_fill, dim3((npix + 255) / 256), dim3(256), 0, stream, ad_work, drgb, p.width, nrows, sqx, ad_f0, ad_f1, ad_f2);
     }
     HIP_OK(hipGetLastError());
-    const uint32_t npix = static_cast<uint32_t>(local_pix);
-    hipLaunchKernelGGL(k_finalize, dim3((npix + 255) / 256), dim3(256), 0, stream, w.acc, drgb, npix, p.spp);
     HIP_OK(hipEventRecord(I.ev[1], stream));
     const hipMemcpyKind kind_rgb = (p.flags & RT_OUT_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
     if (out_rgb) HIP_OK(hipMemcpyAsync(out_rgb, drgb, 3 * local_pix, kind_rgb, stream));
-    if (out_acc) HIP_OK(hipMemcpyAsync(out_acc, w.acc, sizeof(double) * 3 * local_pix, kind_rgb, stream));
+    if (out_acc && !adaptive) HIP_OK(hipMemcpyAsync(out_acc, w.acc, sizeof(double) * 3 * local_pix, kind_rgb, stream));
     unsigned long long segs = 0;
     HIP_OK(hipMemcpyAsync(&segs, w.segments, sizeof segs, hipMemcpyDeviceToHost, stream));
     HIP_OK(hipStreamSynchronize(stream));
     float ms = 0;
     HIP_OK(hipEventElapsedTime(&ms, I.ev[0], I.ev[1]));
     stats.ms = ms;
-    stats.passes = npasses;
+    stats.passes = passes_run;
     stats.samples_per_pass = static_cast<int>(k);
     stats.segments = segs;
     stats.extend_variant = variant;
-    stats.primary = static_cast<uint64_t>(local_pix) * static_cast<uint64_t>(p.spp);
+    stats.primary = traced * static_cast<uint64_t>(p.spp);
     if (prof) {
         double ext_ms = 0, sh_ms = 0;
-        for (size_t e = 0; e + 2 < evs.size(); e += 3) {
+        for (size_t e = 0; e + 2 < ev_next; e += 3) {
             float a = 0, b = 0;
             HIP_OK(hipEventElapsedTime(&a, evs[e], evs[e + 1]));
             HIP_OK(hipEventElapsedTime(&b, evs[e + 1], evs[e + 2]));
@@ -1011,7 +1212,7 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
         }
         stats.extend_ms = ext_ms;
         stats.shade_ms = sh_ms;
-        stats.extend_launches = static_cast<uint64_t>(npasses) * p.max_depth;
+        stats.extend_launches = static_cast<uint64_t>(passes_run) * p.max_depth;
         stats.shade_launches = stats.extend_launches;
         for (auto e : evs) (void)hipEventDestroy(e);
     }

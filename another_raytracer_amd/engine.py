@@ -10,7 +10,7 @@ import enum
 
 import numpy as np
 
-from ._lib import RT_FP32, RT_FP64, RT_GLOBAL_SCENE, RT_OUT_DEVICE, RT_PROFILE, RT_SPLIT_SHADE, check, dvec, lib, rt_camera, rt_params, rt_stats
+from ._lib import RT_ADAPTIVE, RT_FP32, RT_FP64, RT_GLOBAL_SCENE, RT_OUT_DEVICE, RT_PROFILE, RT_SPLIT_SHADE, check, dvec, lib, rt_camera, rt_params, rt_stats
 from .scene import compile_world
 
 
@@ -92,15 +92,20 @@ class engine:
 
     def run(self, output_image, accum=None, band_rows=None, band_count=1, band_index=0, profile=False, stream=None):
         """Renders into output_image (uint8, local_rows x W x 3).  Returns elapsed ms, or -1 on an empty world
-        (engine.h:32-36).  `accum` (optional, float64 local_rows x W x 3) receives the per-pixel radiance sums."""
+        (engine.h:32-36).  `accum` (optional, float64 local_rows x W x 3) receives the per-pixel radiance sums.
+        engine_mode.adaptive runs _run_adaptive (engine.h:151-333) on the GPU; single / parallel_stripes /
+        parallel_images all trace every pixel (their only differences are the reference's CPU threading)."""
         if self._scene is None:
             print("Invalid input scene!")
             return -1
-        if self.m == engine_mode.adaptive:
-            raise NotImplementedError("engine_mode.adaptive (engine.h:151-333) is SURVEY §8(f) row 1; use single, "
-                                      "parallel_stripes or parallel_images (all render every pixel)")
+        adaptive = self.m == engine_mode.adaptive
+        if adaptive and (self.width % 12 or self.height % 12):
+            # engine.h:178-179
+            raise ValueError("for adaptive strategy image size should perfectly fit big square size for now!!")
+        if adaptive and accum is not None:
+            raise ValueError("engine_mode.adaptive interpolates most pixels: there are no radiance sums to return")
         flags = ((RT_PROFILE if profile else 0) | (RT_GLOBAL_SCENE if self.global_scene else 0)
-                 | (RT_SPLIT_SHADE if self.split_shade else 0))
+                 | (RT_SPLIT_SHADE if self.split_shade else 0) | (RT_ADAPTIVE if adaptive else 0))
         p = self.params(band_rows, band_count, band_index, flags, stream)
         rows = check(lib.rt_local_rows(ctypes.byref(p), None), "rt_local_rows")
         nbytes = rows * self.width * 3

@@ -51,6 +51,11 @@ extern "C" {
 #define RT_PROFILE 2        /* time every extend/shade launch with HIP events (rt_stats.*_ms) */
 #define RT_GLOBAL_SCENE 4   /* never use the LDS-resident scene variant of the extend kernel (A/B and parity tests) */
 #define RT_SPLIT_SHADE 8    /* never fuse shading into the extend kernel: one k_shade launch per material (A/B, tests) */
+#define RT_ADAPTIVE 16      /* engine_mode::adaptive (engine.h:96-333): trace the corners of 12/6/3-px squares, subdivide
+                               where neighbouring corners differ by > 100 (squared gamma-corrected RGB), interpolate
+                               the rest.  Width and local rows must be multiples of 12 (the reference throws
+                               std::logic_error otherwise: RT_E_INVALID here), band_rows a multiple of 12 when
+                               band_count > 1, and out_accum NULL (interpolated pixels have no radiance sums). */
 
 typedef struct rt_scene rt_scene;
 typedef struct rt_graph rt_graph;
@@ -116,7 +121,8 @@ int rt_scene_info_get(const rt_scene* scene, rt_scene_info* info);
 size_t rt_scene_dump(const rt_scene* scene, char* buf, size_t cap);
 void rt_scene_destroy(rt_scene* scene);
 
-/* ---- render (engine::run) ----
+/* ---- render (engine::run; the engine_mode is rt_params.flags & RT_ADAPTIVE: single, parallel_stripes and
+ * parallel_images all compute every pixel and are one mode here) ----
  * out_rgb8: local_rows * width * 3 bytes (row-major, local row 0 = the first row this band set owns, top-most first);
  * out_accum (optional): local_rows * width * 3 f64 radiance sums (pixel_color before write_color).  Host pointers
  * unless RT_OUT_DEVICE.  Blocking. */

@@ -15,8 +15,10 @@
 //
 // Commands:
 //   ref_harness kat N                               first N random_double() of a fresh generator
-//   ref_harness render SCENE W H SPP OUT [single|stripes T]
-//                                                   writes OUT.rgb (u8) and OUT.acc (f64 sums), prints JSON
+//   ref_harness render SCENE W H SPP OUT [single|stripes T|adaptive]
+//                                                   writes OUT.rgb (u8) and OUT.acc (f64 sums; zero in adaptive
+//                                                   mode), prints JSON.  "adaptive" = `_run_adaptive` (engine.h:96-333)
+//                                                   with its 4 stripes run one after another (deterministic)
 //   ref_harness probe SCENE K                       next K random_double() after the scene build (RNG pin)
 //   ref_harness dump SCENE OUT.json                 canonical dump of the scene graph (scene pin)
 //   ref_harness mesh SCENE OUT.bin                  post-triangulation triangle list (f32 xyz*3 + f64 rgb)
@@ -276,8 +278,82 @@ int cmd_render(const std::string& name, int W, int H, int spp, const std::string
         }
     };
 
+    // engine.h:96-333 (_run_adaptive) on reference types, its four stripes run one after another on this thread (the
+    // reference runs them on 4 threads sharing the global RNG, so its own output is not reproducible).
+    auto sample = [&](int i, int j, long long& segs) {
+        color pixel_color(0, 0, 0);
+        for (int s = 0; s < spp; ++s) {
+            auto u = (i + random_double()) / (W - 1);
+            auto v = ((H - 1 - j) + random_double()) / (H - 1);
+            ray r = cam.get_ray(u, v);
+            pixel_color += ray_color(r, world.background, objs, 50, segs);
+        }
+        return pixel_color;
+    };
+    std::vector<int> work(static_cast<size_t>(W) * H * 3, -1);
+    auto px = [&](int i, int j) { return work.data() + 3 * (static_cast<size_t>(j) * W + i); };
+    auto evaluate = [&](int i, int j, long long& segs) { write_color<int>(px(i, j), sample(i, j, segs), spp); };
+    auto corners = [&](int i, int j, int L, long long& segs) {  // engine.h:223-233
+        evaluate(i, j, segs);
+        evaluate(i + L - 1, j, segs);
+        evaluate(i, j + L - 1, segs);
+        evaluate(i + L - 1, j + L - 1, segs);
+    };
+    auto subdivide = [&](int i, int j, int L) {  // engine.h:96-136 _compute_corners_heuristic
+        const int* c1 = px(i, j);
+        const int* c2 = px(i + L - 1, j);
+        const int* c3 = px(i, j + L - 1);
+        const int* c4 = px(i + L - 1, j + L - 1);
+        auto d = [](const int* a, const int* b) { return (a[0] - b[0]) * (a[0] - b[0]) + (a[1] - b[1]) * (a[1] - b[1]) + (a[2] - b[2]) * (a[2] - b[2]); };
+        return d(c1, c2) > 100 || d(c2, c4) > 100 || d(c4, c3) > 100 || d(c3, c1) > 100;
+    };
+    auto interpolate = [&](int i, int j, int L) {  // engine.h:185-219 + _interpolate engine.h:138-149
+        const int x1 = i, x2 = i + L - 1, y1 = j, y2 = j + L - 1;
+        auto col = [&](int x, int y) { const int* p = px(x, y); return color{static_cast<double>(p[0]), static_cast<double>(p[1]), static_cast<double>(p[2])}; };
+        const color Q11 = col(x1, y1), Q12 = col(x1, y2), Q21 = col(x2, y1), Q22 = col(x2, y2);
+        for (int l = 0; l < L; ++l)
+            for (int k = 0; k < L; ++k) {
+                int* p = px(i + k, j + l);
+                if (p[0] >= 0) continue;
+                const int x = i + k, y = j + l;
+                const auto xdiff = x2 - x1;
+                const color R1 = (x2 - x) * Q11 / xdiff + (x - x1) * Q21 / xdiff;
+                const color R2 = (x2 - x) * Q12 / xdiff + (x - x1) * Q22 / xdiff;
+                const auto ydiff = y2 - y1;
+                write_color_raw(p, (y2 - y) * R1 / ydiff + (y - y1) * R2 / ydiff);
+            }
+    };
+    auto run_adaptive = [&](long long& segs) {  // engine.h:236-292 process_square over every 12-px square, row-major
+        for (int j = 0; j < H; j += 12)
+            for (int i = 0; i < W; i += 12) {
+                corners(i, j, 12, segs);
+                if (!subdivide(i, j, 12)) { interpolate(i, j, 12); continue; }
+                for (int l = j; l < j + 12; l += 6)
+                    for (int k = i; k < i + 12; k += 6) {
+                        corners(k, l, 6, segs);
+                        if (!subdivide(k, l, 6)) { interpolate(k, l, 6); continue; }
+                        for (int n = l; n < l + 6; n += 3)
+                            for (int m = k; m < k + 6; m += 3) {
+                                corners(m, n, 3, segs);
+                                if (!subdivide(m, n, 3)) { interpolate(m, n, 3); continue; }
+                                evaluate(m + 1, n, segs);
+                                evaluate(m, n + 1, segs);
+                                evaluate(m + 1, n + 1, segs);
+                                evaluate(m + 2, n + 1, segs);
+                                evaluate(m + 1, n + 2, segs);
+                            }
+                    }
+            }
+        std::transform(work.begin(), work.end(), rgb.begin(), [](int v) { return static_cast<std::uint8_t>(v); });
+    };
+
     const auto start = std::chrono::steady_clock::now();
-    if (mode == "single") {
+    if (mode == "adaptive") {
+        if (W % 12 != 0 || H % 12 != 0) throw std::logic_error("for adaptive strategy image size should perfectly fit big square size for now!!");
+        long long segs = 0;
+        run_adaptive(segs);
+        g_segments += segs;
+    } else if (mode == "single") {
         long long segs = 0;
         for (int j = 0; j < H; ++j) run_row(j, segs);
         g_segments += segs;
@@ -301,7 +377,7 @@ int cmd_render(const std::string& name, int W, int H, int spp, const std::string
     std::ofstream(out + ".rgb", std::ios::binary).write(reinterpret_cast<const char*>(rgb.data()), static_cast<std::streamsize>(rgb.size()));
     std::ofstream(out + ".acc", std::ios::binary).write(reinterpret_cast<const char*>(acc.data()), static_cast<std::streamsize>(acc.size() * sizeof(double)));
     std::printf("{\"scene\":\"%s\",\"W\":%d,\"H\":%d,\"spp\":%d,\"mode\":\"%s\",\"threads\":%d,\"segments\":%lld,\"ms\":%.3f,\"mseg_per_s\":%.6f}\n",
-                name.c_str(), W, H, spp, mode.c_str(), mode == "single" ? 1 : threads, g_segments.load(), ms,
+                name.c_str(), W, H, spp, mode.c_str(), mode == "stripes" ? threads : 1, g_segments.load(), ms,
                 g_segments.load() / (ms * 1e3));
     return 0;
 }

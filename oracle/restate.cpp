@@ -1149,4 +1149,114 @@ int orc_render(const char* scene, int W, int H, int spp, int max_depth, int mode
     return -1;
 }
 
+// engine.h:96-333 (_run_adaptive), the 4 stripes one after another.  ORC_MT replays the reference's draw sequence
+// (a corner shared by two levels is traced again, from the continuing stream); ORC_PCG traces every distinct pixel
+// once (its (pixel, sample) streams would give the same value again), as the GPU does.
+int orc_render_adaptive(const char* scene, int W, int H, int spp, int max_depth, int mode, uint64_t seed, int threads,
+                        uint8_t* rgb_out, long long* segments_out, double* ms_out) try {
+    if (W < 12 || H < 12 || spp < 1 || max_depth < 0) { g_err = "invalid render arguments"; return -2; }
+    if (W % 12 != 0 || H % 12 != 0) { g_err = "for adaptive strategy image size should perfectly fit big square size for now!!"; return -3; }
+    Scene s;
+    Rng scene_rng;
+    build_scene(s, scene, scene_rng);
+    Camera cam(s.lookfrom, s.lookat, V3(0, 1, 0), s.vfov, static_cast<double>(W) / static_cast<double>(H), s.aperture, 10.0, 0.0, 1.0);
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<int> work(static_cast<size_t>(W) * H * 3, -1);
+    std::vector<uint8_t> traced(static_cast<size_t>(W) * H, 0);
+    auto px = [&](int i, int j) { return work.data() + 3 * (static_cast<size_t>(j) * W + i); };
+    auto evaluate = [&](int i, int j, Rng& rng, long long& segs) {  // write_color<int>(pixel, _stochastic_sample(i, j))
+        const size_t p = static_cast<size_t>(j) * W + i;
+        if (mode == ORC_PCG && traced[p]) return;
+        traced[p] = 1;
+        V3 pc(0, 0, 0);
+        for (int sidx = 0; sidx < spp; ++sidx) {
+            if (mode == ORC_PCG) rng.state = pcg_seed(seed, static_cast<uint32_t>(p), static_cast<uint32_t>(sidx));
+            double ru = rng.d();
+            double rv = rng.d();
+            Ray r = cam.get_ray((i + ru) / (W - 1), ((H - 1 - j) + rv) / (H - 1), rng);
+            pc += mode == ORC_PCG ? ray_color_iter(s, r, max_depth, rng, segs) : ray_color_rec(s, r, max_depth, rng, segs);
+        }
+        uint8_t c[3];
+        write_color(c, pc, spp);
+        int* o = px(i, j);
+        o[0] = c[0]; o[1] = c[1]; o[2] = c[2];
+    };
+    auto corners = [&](int i, int j, int L, Rng& rng, long long& segs) {  // engine.h:223-233: ul, ur, bl, br
+        evaluate(i, j, rng, segs);
+        evaluate(i + L - 1, j, rng, segs);
+        evaluate(i, j + L - 1, rng, segs);
+        evaluate(i + L - 1, j + L - 1, rng, segs);
+    };
+    auto subdivide = [&](int i, int j, int L) {  // engine.h:96-136
+        const int *c1 = px(i, j), *c2 = px(i + L - 1, j), *c3 = px(i, j + L - 1), *c4 = px(i + L - 1, j + L - 1);
+        auto d = [](const int* a, const int* b) { return (a[0] - b[0]) * (a[0] - b[0]) + (a[1] - b[1]) * (a[1] - b[1]) + (a[2] - b[2]) * (a[2] - b[2]); };
+        return d(c1, c2) > 100 || d(c2, c4) > 100 || d(c4, c3) > 100 || d(c3, c1) > 100;
+    };
+    auto interpolate = [&](int i, int j, int L) {  // engine.h:185-219, _interpolate engine.h:138-149 (v/t == (1/t)*v)
+        const int x1 = i, x2 = i + L - 1, y1 = j, y2 = j + L - 1;
+        auto col = [&](int x, int y) { const int* p = px(x, y); return V3(p[0], p[1], p[2]); };
+        const V3 Q11 = col(x1, y1), Q12 = col(x1, y2), Q21 = col(x2, y1), Q22 = col(x2, y2);
+        for (int l = 0; l < L; ++l)
+            for (int k = 0; k < L; ++k) {
+                int* p = px(i + k, j + l);
+                if (p[0] >= 0) continue;
+                const int x = i + k, y = j + l;
+                const double xdiff = x2 - x1, ydiff = y2 - y1;
+                const V3 R1 = (x2 - x) * Q11 / xdiff + (x - x1) * Q21 / xdiff;
+                const V3 R2 = (x2 - x) * Q12 / xdiff + (x - x1) * Q22 / xdiff;
+                const V3 c = (y2 - y) * R1 / ydiff + (y - y1) * R2 / ydiff;
+                p[0] = static_cast<int>(c[0]); p[1] = static_cast<int>(c[1]); p[2] = static_cast<int>(c[2]);  // write_color_raw<int>
+            }
+    };
+    auto square = [&](int i, int j, Rng& rng, long long& segs) {  // engine.h:236-292 process_square
+        corners(i, j, 12, rng, segs);
+        if (!subdivide(i, j, 12)) { interpolate(i, j, 12); return; }
+        for (int l = j; l < j + 12; l += 6)
+            for (int k = i; k < i + 12; k += 6) {
+                corners(k, l, 6, rng, segs);
+                if (!subdivide(k, l, 6)) { interpolate(k, l, 6); continue; }
+                for (int n = l; n < l + 6; n += 3)
+                    for (int m = k; m < k + 6; m += 3) {
+                        corners(m, n, 3, rng, segs);
+                        if (!subdivide(m, n, 3)) { interpolate(m, n, 3); continue; }
+                        evaluate(m + 1, n, rng, segs);
+                        evaluate(m, n + 1, rng, segs);
+                        evaluate(m + 1, n + 1, rng, segs);
+                        evaluate(m + 2, n + 1, rng, segs);
+                        evaluate(m + 1, n + 2, rng, segs);
+                    }
+            }
+    };
+    std::atomic<long long> segs_total{0};
+    if (mode == ORC_MT) {
+        long long segs = 0;
+        for (int j = 0; j < H; j += 12)
+            for (int i = 0; i < W; i += 12) square(i, j, scene_rng, segs);
+        segs_total = segs;
+    } else {  // big squares are independent: one row of squares per task
+        int nt = threads > 0 ? threads : static_cast<int>(std::max(1u, std::thread::hardware_concurrency()));
+        std::atomic<int> next{0};
+        std::vector<std::thread> pool;
+        for (int t = 0; t < nt; ++t)
+            pool.emplace_back([&]() {
+                Rng rng;
+                rng.pcg = true;
+                long long segs = 0;
+                for (int j = 12 * next++; j < H; j = 12 * next++)
+                    for (int i = 0; i < W; i += 12) square(i, j, rng, segs);
+                segs_total += segs;
+            });
+        for (auto& th : pool) th.join();
+    }
+    if (rgb_out)
+        for (size_t k = 0; k < work.size(); ++k) rgb_out[k] = static_cast<uint8_t>(work[k]);
+    auto t1 = std::chrono::steady_clock::now();
+    if (segments_out) *segments_out = segs_total.load();
+    if (ms_out) *ms_out = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    return 0;
+} catch (const std::exception& e) {
+    g_err = e.what();
+    return -1;
+}
+
 }  // extern "C"

@@ -37,6 +37,13 @@ int orc_render(const char* scene, int W, int H, int spp, int max_depth, int mode
                int row0, int nrows, int threads, uint8_t* rgb_out, double* acc_out,
                long long* segments_out, double* ms_out);
 
+// engine_mode::adaptive (engine.h:96-333) over the whole WxH image (W, H multiples of 12).  ORC_MT: the
+// reference's draw sequence with its 4 stripes run one after another (bit-exact vs `ref_harness render .. adaptive`);
+// ORC_PCG: the product's streams, every distinct pixel traced once.  rgb_out: H*W*3 u8.  Returns -3 on a size the
+// reference rejects (its std::logic_error).
+int orc_render_adaptive(const char* scene, int W, int H, int spp, int max_depth, int mode, uint64_t seed, int threads,
+                        uint8_t* rgb_out, long long* segments_out, double* ms_out);
+
 const char* orc_last_error(void);
 
 #ifdef __cplusplus

@@ -12,6 +12,8 @@ fixtures pin:
                        scene build incl. BVH-build draws) and the sha256 of the canonical scene dump
   * render_<scene>.npz reference renders (engine_mode::single semantics): RGB8, f64 per-pixel sums and the
                        exact segment count (world.hit calls)
+  * render_adaptive_<scene>.npz  engine_mode::adaptive renders (engine.h:96-333, its 4 stripes run in order):
+                       RGB8 and segment count (`python tests/golden/make_golden.py adaptive` makes only these)
 Assets (assets/*.tris, assets/earthmap.rgb) are the reference's post-triangulation meshes and stb-decoded
 texture bytes, written by the same harness.
 """
@@ -31,6 +33,8 @@ REF = "/root/reference"
 SCENES = ["c1", "1", "2", "3", "4", "5", "6", "7", "8", "cow", "dino"]
 SMALL = (64, 36, 4)          # every scene, RGB + f64 sums + segments
 CONFIG1 = ("c1", 400, 225, 64)  # BASELINE configs[0]: the CPU reference path at full size
+ADAPTIVE = ["c1", "1", "8", "cow"]
+ADAPTIVE_SIZE = (96, 48, 4)     # multiples of the 12-px big square (engine.h:178-179)
 
 
 def run(*args):
@@ -44,9 +48,23 @@ def render(scene, W, H, spp, tmp="/tmp/golden_ref"):
     return rgb, acc, info
 
 
+def adaptive_fixtures():
+    W, H, spp = ADAPTIVE_SIZE
+    for sc in ADAPTIVE:
+        tmp = "/tmp/golden_adaptive"
+        info = json.loads(run("render", sc, W, H, spp, tmp, "adaptive").strip().splitlines()[-1])
+        rgb = np.fromfile(tmp + ".rgb", np.uint8).reshape(H, W, 3)
+        np.savez_compressed(os.path.join(HERE, f"render_adaptive_{sc}_{W}x{H}x{spp}.npz"), rgb=rgb,
+                            segments=np.int64(info["segments"]), W=W, H=H, spp=spp)
+        print("adaptive", sc, info)
+
+
 def main():
     if not os.path.exists(HARNESS):
         sys.exit("build the reference harness first: make -C oracle ref")
+    if sys.argv[1:] == ["adaptive"]:
+        adaptive_fixtures()
+        return
     assets = os.path.join(ROOT, "assets")
     os.makedirs(assets, exist_ok=True)
     run("mesh", "cow", os.path.join(assets, "cow.tris"))
@@ -77,6 +95,7 @@ def main():
     np.savez_compressed(os.path.join(HERE, f"render_{sc}_{W}x{H}x{spp}.npz"), rgb=rgb,
                         acc=acc.astype(np.float64), segments=np.int64(info["segments"]), W=W, H=H, spp=spp)
     print(sc, info)
+    adaptive_fixtures()
 
 
 if __name__ == "__main__":

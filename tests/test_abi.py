@@ -112,3 +112,23 @@ def test_render_without_a_device_fails_loudly():
     eng.set_scene(w.objects, w.background)
     with pytest.raises(art.RTError, match="RT_E_DEVICE"):
         eng.run(np.zeros((4, 8, 3), np.uint8))
+
+
+def test_adaptive_mode_rejects_off_grid_sizes_like_the_reference():
+    """engine.h:178-179 throws std::logic_error off the 12-px grid: RT_E_INVALID here, before any device work."""
+    w = _scene()
+    cam = _lib.rt_camera()
+    st = _lib.rt_stats()
+    for kw in (dict(width=50, height=36), dict(width=48, height=30), dict(width=48, height=48, band_rows=8, band_count=2)):
+        p = _lib.rt_params(spp=1, max_depth=50, band_rows=kw.pop("band_rows", kw["height"]), band_count=kw.pop("band_count", 1),
+                           band_index=0, flags=_lib.RT_ADAPTIVE, **kw)
+        assert _lib.lib.rt_render(w.objects._native, ctypes.byref(cam), ctypes.byref(p), None, None, ctypes.byref(st)) == -1
+        assert b"big square" in _lib.lib.rt_last_error()
+    acc = np.zeros((12, 24, 3), np.float64)
+    p = _lib.rt_params(width=24, height=12, spp=1, max_depth=50, band_rows=12, band_count=1, band_index=0, flags=_lib.RT_ADAPTIVE)
+    assert _lib.lib.rt_render(w.objects._native, ctypes.byref(cam), ctypes.byref(p), None, acc.ctypes.data_as(ctypes.c_void_p),
+                              ctypes.byref(st)) == -1
+    eng = art.engine(art.camera(w.lookfrom, w.lookat, (0, 1, 0), w.vfov, 2.0, 0, 10), art.engine_mode.adaptive, width=50, height=36)
+    eng.set_scene(w.objects, w.background)
+    with pytest.raises(ValueError, match="big square"):
+        eng.run(np.zeros((36, 50, 3), np.uint8))

@@ -82,8 +82,12 @@ def test_python_built_scene_renders_like_the_builtin(gpu):
     assert np.array_equal(imgs[0], imgs[1])
 
 
-def test_adaptive_mode_is_reported_not_silently_replaced(gpu):
-    e = make()
+def test_adaptive_mode_refuses_accum_and_off_grid_sizes(gpu):
+    e = make(W=48, H=36)
     e.m = art.engine_mode.adaptive
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(ValueError):
+        e.run(np.zeros((36, 48, 3), np.uint8), accum=np.zeros((36, 48, 3), np.float64))
+    e = make(W=64, H=40)
+    e.m = art.engine_mode.adaptive
+    with pytest.raises(ValueError, match="big square"):
         e.run(np.zeros((40, 64, 3), np.uint8))

@@ -7,7 +7,7 @@ import os
 import numpy as np
 import pytest
 
-from tests.oracle_lib import REF_HARNESS, oracle_dump, oracle_kat, oracle_probe, oracle_render
+from tests.oracle_lib import REF_HARNESS, oracle_dump, oracle_kat, oracle_probe, oracle_render, oracle_render_adaptive
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 SCENES = ["c1", "1", "2", "3", "4", "5", "6", "7", "8", "cow", "dino"]
@@ -87,3 +87,35 @@ def test_live_reference_other_size(scene, tmp_path):
     o = oracle_render(scene, W, H, spp, mode="mt")
     assert o["segments"] == info["segments"]
     assert np.array_equal(o["rgb"], np.fromfile(tmp_path / "r.rgb", np.uint8).reshape(H, W, 3))
+
+
+ADAPTIVE = ["c1", "1", "8", "cow"]
+
+
+@pytest.mark.parametrize("scene", ADAPTIVE)
+def test_adaptive_mt_bit_exact(scene):
+    """engine_mode::adaptive (engine.h:96-333) restated: bit-exact vs the reference's own adaptive render."""
+    g = np.load(os.path.join(GOLD, f"render_adaptive_{scene}_96x48x4.npz"))
+    o = oracle_render_adaptive(scene, 96, 48, 4, mode="mt")
+    assert o["segments"] == int(g["segments"])
+    assert np.array_equal(o["rgb"], g["rgb"])
+
+
+def test_adaptive_pcg_traces_corners_like_the_full_render():
+    """Big-square corners are always traced: with (pixel, sample)-keyed streams they equal the full render's pixels,
+    and the result does not depend on the thread count."""
+    a = oracle_render_adaptive("1", 48, 36, 3, mode="pcg", threads=1)
+    b = oracle_render_adaptive("1", 48, 36, 3, mode="pcg", threads=4)
+    assert np.array_equal(a["rgb"], b["rgb"]) and a["segments"] == b["segments"]
+    full = oracle_render("1", 48, 36, 3, mode="pcg")
+    for y0 in range(0, 36, 12):
+        for x0 in range(0, 48, 12):
+            for y in (y0, y0 + 11):
+                for x in (x0, x0 + 11):
+                    assert np.array_equal(a["rgb"][y, x], full["rgb"][y, x])
+    assert a["segments"] < full["segments"]
+
+
+def test_adaptive_rejects_sizes_off_the_12px_grid():
+    with pytest.raises(RuntimeError, match="big square"):
+        oracle_render_adaptive("c1", 50, 36, 2)
