@@ -284,6 +284,23 @@ __device__ __forceinline__ bool hit_lds_slot(const uint8_t* lds, uint32_t slot, 
     return hit_sphere_at(center, b.y, r, tmin, tmax, t);
 }
 
+#ifdef ART_STATS
+// Divergence statistics (diagnostic builds only): [0] node-loop wave iterations, [1] node visits (lane sum), [2] leaf-
+// loop wave iterations, [3] leaf tests (lane sum), [4] outer-loop wave iterations, [5] outer iterations (lane sum),
+// [6] traversals, [7] hit_sphere tests with disc >= 0.
+__device__ unsigned long long g_art_stats[16];
+__device__ __forceinline__ void stat_wave(int k) {
+    const uint64_t m = __ballot(true);
+    if (static_cast<int>(__lane_id()) == __ffsll(static_cast<long long>(m)) - 1) atomicAdd(&g_art_stats[k], 1ull);
+}
+__device__ __forceinline__ void stat_lane(int k) { atomicAdd(&g_art_stats[k], 1ull); }
+#define ART_STAT_WAVE(k) stat_wave(k)
+#define ART_STAT_LANE(k) stat_lane(k)
+#else
+#define ART_STAT_WAVE(k)
+#define ART_STAT_LANE(k)
+#endif
+
 // Traversal stack entry: node/leaf codes, 16 bits in the LDS-scene variant (layout.h lds_leaf), 32 bits otherwise.
 template <bool L> using StackT = typename std::conditional<L, int16_t, int32_t>::type;
 
@@ -299,8 +316,13 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
     bool hit = false;
     int sp = 0;
     int32_t node = root;
+    ART_STAT_LANE(6);
     for (;;) {
+        ART_STAT_WAVE(4);
+        ART_STAT_LANE(5);
         while (node >= 0) {
+            ART_STAT_WAVE(0);
+            ART_STAT_LANE(1);
             float4 lx, hx, ly, hy, lz, hz;
             int4 ch;
             if constexpr (L) {
@@ -347,6 +369,8 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
             cnt = leaf_count(node);
         }
         for (uint32_t k = 0; k < cnt; ++k) {
+            ART_STAT_WAVE(2);
+            ART_STAT_LANE(3);
             R tt;
             uint32_t fc = 0, ref, m = kMatUnknown;
             bool h;

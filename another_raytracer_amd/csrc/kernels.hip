@@ -442,6 +442,18 @@ __global__ __launch_bounds__(L ? kBlockL : kBlock, L ? 1 : ART_EXTEND_MIN_WAVES)
     const uint32_t wave = blockIdx.x * (B / 64) + (threadIdx.x >> 6);
     const uint32_t nwaves = gridDim.x * (B / 64);
     const int shard = static_cast<int>(wave % kShards);
+#ifdef ART_STATS
+    unsigned long long tm_load = 0, tm_trace = 0, tm_shade = 0, tm_app = 0, tm_prev = __builtin_amdgcn_s_memtime();
+#define ART_TICK(acc)                                               \
+    do {                                                            \
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  \
+        const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+        acc += now_ - tm_prev;                                      \
+        tm_prev = now_;                                             \
+    } while (0)
+#else
+#define ART_TICK(acc)
+#endif
     for (uint32_t b = wave; b * 64u < count; b += nwaves) {
         const uint32_t i = b * 64u + __lane_id();
         int mtype = -1;
@@ -461,15 +473,27 @@ __global__ __launch_bounds__(L ? kBlockL : kBlock, L ? 1 : ART_EXTEND_MIN_WAVES)
                 load_path(w.paths, q, st, false);
             }
         }
-        if (live) {
+        ART_TICK(tm_load);
+        if (FUSE) {
             R t;
             HitOut h{0, 0, kMatUnknown};
-            if (FUSE && trace_world<R, F, B, L>(S, lds, st.ray, stk, st.rng, t, h)) {
+            const bool hitf = live && trace_world<R, F, B, L>(S, lds, st.ray, stk, st.rng, t, h);
+            ART_TICK(tm_trace);
+            if (hitf) {
                 if (d != 0) load_tl(w.paths, q, st);
                 cont = shade_hit<R, F, kTexBasic>(S, h, t, d + 1 >= g.max_depth, st);
                 if (cont) store_path(w.paths, q, st);
                 else store_res(w.res, q, st.L);
-            } else if (!FUSE && trace_world<R, F, B, L>(S, lds, st.ray, stk, st.rng, t, h)) {
+            } else if (live) {  // engine.h:455-456: miss -> background
+                if (d != 0) load_path(w.paths, q, st, true);
+                st.L = st.L + st.T * mk(S.bg[0], S.bg[1], S.bg[2]);
+                store_res(w.res, q, st.L);
+            }
+            ART_TICK(tm_shade);
+        } else if (live) {
+            R t;
+            HitOut h{0, 0, kMatUnknown};
+            if (trace_world<R, F, B, L>(S, lds, st.ray, stk, st.rng, t, h)) {
                 w.hits[q] = HitRecD<R>{t, h.prim, h.obj};
                 if (L && h.mt != kMatUnknown) {
                     mtype = static_cast<int>(h.mt);  // from the LDS image: no dependent global loads
@@ -500,7 +524,16 @@ __global__ __launch_bounds__(L ? kBlockL : kBlock, L ? 1 : ART_EXTEND_MIN_WAVES)
         }
         if constexpr (FUSE) wave_append(cont, q, w.active[(d + 1) & 1] + static_cast<size_t>(shard) * g.cap, counter(w, d + 1, 0, shard));
         else append_by_material(mtype, q, w, g, d, shard);
+        ART_TICK(tm_app);
     }
+#ifdef ART_STATS
+    if (__lane_id() == 0) {
+        atomicAdd(&g_art_stats[8], tm_load);
+        atomicAdd(&g_art_stats[9], tm_trace);
+        atomicAdd(&g_art_stats[10], tm_shade);
+        atomicAdd(&g_art_stats[11], tm_app);
+    }
+#endif
 }
 
 // Input: the kShards shards of material queue M at depth d (the extend stage sorted hits by material type).
@@ -978,7 +1011,6 @@ static void launch_extend(int num_cu, hipStream_t st, const DevScene<R>& S, cons
 }
 // Extend variant of one bounce: 0 = HBM scene, 1 = LDS scene, 2 = LDS scene with fused shading (no k_shade launches).
 enum ExtendVariant { EXT_GLOBAL = 0, EXT_LDS = 1, EXT_FUSED = 2 };
-
 // One bounce (extend + one shade launch per material type present, unless fused) of the smallest kernel
 // instantiation that covers the scene's features.
 template <class R, uint32_t F>
@@ -1186,6 +1218,21 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
         hipLaunchKernelGGL(k_adapt_fill, dim3((npix + 255) / 256), dim3(256), 0, stream, ad_work, drgb, p.width, nrows, sqx, ad_f0, ad_f1, ad_f2);
     }
     HIP_OK(hipGetLastError());
+#ifdef ART_STATS
+    {
+        unsigned long long st[16] = {0};
+        HIP_OK(hipStreamSynchronize(stream));
+        HIP_OK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_art_stats), sizeof st));
+        std::fprintf(stderr, "ART_STATS node_w %llu node_l %llu (util %.3f) leaf_w %llu leaf_l %llu (util %.3f) outer_w %llu outer_l %llu (util %.3f) "
+                     "traversals %llu nodes/trav %.2f leaftests/trav %.2f\n",
+                     st[0], st[1], st[1] / (64.0 * st[0]), st[2], st[3], st[3] / (64.0 * st[2]), st[4], st[5], st[5] / (64.0 * st[4]), st[6],
+                     double(st[1]) / st[6], double(st[3]) / st[6]);
+        const double tt = double(st[8] + st[9] + st[10] + st[11]);
+        std::fprintf(stderr, "ART_STATS cycles: load %.3f trace %.3f shade %.3f append %.3f\n", st[8] / tt, st[9] / tt, st[10] / tt, st[11] / tt);
+        std::memset(st, 0, sizeof st);
+        HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(g_art_stats), st, sizeof st));
+    }
+#endif
     HIP_OK(hipEventRecord(I.ev[1], stream));
     const hipMemcpyKind kind_rgb = (p.flags & RT_OUT_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
     if (out_rgb) HIP_OK(hipMemcpyAsync(out_rgb, drgb, 3 * local_pix, kind_rgb, stream));
