@@ -376,6 +376,7 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
             bool h;
             if constexpr (L) {
                 h = hit_lds_slot(lds, first + k, r, tmin, tmax, tt, ref, m);
+                fc = first + k;  // the leaf slot travels in the face field (spheres have no face): LDS shading reads it
             } else {
                 ref = S.primrefs[first + k];
                 h = hit_prim<R, F>(S, ref, r, tmin, tmax, tt, fc);

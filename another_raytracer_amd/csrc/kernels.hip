@@ -354,26 +354,69 @@ __device__ __forceinline__ bool scatter(const DevScene<R>& S, const MatRec<R>& m
     return false;  // diffuse_light (material.h:106-110)
 }
 
-// Emission + scatter of one hit whose material type is only known at run time (the fused extend variant): the
-// same scatter<R, M, TF> the split k_shade kernels run, dispatched per lane.  Returns true when the path continues
-// (st then holds the scattered ray and the updated throughput).
-template <class R, uint32_t F, uint32_t TF>
-__device__ __forceinline__ bool shade_hit(const DevScene<R>& S, const HitOut& h, R t, bool last, PathState<R>& st) {
+// Emission + scatter of one hit of the fused extend variant, read entirely from the LDS scene image: the surface
+// (sphere.h:57-63 via the slot's centre/radius/motion planes, which are the f64 values the hit test used) and the
+// material (the image's shading table, layout.h) -- no dependent global loads after a hit.  The arithmetic and the
+// draws are those of prim_surface + scatter<R, M, kTexBasic> (tex_value of a solid or solid/solid checker texture).
+// Returns true when the path continues (st then holds the scattered ray and the updated throughput).
+__device__ __forceinline__ V3<double> lds_mat_color(const uint8_t* lds, uint32_t e) {
+    const double2* m = reinterpret_cast<const double2*>(lds + kLdsOffMat) + 2 * e;
+    const double2 a = m[0], b = m[1];
+    return mk(a.x, a.y, b.x);
+}
+__device__ __forceinline__ bool shade_hit_lds(const uint8_t* lds, uint32_t slot, uint32_t mtype, double t, bool last, PathState<double>& st) {
+    using R = double;
+    const double2* sp = reinterpret_cast<const double2*>(lds + kLdsOffSph) + slot;
+    const double2 a = sp[0], b = sp[kLdsSlotCap];
+    const uint32_t code = reinterpret_cast<const uint32_t*>(lds + kLdsOffRef)[slot];
+    const uint32_t mi = reinterpret_cast<const uint16_t*>(lds + kLdsOffMatIdx)[slot];
+    V3<R> center{a.x, a.y, b.x};
+    const uint32_t mv = (code >> kLdsRefMovShift) & ((1u << (kLdsRefMatShift - kLdsRefMovShift)) - 1);
+    if (mv) {  // moving_sphere.h:72-74, as prim_surface
+        const double2* mp = reinterpret_cast<const double2*>(lds + kLdsOffMov) + (mv - 1);
+        const double2 m0 = mp[0], m1 = mp[kLdsMovCap], m2 = mp[2 * kLdsMovCap];
+        center = center + ((st.ray.tm - m1.y) / m2.x) * V3<R>{m0.x, m0.y, m1.x};
+    }
     Surf<R> s;
-    world_surface<R, F, (TF & TF_IMAGE) != 0>(S, h, st.ray, t, s);
-    const MatRec<R>& mat = S.mats[s.mat];
-    const uint32_t mtype = mat.type;
+    s.p = st.ray.at(t);
+    set_face_normal(s, st.ray, divs(s.p - center, b.y));
+    const uint32_t e = mi & ~kLdsMatChecker;
+    const bool checker = (mi & kLdsMatChecker) != 0;
     if (mtype == MAT_LIGHT) {  // material.h:114-116; diffuse_light never scatters
-        st.L = st.L + st.T * tex_value<R, TF>(S, mat.tex, s.u, s.v, s.p);
+        st.L = st.L + st.T * lds_mat_color(lds, (checker && checker_odd(s.p)) ? e + 1 : e);
         return false;
     }
     if (last) return false;
     V3<R> att, dir;
-    bool cont;
-    if (mtype == MAT_LAMBERTIAN) cont = scatter<R, MAT_LAMBERTIAN, TF>(S, mat, s, st, att, dir);
-    else if (mtype == MAT_METAL) cont = scatter<R, MAT_METAL, TF>(S, mat, s, st, att, dir);
-    else cont = scatter<R, MAT_DIELECTRIC, TF>(S, mat, s, st, att, dir);
-    if (!cont) return false;
+    if (mtype == MAT_LAMBERTIAN) {  // material.h:20-43
+        const V3<R> rv = unit(in_unit_sphere<R>(st.rng));
+        dir = s.n + rv;
+        if (near_zero(dir)) dir = s.n;
+        att = lds_mat_color(lds, (checker && checker_odd(s.p)) ? e + 1 : e);
+    } else if (mtype == MAT_METAL) {  // material.h:45-61
+        const double2* m = reinterpret_cast<const double2*>(lds + kLdsOffMat) + 2 * e;
+        const double2 ma = m[0], mb = m[1];
+        const V3<R> reflected = reflect(unit(st.ray.d), s.n);
+        dir = reflected + mb.y * in_unit_sphere<R>(st.rng);
+        att = mk(ma.x, ma.y, mb.x);
+        if (!(dot(dir, s.n) > R(0))) return false;
+    } else {  // dielectric, material.h:63-99
+        const R ir = (reinterpret_cast<const double2*>(lds + kLdsOffMat) + 2 * e)[1].y;
+        att = mk(R(1), R(1), R(1));
+        const R ratio = s.ff ? (R(1) / ir) : ir;
+        const V3<R> ud = unit(st.ray.d);
+        const R cos_theta = fmin(dot(-ud, s.n), R(1));
+        const R sin_theta = sqrt(R(1) - cos_theta * cos_theta);
+        const bool cannot = ratio * sin_theta > R(1);
+        bool refl = cannot;
+        if (!cannot) {
+            R r0 = (R(1) - ratio) / (R(1) + ratio);
+            r0 = r0 * r0;
+            const R refl_p = r0 + (R(1) - r0) * pow((R(1) - cos_theta), R(5));
+            refl = refl_p > uniform<R>(st.rng);
+        }
+        dir = refl ? reflect(ud, s.n) : refract(ud, s.n, ratio);
+    }
     st.T = st.T * att;
     st.ray.o = s.p;
     st.ray.d = dir;
@@ -481,7 +524,7 @@ __global__ __launch_bounds__(L ? kBlockL : kBlock, L ? 1 : ART_EXTEND_MIN_WAVES)
             ART_TICK(tm_trace);
             if (hitf) {
                 if (d != 0) load_tl(w.paths, q, st);
-                cont = shade_hit<R, F, kTexBasic>(S, h, t, d + 1 >= g.max_depth, st);
+                if constexpr (std::is_same<R, double>::value) cont = shade_hit_lds(lds, h.obj >> 16, h.mt, t, d + 1 >= g.max_depth, st);
                 if (cont) store_path(w.paths, q, st);
                 else store_res(w.res, q, st.L);
             } else if (live) {  // engine.h:455-456: miss -> background
@@ -757,6 +800,7 @@ struct DeviceScene {
     uint32_t mat_types = (1u << kNumMatTypes) - 1;  // bit m: some material of type m exists
     bool tex_basic = false;                          // only solid and checker textures
     bool lds_scene = false;                          // view.lds_image holds the layout.h LDS scene image
+    bool lds_shade = false;                          // ... including a complete shading table (fused variant)
     size_t bytes = 0;
 
     template <class T>
@@ -792,9 +836,10 @@ static size_t extend_lds_bytes(bool L, uint32_t stack) {
 
 // Builds the layout.h LDS scene image when the f64 scene qualifies: spheres only, every BVH node and leaf slot within
 // the plane capacities, and image + stack within one CU's LDS.  Returns an empty vector otherwise.
-static std::vector<uint8_t> lds_scene_image(const FlatScene& f, uint32_t& nmov) {
+static std::vector<uint8_t> lds_scene_image(const FlatScene& f, uint32_t& nmov, bool& shade_ok) {
     std::vector<uint8_t> img;
     nmov = 0;
+    shade_ok = false;
     if ((f.features & ~kFeatSpheres) != 0 || f.nodes.empty() || f.nodes.size() > kLdsNodeCap || f.primrefs.size() > kLdsSlotCap ||
         f.spheres.size() > kLdsRefIndexMask || extend_lds_bytes(true, stack_rows(f.max_stack)) + 4 * (kShards + 1) > kLdsPerCu)
         return img;
@@ -817,6 +862,17 @@ static std::vector<uint8_t> lds_scene_image(const FlatScene& f, uint32_t& nmov) 
             child[c] = (b.child[c] >= 0 || b.child[c] == kNodeEmpty) ? b.child[c] : lds_leaf(leaf_first(b.child[c]), leaf_count(b.child[c]));
         put(kLdsOffNodes + (6 * kLdsNodeCap + static_cast<uint32_t>(n)) * 16, child, 16);
     }
+    // shading table: one entry per material (two for a checker of solid colours); anything else keeps the scene off
+    // the fused variant (shade_ok = false), which shades from the global scene records instead
+    std::vector<int32_t> entry(f.mats.size(), -1);
+    uint32_t nent = 0;
+    shade_ok = true;
+    auto put_entry = [&](const double c[3], double param) {
+        const double v[4] = {c[0], c[1], c[2], param};
+        if (nent < kLdsMatCap) put(kLdsOffMat + nent * 32, v, 32);
+        return nent++;
+    };
+    auto solid = [&](int32_t t) { return t >= 0 && static_cast<size_t>(t) < f.texs.size() && f.texs[t].type == TEX_SOLID; };
     uint32_t m = 0;
     for (size_t slot = 0; slot < f.primrefs.size(); ++slot) {
         const uint32_t idx = primref_index(f.primrefs[slot]);
@@ -835,7 +891,31 @@ static std::vector<uint8_t> lds_scene_image(const FlatScene& f, uint32_t& nmov) 
             ++m;
         }
         put(kLdsOffRef + sl * 4, &code, 4);
+        const auto& mat = f.mats[sp.mat];
+        if (entry[sp.mat] < 0) {
+            const double zero[3] = {0, 0, 0};
+            if (mat.type == MAT_LAMBERTIAN || mat.type == MAT_LIGHT) {
+                const auto& t = f.texs[mat.tex];
+                if (t.type == TEX_SOLID) {
+                    entry[sp.mat] = static_cast<int32_t>(put_entry(t.c, 0.0));
+                } else if (t.type == TEX_CHECKER && solid(t.even) && solid(t.odd)) {
+                    entry[sp.mat] = static_cast<int32_t>(put_entry(f.texs[t.even].c, 0.0)) | static_cast<int32_t>(kLdsMatChecker);
+                    put_entry(f.texs[t.odd].c, 0.0);
+                } else {
+                    shade_ok = false;
+                }
+            } else if (mat.type == MAT_METAL) {
+                entry[sp.mat] = static_cast<int32_t>(put_entry(mat.albedo, mat.fuzz));
+            } else if (mat.type == MAT_DIELECTRIC) {
+                entry[sp.mat] = static_cast<int32_t>(put_entry(zero, mat.ir));
+            } else {
+                shade_ok = false;
+            }
+        }
+        const uint16_t mi = static_cast<uint16_t>(entry[sp.mat] < 0 ? 0 : entry[sp.mat]);
+        put(kLdsOffMatIdx + sl * 2, &mi, 2);
     }
+    if (nent > kLdsMatCap) shade_ok = false;
     return img;
 }
 
@@ -899,10 +979,12 @@ static void build_device_scene(const FlatScene& f, DeviceScene<R>& ds) {
     ds.view.texels = ds.upload(f.texels);
     if (std::is_same<R, double>::value) {
         uint32_t nmov = 0;
-        const std::vector<uint8_t> img = lds_scene_image(f, nmov);
+        bool shade_ok = false;
+        const std::vector<uint8_t> img = lds_scene_image(f, nmov, shade_ok);
         if (!img.empty()) {
             ds.view.lds_image = ds.upload(img);
             ds.lds_scene = true;
+            ds.lds_shade = shade_ok;
         }
     }
     ds.view.nworld = static_cast<int32_t>(f.world.size());
@@ -1038,7 +1120,7 @@ static void launch_bounce(uint32_t mat_types, bool tex_basic, int variant, int n
 template <class R>
 static int extend_variant(const DeviceScene<R>& ds, int flags) {
     if (!ds.lds_scene || (flags & RT_GLOBAL_SCENE) || (ds.features & ~kFeatSpheres) != 0) return EXT_GLOBAL;
-    const bool fusable = ds.tex_basic && (ds.mat_types & (1u << MAT_ISOTROPIC)) == 0;
+    const bool fusable = ds.lds_shade;
     return (fusable && !(flags & RT_SPLIT_SHADE)) ? EXT_FUSED : EXT_LDS;
 }
 template <class R>

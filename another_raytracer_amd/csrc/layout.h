@@ -92,7 +92,14 @@ constexpr uint32_t kLdsOffSph = kLdsOffNodes + 7 * kLdsNodeCap * 16;
 constexpr uint32_t kLdsOffMov = kLdsOffSph + 2 * kLdsSlotCap * 16;
 // u32 per slot: sphere index (19 bits) | (moving index + 1) << 19 (10 bits) | material type << 29 (3 bits)
 constexpr uint32_t kLdsOffRef = kLdsOffMov + 3 * kLdsMovCap * 16;
-constexpr uint32_t kLdsImageBytes = kLdsOffRef + kLdsSlotCap * 4;
+// Shading table (fused variant): u16 per slot = material entry e | kLdsMatChecker, and kLdsMatCap 32-B entries
+// (c.x, c.y), (c.z, param): lambertian / diffuse_light colour (a checker of two solid colours takes entries e = even,
+// e + 1 = odd), metal albedo + fuzz, dielectric (-, -, -, ir).  A hit is then shaded without any global load.
+constexpr uint32_t kLdsOffMatIdx = kLdsOffRef + kLdsSlotCap * 4;
+constexpr uint32_t kLdsMatCap = 512;
+constexpr uint32_t kLdsMatChecker = 0x8000u;
+constexpr uint32_t kLdsOffMat = kLdsOffMatIdx + kLdsSlotCap * 2;
+constexpr uint32_t kLdsImageBytes = kLdsOffMat + kLdsMatCap * 32;
 constexpr uint32_t kLdsRefMovShift = 19;
 constexpr uint32_t kLdsRefMatShift = 29;
 constexpr uint32_t kMatUnknown = 0xFFu;  // HitOut::mt when the hit did not come from the LDS image
