@@ -513,7 +513,9 @@ __global__ __launch_bounds__(L ? kBlockL : kBlock, L ? 1 : ART_EXTEND_MIN_WAVES)
             } else {
                 const int s = find_segment(pre, kShards, i);
                 q = in[s * g.cap + (i - pre[s])];
-                load_path(w.paths, q, st, false);
+                // FUSE: the throughput/radiance line is needed after the traversal; issuing it with the ray line
+                // puts its HBM latency under the traversal instead of after it
+                load_path(w.paths, q, st, FUSE);
             }
         }
         ART_TICK(tm_load);
@@ -523,12 +525,10 @@ __global__ __launch_bounds__(L ? kBlockL : kBlock, L ? 1 : ART_EXTEND_MIN_WAVES)
             const bool hitf = live && trace_world<R, F, B, L>(S, lds, st.ray, stk, st.rng, t, h);
             ART_TICK(tm_trace);
             if (hitf) {
-                if (d != 0) load_tl(w.paths, q, st);
                 if constexpr (std::is_same<R, double>::value) cont = shade_hit_lds(lds, h.obj >> 16, h.mt, t, d + 1 >= g.max_depth, st);
                 if (cont) store_path(w.paths, q, st);
                 else store_res(w.res, q, st.L);
             } else if (live) {  // engine.h:455-456: miss -> background
-                if (d != 0) load_path(w.paths, q, st, true);
                 st.L = st.L + st.T * mk(S.bg[0], S.bg[1], S.bg[2]);
                 store_res(w.res, q, st.L);
             }
