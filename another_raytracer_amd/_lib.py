@@ -79,6 +79,9 @@ SIGNATURES = {
     "rt_tex_checker": (_I, [_P, _I, _I]),
     "rt_tex_noise": (_I, [_P, _D]),
     "rt_tex_image": (_I, [_P, _I, _I, _I, _P]),
+    "rt_tex_bary_image": (_I, [_P, _DP, _I]),
+    "rt_mesh_parse": (_I, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
+    "rt_mesh_build": (_I, [_P, ctypes.c_char_p, _IP]),
     "rt_mat_lambertian": (_I, [_P, _I]),
     "rt_mat_metal": (_I, [_P, _D, _D, _D, _D]),
     "rt_mat_dielectric": (_I, [_P, _D]),

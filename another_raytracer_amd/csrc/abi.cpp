@@ -9,6 +9,7 @@
 
 #include "art.h"
 #include "renderer.h"
+#include "objmesh.h"
 #include "scene.h"
 
 namespace art {
@@ -257,6 +258,31 @@ int rt_tex_image(rt_graph* g, int w, int h, int bpp, const uint8_t* texels) {
         im.data.assign(texels, texels + static_cast<size_t>(w) * h * bpp);
         return g->g.image(std::move(im));
     }()));
+}
+int rt_tex_bary_image(rt_graph* g, const double uv[6], int image_tex) {
+    GRAPH_CALL(([&] {
+        if (!uv) throw std::runtime_error("uv is NULL");
+        check_tex(g, image_tex);
+        if (g->g.textures[image_tex].type != art::TEX_IMAGE) throw std::runtime_error("image_tex must be an rt_tex_image texture");
+        return g->g.bary_image(uv[0], uv[1], uv[2], uv[3], uv[4], uv[5], image_tex);
+    }()));
+}
+int rt_mesh_parse(const char* obj_path, int64_t* triangles, int64_t* shapes) {
+    if (!obj_path) return fail(RT_E_INVALID, "obj_path is NULL");
+    return guard(RT_E_SCENE, [&] {
+        const art::ObjMesh m = art::load_obj(obj_path);
+        if (triangles) *triangles = static_cast<int64_t>(m.tri.size() / 3);
+        if (shapes) *shapes = static_cast<int64_t>(m.shapes);
+        return RT_OK;
+    });
+}
+int rt_mesh_build(rt_graph* g, const char* obj_path, int* first_id) {
+    if (!g || !obj_path) return fail(RT_E_INVALID, "graph/obj_path is NULL");
+    return guard(RT_E_SCENE, [&] {
+        const std::vector<int> ids = art::build_mesh(g->g, art::load_obj(obj_path));
+        if (first_id) *first_id = ids.empty() ? static_cast<int>(g->g.nodes.size()) : ids.front();
+        return static_cast<int>(ids.size());
+    });
 }
 int rt_mat_lambertian(rt_graph* g, int tex) { GRAPH_CALL((check_tex(g, tex), g->g.lambertian(tex))); }
 int rt_mat_metal(rt_graph* g, double r, double gr, double b, double fuzz) { GRAPH_CALL(g->g.metal(art::Vec3(r, gr, b), fuzz)); }

@@ -10,7 +10,10 @@
 #include <limits>
 #include <stdexcept>
 
+#include <zlib.h>
+
 #include "bvh.h"
+#include "objmesh.h"
 
 namespace art {
 
@@ -90,18 +93,26 @@ int SceneGraph::image(Image img) {
     return static_cast<int>(textures.size()) - 1;
 }
 int SceneGraph::image_file(const std::string& path) {
-    std::ifstream f(path, std::ios::binary);
+    // raw texel asset (int32 w, h, bpp + bytes), optionally gzip-compressed (".gz"); gzread passes plain files through
+    gzFile f = gzopen(path.c_str(), "rb");
     if (!f) throw std::runtime_error("cannot open texture asset " + path);
+    auto read = [&](void* dst, size_t n) {
+        return gzread(f, dst, static_cast<unsigned>(n)) == static_cast<int>(n);
+    };
     int32_t hdr[3];
-    f.read(reinterpret_cast<char*>(hdr), sizeof hdr);
     Image img;
+    bool ok = read(hdr, sizeof hdr);
     img.w = hdr[0];
     img.h = hdr[1];
     img.bpp = hdr[2];
-    if (img.w <= 0 || img.h <= 0 || img.bpp < 3) throw std::runtime_error("bad texture asset " + path);
+    if (!ok || img.w <= 0 || img.h <= 0 || img.bpp < 3 || img.w > (1 << 16) || img.h > (1 << 16) || img.bpp > 4) {
+        gzclose(f);
+        throw std::runtime_error("bad texture asset " + path);
+    }
     img.data.resize(static_cast<size_t>(img.w) * img.h * img.bpp);
-    f.read(reinterpret_cast<char*>(img.data.data()), static_cast<std::streamsize>(img.data.size()));
-    if (!f) throw std::runtime_error("truncated texture asset " + path);
+    ok = read(img.data.data(), img.data.size());
+    gzclose(f);
+    if (!ok) throw std::runtime_error("truncated texture asset " + path);
     return image(std::move(img));
 }
 int SceneGraph::bary_image(double ua, double va, double ub, double vb, double uc, double vc, int image_tex) {
@@ -340,22 +351,6 @@ bool SceneGraph::bounding_box(int idx, double time0, double time1, AABBd& out) c
 // ------------------------------------------------------------------------------------------------ recipes
 namespace {
 
-void load_tris(SceneGraph& g, const std::string& path, std::vector<int>& out) {
-    std::ifstream f(path, std::ios::binary);
-    if (!f) throw std::runtime_error("cannot open mesh asset " + path);
-    uint32_t n = 0;
-    f.read(reinterpret_cast<char*>(&n), 4);
-    std::vector<float> p(static_cast<size_t>(n) * 9);
-    f.read(reinterpret_cast<char*>(p.data()), static_cast<std::streamsize>(p.size() * sizeof(float)));
-    if (!f) throw std::runtime_error("truncated mesh asset " + path);
-    for (uint32_t t = 0; t < n; ++t) {
-        const float* q = &p[static_cast<size_t>(t) * 9];
-        // mesh.h:136-141: the OBJ has no materials -> lambertian(color::random()) per triangle
-        int m = g.lambertian_color(g.rng.vec01());
-        out.push_back(g.triangle(Vec3(q[0], q[1], q[2]), Vec3(q[3], q[4], q[5]), Vec3(q[6], q[7], q[8]), m));
-    }
-}
-
 void random_scene(SceneGraph& g) {  // scene_manager.cpp:13-64
     std::vector<int> objects;
     int ground = g.lambertian(g.checker(g.solid(Vec3(0.2, 0.3, 0.1)), g.solid(Vec3(0.9, 0.9, 0.9))));
@@ -461,9 +456,8 @@ void final_scene(SceneGraph& g, const std::string& assets) {  // scene_manager.c
     g.world.push_back(g.translate(g.rotate_y(g.bvh(boxes2), 15), Vec3(-100, 270, 395)));
 }
 
-void mesh_scene(SceneGraph& g, const std::string& tris_path) {  // scene_manager.cpp:236-258
-    std::vector<int> tris;
-    load_tris(g, tris_path, tris);
+void mesh_scene(SceneGraph& g, const std::string& obj_path) {  // scene_manager.cpp:236-258 (SURVEY Q8 for cow/dino)
+    const std::vector<int> tris = build_mesh(g, load_obj(obj_path));  // mesh::parse + mesh::build (mesh.h:31-145)
     g.world.push_back(g.bvh(tris));
     g.world.push_back(g.rect(1, 123, 423, 147, 412, 554, g.diffuse_light(g.solid(Vec3(7, 7, 7)))));
     int boundary = g.sphere(Vec3(0, 0, 0), 5000, g.dielectric(1.5));
@@ -518,13 +512,14 @@ void build_builtin_scene(SceneGraph& g, const std::string& name, const std::stri
         final_scene(g, assets);
         cam(Vec3(478, 278, -600), Vec3(278, 278, 0), 40.0, 0.0, Vec3(0, 0, 0));
     } else if (name == "cow") {
-        mesh_scene(g, assets + "/cow.tris");
+        mesh_scene(g, assets + "/models/cow.obj");
         cam(Vec3(4, 2, 6), Vec3(2, 0, 0), 75.0, 0.0, sky);
     } else if (name == "dino") {
-        mesh_scene(g, assets + "/dino.tris");
+        mesh_scene(g, assets + "/models/dino.obj");
         cam(Vec3(0, 15, 25), Vec3(0, 10, 0), 75.0, 0.0, sky);
-    } else if (name == "9" || name == "mesh") {
-        throw std::runtime_error("scene 9 (textured capsule mesh) needs OBJ/MTL ingestion, not built yet (SURVEY §8(f) row 2)");
+    } else if (name == "9" || name == "mesh") {  // ressources::capsule_obj_path, the stock _mesh_scene
+        mesh_scene(g, assets + "/models/capsule/capsule.obj");
+        cam(Vec3(2, 2, 1), Vec3(0, 0, 0), 75.0, 0.0, sky);
     } else {
         throw std::runtime_error("unkwnown scene requested: " + name);  // scene_manager.cpp:351 wording
     }
@@ -550,8 +545,9 @@ uint64_t fnv1a(const uint8_t* p, size_t n) {
 
 struct Dumper {
     const SceneGraph& g;
-    std::string tex(int ti) const {
-        const Texture& t = g.textures[ti];
+    mutable std::vector<std::string> image_dump;  // per image: its dump (the texel hash is computed once)
+    std::string tex(int ti) const { return tex_rec(g.textures[ti]); }
+    std::string tex_rec(const Texture& t) const {
         switch (t.type) {
             case TEX_SOLID: return "{\"type\":\"solid\",\"c\":" + V(t.c) + "}";
             case TEX_CHECKER: return "{\"type\":\"checker\",\"even\":" + tex(t.even) + ",\"odd\":" + tex(t.odd) + "}";
@@ -567,13 +563,24 @@ struct Dumper {
                 return r + "],\"perm_x\":" + perm(p.perm[0]) + ",\"perm_y\":" + perm(p.perm[1]) + ",\"perm_z\":" + perm(p.perm[2]) + "}";
             }
             case TEX_IMAGE: {
-                const Image& im = g.images[t.image];
-                char h[32];
-                std::snprintf(h, sizeof h, "%016llx", static_cast<unsigned long long>(fnv1a(im.data.data(), im.data.size())));
-                return "{\"type\":\"image\",\"w\":" + std::to_string(im.w) + ",\"h\":" + std::to_string(im.h) + ",\"bpp\":" +
-                       std::to_string(im.bpp) + ",\"fnv1a\":\"" + h + "\"}";
+                if (image_dump.size() < g.images.size()) image_dump.resize(g.images.size());
+                std::string& s = image_dump[static_cast<size_t>(t.image)];
+                if (s.empty()) {
+                    const Image& im = g.images[t.image];
+                    char h[32];
+                    std::snprintf(h, sizeof h, "%016llx", static_cast<unsigned long long>(fnv1a(im.data.data(), im.data.size())));
+                    s = "{\"type\":\"image\",\"w\":" + std::to_string(im.w) + ",\"h\":" + std::to_string(im.h) + ",\"bpp\":" +
+                        std::to_string(im.bpp) + ",\"fnv1a\":\"" + h + "\"}";
+                }
+                return s;
             }
-            case TEX_BARY_IMAGE: return "{\"type\":\"bary_image\"}";
+            case TEX_BARY_IMAGE: {  // oracle/ref_harness dump_texture schema
+                Texture img;
+                img.type = TEX_IMAGE;
+                img.image = t.image;
+                return "{\"type\":\"bary_image\",\"a\":[" + D(t.uv[0]) + "," + D(t.uv[1]) + "],\"b\":[" + D(t.uv[2]) + "," + D(t.uv[3]) +
+                       "],\"c\":[" + D(t.uv[4]) + "," + D(t.uv[5]) + "],\"tex\":" + tex_rec(img) + "}";
+            }
         }
         return "{}";
     }
@@ -641,7 +648,7 @@ struct Dumper {
 }  // namespace
 
 std::string dump_scene(const SceneGraph& g) {
-    Dumper d{g};
+    Dumper d{g, {}};
     std::string r = "{\"lookfrom\":" + V(g.lookfrom) + ",\"lookat\":" + V(g.lookat) + ",\"vfov\":" + D(g.vfov) + ",\"aperture\":" + D(g.aperture) +
                     ",\"background\":" + V(g.background) + ",\"objects\":[";
     for (size_t i = 0; i < g.world.size(); ++i) r += (i ? ",\n" : "\n") + d.obj(g.world[i]);

@@ -2,6 +2,7 @@
 
 * `scene_manager().build(alias)` == scene_manager::build (src/scene_manager.cpp:260-355), plus the build-defined
   scenes "c1"  and "cow"/"dino" (SURVEY Q8).
+* `mesh().parse(path)` / `.build()` == the reference's OBJ/MTL mesh class (src/primitives/mesh.h:29-145).
 * The hittable / material / texture classes take the reference constructors' arguments.  Like the reference,
   which draws from ONE process-wide std::mt19937 (src/utils/tracer_utils.h:27-31), they all record into one
   process-wide native graph whose generator draws in construction order: `noise_texture` (perlin tables,
@@ -90,6 +91,14 @@ class image_texture(texture):  # texture.h:67-118
         data = np.ascontiguousarray(data)
         h, w, c = data.shape
         self.id = check(lib.rt_tex_image(_g(), w, h, c, data.ctypes.data_as(ctypes.c_void_p)), "image_texture")
+
+
+class barycentric_image_texture(texture):  # texture.h:135-154
+    def __init__(self, a, b, c, tex):
+        if not isinstance(tex, image_texture):
+            raise TypeError("barycentric_image_texture samples an image_texture")
+        uv = (ctypes.c_double * 6)(*[float(x) for x in (*a, *b, *c)])
+        self.id = check(lib.rt_tex_bary_image(_g(), uv, tex.id), "barycentric_image_texture")
 
 
 # ------------------------------------------------------------------------------------------------ materials
@@ -201,6 +210,35 @@ class bvh_node(hittable):  # bvh.h / bvh.cpp (draws its random_int(0,2) per node
     def __init__(self, objects, time0=0.0, time1=1.0):
         items = objects.objects if isinstance(objects, hittable_list) else list(objects)
         self.id = check(lib.rt_obj_bvh(_g(), len(items), _ids(items)), "bvh_node")
+
+
+class mesh:  # primitives/mesh.h:29-145
+    """Wavefront OBJ (+ MTL) triangle mesh.  parse() validates and counts like mesh::parse; build() adds one triangle per
+    post-triangulation face to the shared graph (drawing color::random() per triangle when the OBJ has no material
+    library, exactly as mesh::build) and returns them as a hittable_list."""
+
+    def __init__(self):
+        self.path = None
+        self.triangles = self.shapes = 0
+
+    def parse(self, mesh_path):
+        t, sh = ctypes.c_int64(), ctypes.c_int64()
+        if lib.rt_mesh_parse(os.fspath(mesh_path).encode(), ctypes.byref(t), ctypes.byref(sh)) < 0:
+            return False  # mesh.h:33-40 reports the error and returns false
+        self.path, self.triangles, self.shapes = os.fspath(mesh_path), t.value, sh.value
+        return True
+
+    def build(self):
+        if self.path is None:
+            raise RuntimeError("mesh::build before a successful parse")
+        first = ctypes.c_int()
+        n = check(lib.rt_mesh_build(_g(), self.path.encode(), ctypes.byref(first)), "mesh.build")
+        out = hittable_list()
+        for i in range(n):
+            h = hittable()
+            h.id = first.value + i
+            out.add(h)
+        return out
 
 
 class translate(hittable):  # hittable.cpp:3-23

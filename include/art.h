@@ -18,6 +18,8 @@
  *   hittable constructors (sphere.h, moving_sphere.h, triangle.h, rt_graph_* (one call per constructor, same
  *     aarect.h, box.h, hittable_list.h, bvh.h, hittable.h,          arguments); rt_graph_compile -> rt_scene
  *     constant_medium.h, material.h, texture.h)
+ *   bool mesh::parse(path)                    mesh.h:31-65        rt_mesh_parse(path, &triangles, &shapes)
+ *   hittable_list mesh::build()               mesh.h:67-145       rt_mesh_build(graph, path, &first_id)
  *
  * RNG contract: the reference draws from one global std::mt19937 (tracer_utils.h:27-31).  Scene construction here
  * replays that generator exactly (seed 5489, same draw order), so scenes are bit-identical.  Rendering draws come
@@ -114,7 +116,8 @@ int rt_device_count(void);
 /* ---- scenes ---- */
 /* Builtin scenes = scene_manager::build(alias): "1".."8" or "random", "two_spheres", "two_perlin_spheres", "earth",
  * "simple_light", "cornell_box", "cornell_smoke", "final"; plus "c1" (SURVEY Q7 3-sphere scene), "cow", "dino"
- * (SURVEY Q8 mesh scenes).  asset_dir holds cow.tris, dino.tris, earthmap.rgb. */
+ * (SURVEY Q8 mesh scenes) and "9"/"mesh" (the capsule, the reference's default scene).  asset_dir holds earthmap.rgb
+ * and models/{cow.obj, dino.obj, capsule/capsule.obj + .mtl + capsule.rgb.gz}. */
 int rt_scene_build(const char* name, const char* asset_dir, int device, rt_scene** out);
 int rt_scene_info_get(const rt_scene* scene, rt_scene_info* info);
 /* Canonical JSON of the scene graph (schema of oracle/ref_harness `dump`); returns the size needed incl. NUL. */
@@ -140,6 +143,8 @@ int rt_tex_solid(rt_graph* g, double r, double gr, double b);       /* texture.h
 int rt_tex_checker(rt_graph* g, int even, int odd);                 /* texture.h:31-50 */
 int rt_tex_noise(rt_graph* g, double scale);                        /* texture.h:52-65 */
 int rt_tex_image(rt_graph* g, int w, int h, int bpp, const uint8_t* texels); /* texture.h:67-118 */
+/* barycentric_image_texture(a, b, c, image) (texture.h:135-154): uv = {ua, va, ub, vb, uc, vc}; image_tex from rt_tex_image */
+int rt_tex_bary_image(rt_graph* g, const double uv[6], int image_tex);
 int rt_mat_lambertian(rt_graph* g, int tex);                        /* material.h:20-43 */
 int rt_mat_metal(rt_graph* g, double r, double gr, double b, double fuzz); /* material.h:45-61 */
 int rt_mat_dielectric(rt_graph* g, double ir);                      /* material.h:63-99 */
@@ -158,6 +163,15 @@ int rt_graph_add_world(rt_graph* g, int obj);                                   
 int rt_graph_clear_world(rt_graph* g);
 int rt_graph_set_view(rt_graph* g, const double lookfrom[3], const double lookat[3], double vfov, double aperture,
                       const double background[3]);
+/* ---- meshes (Wavefront OBJ + MTL, rapidobj v1.0.1 semantics: objmesh.h) ----
+ * rt_mesh_parse = mesh::parse: parses and triangulates; reports the triangle and shape counts (either may be NULL).
+ * rt_mesh_build = mesh::parse + mesh::build into the graph: one triangle per post-triangulation face with
+ *   lambertian(color::random()) (no MTL; draws from the graph's generator), lambertian(Ka + Kd), or
+ *   lambertian(barycentric_image_texture) for a map_Kd material, whose texels are read from the pre-decoded asset
+ *   <map stem>.rgb.gz or .rgb next to the MTL (JPEG decoding is not part of this library).  The triangle ids are
+ *   *first_id .. *first_id + n - 1; returns n >= 0 or a negative code. */
+int rt_mesh_parse(const char* obj_path, int64_t* triangles, int64_t* shapes);
+int rt_mesh_build(rt_graph* g, const char* obj_path, int* first_id);
 /* Compiles the graph (flat SoA + SAH BVH) and uploads it to `device`.  The graph stays owned by the caller. */
 int rt_graph_compile(rt_graph* g, int device, rt_scene** out);
 

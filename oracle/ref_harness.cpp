@@ -21,7 +21,8 @@
 //                                                   with its 4 stripes run one after another (deterministic)
 //   ref_harness probe SCENE K                       next K random_double() after the scene build (RNG pin)
 //   ref_harness dump SCENE OUT.json                 canonical dump of the scene graph (scene pin)
-//   ref_harness mesh SCENE OUT.bin                  post-triangulation triangle list (f32 xyz*3 + f64 rgb)
+//   ref_harness mesh SCENE|PATH.obj OUT.bin                 post-triangulation triangle list: u32 n, f32 xyz*3*n, f64 rgb*n (solid albedo,
+//                                                   else 0), and for a map_Kd mesh f64 (ua,va,ub,vb,uc,vc)*n
 //   ref_harness texture PATH OUT.bin                stb-decoded texture bytes (w,h,c header + bytes)
 
 // Pre-include the standard library so the access override below only touches reference classes.
@@ -171,10 +172,13 @@ std::string dump_texture(const std::shared_ptr<texture>& t) {
         return s;
     }
     if (auto im = std::dynamic_pointer_cast<image_texture>(t)) {
+        static std::map<const image_texture*, std::string> cache;  // a textured mesh shares one image over all triangles
+        auto it = cache.find(im.get());
+        if (it != cache.end()) return it->second;
         size_t n = static_cast<size_t>(im->width) * im->height * im->bytes_per_pixel;
         char h[32];
         std::snprintf(h, sizeof h, "%016llx", (unsigned long long)(im->data ? fnv1a(im->data.get(), n) : 0));
-        return "{\"type\":\"image\",\"w\":" + std::to_string(im->width) + ",\"h\":" + std::to_string(im->height) +
+        return cache[im.get()] = "{\"type\":\"image\",\"w\":" + std::to_string(im->width) + ",\"h\":" + std::to_string(im->height) +
                ",\"bpp\":" + std::to_string(im->bytes_per_pixel) + ",\"fnv1a\":\"" + h + "\"}";
     }
     if (auto b = std::dynamic_pointer_cast<barycentric_image_texture>(t))
@@ -417,7 +421,8 @@ int main(int argc, char** argv) try {
         // Post-triangulation triangle list of a mesh scene, in leaf order of the BVH is NOT wanted: rebuild from the parser.
         std::string name = argv[2];
         mesh m;
-        if (!m.parse(name == "cow" ? ressources::cow_obj_path : name == "dino" ? ressources::dino_obj_path : ressources::capsule_obj_path)) return 1;
+        const bool file = name.size() > 4 && name.compare(name.size() - 4, 4, ".obj") == 0;  // any OBJ path (test meshes)
+        if (!m.parse(file ? name : name == "cow" ? ressources::cow_obj_path : name == "dino" ? ressources::dino_obj_path : ressources::capsule_obj_path)) return 1;
         auto tris = m.build();
         std::ofstream f(argv[3], std::ios::binary);
         uint32_t n = static_cast<uint32_t>(tris.objects.size());
@@ -428,12 +433,26 @@ int main(int argc, char** argv) try {
             for (int k = 0; k < 3; ++k) { p[k] = (float)t->pt1[k]; p[3 + k] = (float)t->pt2[k]; p[6 + k] = (float)t->pt3[k]; }
             f.write(reinterpret_cast<const char*>(p), sizeof p);
         }
+        bool textured = false;
         for (auto& o : tris.objects) {
             auto t = std::dynamic_pointer_cast<triangle>(o);
             auto l = std::dynamic_pointer_cast<lambertian>(t->mat_ptr);
             double c[3] = {0, 0, 0};
             if (auto s = std::dynamic_pointer_cast<solid_color>(l->albedo)) { c[0] = s->color_value[0]; c[1] = s->color_value[1]; c[2] = s->color_value[2]; }
+            textured |= static_cast<bool>(std::dynamic_pointer_cast<barycentric_image_texture>(l->albedo));
             f.write(reinterpret_cast<const char*>(c), sizeof c);
+        }
+        // textured meshes (map_Kd): per triangle the barycentric_image_texture coordinates a, b, c (f64 u, v each)
+        for (auto& o : tris.objects) {
+            if (!textured) break;
+            auto t = std::dynamic_pointer_cast<triangle>(o);
+            auto b = std::dynamic_pointer_cast<barycentric_image_texture>(std::dynamic_pointer_cast<lambertian>(t->mat_ptr)->albedo);
+            double uv[6] = {0, 0, 0, 0, 0, 0};
+            if (b) {
+                uv[0] = b->texcoord_a.first; uv[1] = b->texcoord_a.second; uv[2] = b->texcoord_b.first;
+                uv[3] = b->texcoord_b.second; uv[4] = b->texcoord_c.first; uv[5] = b->texcoord_c.second;
+            }
+            f.write(reinterpret_cast<const char*>(uv), sizeof uv);
         }
         return 0;
     }

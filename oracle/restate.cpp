@@ -30,6 +30,8 @@
 #include <thread>
 #include <vector>
 
+#include <zlib.h>
+
 namespace {
 
 thread_local std::string g_err;
@@ -401,15 +403,20 @@ int noise_tex(Scene& s, double scale, Rng& rng) {
     return s.tex(t);
 }
 
+// The reference's stb_image output as a raw (w, h, bpp + bytes) asset, plain or gzip-compressed.
 bool load_image_asset(Image& img, const std::string& name) {
-    std::ifstream f(g_asset_dir + "/" + name, std::ios::binary);
+    gzFile f = gzopen((g_asset_dir + "/" + name).c_str(), "rb");
     if (!f) return false;
     int32_t hdr[3];
-    f.read(reinterpret_cast<char*>(hdr), sizeof hdr);
+    bool ok = gzread(f, hdr, sizeof hdr) == static_cast<int>(sizeof hdr);
     img.w = hdr[0]; img.h = hdr[1]; img.bpp = hdr[2];
-    img.data.resize(static_cast<size_t>(img.w) * img.h * img.bpp);
-    f.read(reinterpret_cast<char*>(img.data.data()), static_cast<std::streamsize>(img.data.size()));
-    return static_cast<bool>(f);
+    ok = ok && img.w > 0 && img.h > 0 && img.bpp >= 3 && img.w <= 65536 && img.h <= 65536 && img.bpp <= 4;
+    if (ok) {
+        img.data.resize(static_cast<size_t>(img.w) * img.h * img.bpp);
+        ok = gzread(f, img.data.data(), static_cast<unsigned>(img.data.size())) == static_cast<int>(img.data.size());
+    }
+    gzclose(f);
+    return ok;
 }
 int image_tex(Scene& s, const std::string& asset) {
     Image img;
@@ -529,13 +536,24 @@ void final_scene(Scene& s, Rng& rng) {  // scene_manager.cpp:171-234
     s.world.push_back(s.translate(rotate_y(s, bvh2, 15), V3(-100, 270, 395)));
 }
 
-void mesh_scene(Scene& s, Rng& rng, const std::string& asset) {  // scene_manager.cpp:236-258 + mesh.h:67-145
+// The mesh enters as the reference's own post-triangulation triangle list (oracle/ref_harness `mesh`): f32 vertices,
+// then per-triangle solid colours (unused: replayed from rng below) and, for a map_Kd mesh, the texture coordinates.
+void mesh_scene(Scene& s, Rng& rng, const std::string& asset, const std::string& texture = "") {  // scene_manager.cpp:236-258 + mesh.h:67-145
     std::ifstream f(g_asset_dir + "/" + asset, std::ios::binary);
     if (!f) throw std::runtime_error("missing mesh asset " + asset);
     uint32_t n = 0;
     f.read(reinterpret_cast<char*>(&n), 4);
     std::vector<float> p(static_cast<size_t>(n) * 9);
     f.read(reinterpret_cast<char*>(p.data()), static_cast<std::streamsize>(p.size() * 4));
+    std::vector<double> uv;
+    int image = -1;
+    if (!texture.empty()) {  // mesh.h:98-125: lambertian(barycentric_image_texture(uv1, uv2, uv3, map_Kd image))
+        f.seekg(static_cast<std::streamoff>(4 + 36ull * n + 24ull * n));
+        uv.resize(static_cast<size_t>(n) * 6);
+        f.read(reinterpret_cast<char*>(uv.data()), static_cast<std::streamsize>(uv.size() * 8));
+        if (!f) throw std::runtime_error("mesh asset " + asset + " has no texture coordinates");
+        image = s.texs[image_tex(s, texture)].image;
+    }
     std::vector<int> tris;
     for (uint32_t t = 0; t < n; ++t) {
         Obj o{O_TRI};
@@ -543,7 +561,15 @@ void mesh_scene(Scene& s, Rng& rng, const std::string& asset) {  // scene_manage
         o.c0 = V3(q[0], q[1], q[2]);
         o.c1 = V3(q[3], q[4], q[5]);
         o.p3 = V3(q[6], q[7], q[8]);
-        o.mat = s.lambertian(rng.vec01());  // mesh.h:136-141: lambertian(color::random()) when the OBJ has no materials
+        if (image >= 0) {
+            Tex b{T_BARY_IMAGE};
+            b.image = image;
+            const double* w = &uv[static_cast<size_t>(t) * 6];
+            b.ua = w[0]; b.va = w[1]; b.ub = w[2]; b.vb = w[3]; b.uc = w[4]; b.vc = w[5];
+            o.mat = s.lambertian_tex(s.tex(b));
+        } else {
+            o.mat = s.lambertian(rng.vec01());  // mesh.h:136-141: lambertian(color::random()) when the OBJ has no materials
+        }
         tris.push_back(s.add(o));
     }
     s.world.push_back(build_bvh(s, tris, 0, tris.size(), 0.0, 1.0, rng));
@@ -597,6 +623,9 @@ void build_scene(Scene& s, const std::string& name, Rng& rng) {  // scene_manage
         if (name == "cow") { s.lookfrom = V3(4, 2, 6); s.lookat = V3(2, 0, 0); }
         else { s.lookfrom = V3(0, 15, 25); s.lookat = V3(0, 10, 0); }
         s.vfov = 75.0;
+    } else if (name == "9" || name == "mesh") {  // the stock _mesh_scene: the textured capsule
+        mesh_scene(s, rng, "capsule.tris", "models/capsule/capsule.rgb.gz");
+        s.background = sky; s.lookfrom = V3(2, 2, 1); s.lookat = V3(0, 0, 0); s.vfov = 75.0;
     } else {
         throw std::runtime_error("unknown scene " + name);
     }
@@ -955,6 +984,20 @@ uint64_t fnv1a(const unsigned char* p, size_t n) {
     return h;
 }
 
+// Image dumps hash the texels once per image and dump (a textured mesh shares one image over every triangle).
+std::vector<std::string> g_image_dump;
+std::string dump_image(const Scene& s, int ii) {
+    if (g_image_dump.size() < s.images.size()) g_image_dump.resize(s.images.size());
+    std::string& r = g_image_dump[static_cast<size_t>(ii)];
+    if (r.empty()) {
+        const Image& im = s.images[ii];
+        char h[32];
+        std::snprintf(h, sizeof h, "%016llx", static_cast<unsigned long long>(fnv1a(im.data.data(), im.data.size())));
+        r = "{\"type\":\"image\",\"w\":" + std::to_string(im.w) + ",\"h\":" + std::to_string(im.h) + ",\"bpp\":" + std::to_string(im.bpp) +
+            ",\"fnv1a\":\"" + h + "\"}";
+    }
+    return r;
+}
 std::string dump_tex(const Scene& s, int ti) {
     const Tex& t = s.texs[ti];
     switch (t.k) {
@@ -971,14 +1014,10 @@ std::string dump_tex(const Scene& s, int ti) {
             };
             return r + "],\"perm_x\":" + perm(p.px) + ",\"perm_y\":" + perm(p.py) + ",\"perm_z\":" + perm(p.pz) + "}";
         }
-        case T_IMAGE: {
-            const Image& im = s.images[t.image];
-            char h[32];
-            std::snprintf(h, sizeof h, "%016llx", static_cast<unsigned long long>(fnv1a(im.data.data(), im.data.size())));
-            return "{\"type\":\"image\",\"w\":" + std::to_string(im.w) + ",\"h\":" + std::to_string(im.h) + ",\"bpp\":" + std::to_string(im.bpp) +
-                   ",\"fnv1a\":\"" + h + "\"}";
-        }
-        case T_BARY_IMAGE: return "{\"type\":\"bary_image\"}";
+        case T_IMAGE: return dump_image(s, t.image);
+        case T_BARY_IMAGE:  // texture.h:135-154, ref_harness dump_texture schema
+            return "{\"type\":\"bary_image\",\"a\":[" + D(t.ua) + "," + D(t.va) + "],\"b\":[" + D(t.ub) + "," + D(t.vb) + "],\"c\":[" +
+                   D(t.uc) + "," + D(t.vc) + "],\"tex\":" + dump_image(s, t.image) + "}";
     }
     return "{}";
 }
@@ -1075,6 +1114,7 @@ size_t orc_dump(const char* scene, char* buf, size_t cap) try {
     Scene s;
     Rng rng;
     build_scene(s, scene, rng);
+    g_image_dump.clear();
     std::string r = "{\"lookfrom\":" + Vs(s.lookfrom) + ",\"lookat\":" + Vs(s.lookat) + ",\"vfov\":" + D(s.vfov) + ",\"aperture\":" + D(s.aperture) +
                     ",\"background\":" + Vs(s.background) + ",\"objects\":[";
     for (size_t i = 0; i < s.world.size(); ++i) r += (i ? ",\n" : "\n") + dump_obj(s, s.world[i]);

@@ -14,8 +14,10 @@ fixtures pin:
                        exact segment count (world.hit calls)
   * render_adaptive_<scene>.npz  engine_mode::adaptive renders (engine.h:96-333, its 4 stripes run in order):
                        RGB8 and segment count (`python tests/golden/make_golden.py adaptive` makes only these)
-Assets (assets/*.tris, assets/earthmap.rgb) are the reference's post-triangulation meshes and stb-decoded
-texture bytes, written by the same harness.
+Assets written by the same harness: assets/*.tris (the reference's post-triangulation triangle lists: cow,
+dino, capsule incl. its texture coordinates; the oracle's mesh input and the pin of the product's OBJ loader),
+assets/earthmap.rgb and assets/models/capsule/capsule.rgb.gz (stb_image-decoded texels, the latter gzipped).
+`python tests/golden/make_golden.py scene NAME` (re)makes one scene's fixtures without touching the others.
 """
 import hashlib
 import json
@@ -30,7 +32,7 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 HARNESS = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
 REF = "/root/reference"
 
-SCENES = ["c1", "1", "2", "3", "4", "5", "6", "7", "8", "cow", "dino"]
+SCENES = ["c1", "1", "2", "3", "4", "5", "6", "7", "8", "cow", "dino", "9"]
 SMALL = (64, 36, 4)          # every scene, RGB + f64 sums + segments
 CONFIG1 = ("c1", 400, 225, 64)  # BASELINE configs[0]: the CPU reference path at full size
 ADAPTIVE = ["c1", "1", "8", "cow"]
@@ -59,34 +61,56 @@ def adaptive_fixtures():
         print("adaptive", sc, info)
 
 
+def scene_fixtures(sc):
+    """probe + dump hash (scenes.json entry) and the SMALL render of one scene."""
+    # the harness may log texture loads on stdout first: the values are the last 8 lines
+    probe = [float(x) for x in run("probe", sc, 8).strip().splitlines()[-8:]]
+    run("dump", sc, "/tmp/golden_dump.json")
+    dump = open("/tmp/golden_dump.json", "rb").read()
+    W, H, spp = SMALL
+    rgb, acc, info = render(sc, W, H, spp)
+    np.savez_compressed(os.path.join(HERE, f"render_{sc}_{W}x{H}x{spp}.npz"), rgb=rgb, acc=acc,
+                        segments=np.int64(info["segments"]), W=W, H=H, spp=spp)
+    print(sc, info)
+    return {"probe": probe, "dump_sha256": hashlib.sha256(dump).hexdigest(), "dump_len": len(dump)}
+
+
+def assets_fixtures():
+    assets = os.path.join(ROOT, "assets")
+    os.makedirs(os.path.join(assets, "models", "capsule"), exist_ok=True)
+    run("mesh", "cow", os.path.join(assets, "cow.tris"))
+    run("mesh", "dino", os.path.join(assets, "dino.tris"))
+    run("mesh", "capsule", os.path.join(assets, "capsule.tris"))
+    run("texture", f"{REF}/textures/earthmap.jpg", os.path.join(assets, "earthmap.rgb"))
+    raw = "/tmp/golden_capsule.rgb"
+    run("texture", f"{REF}/models/capsule/capsule.jpg", raw)
+    import gzip
+    with open(raw, "rb") as fi, gzip.GzipFile(os.path.join(assets, "models", "capsule", "capsule.rgb.gz"), "wb", 9,
+                                                mtime=0) as fo:
+        fo.write(fi.read())
+
+
 def main():
     if not os.path.exists(HARNESS):
         sys.exit("build the reference harness first: make -C oracle ref")
     if sys.argv[1:] == ["adaptive"]:
         adaptive_fixtures()
         return
-    assets = os.path.join(ROOT, "assets")
-    os.makedirs(assets, exist_ok=True)
-    run("mesh", "cow", os.path.join(assets, "cow.tris"))
-    run("mesh", "dino", os.path.join(assets, "dino.tris"))
-    run("texture", f"{REF}/textures/earthmap.jpg", os.path.join(assets, "earthmap.rgb"))
+    if sys.argv[1:2] == ["scene"]:
+        path = os.path.join(HERE, "scenes.json")
+        scenes = json.load(open(path))
+        for sc in sys.argv[2:]:
+            scenes[sc] = scene_fixtures(sc)
+        with open(path, "w") as f:
+            json.dump(scenes, f, indent=1)
+        return
+    assets_fixtures()
 
     kat = [float(x) for x in run("kat", 32).split()]
     with open(os.path.join(HERE, "kat.json"), "w") as f:
         json.dump({"seed": 5489, "random_double": kat}, f, indent=1)
 
-    scenes = {}
-    for sc in SCENES:
-        # the harness may log texture loads on stdout first: the values are the last 8 lines
-        probe = [float(x) for x in run("probe", sc, 8).strip().splitlines()[-8:]]
-        run("dump", sc, "/tmp/golden_dump.json")
-        dump = open("/tmp/golden_dump.json", "rb").read()
-        scenes[sc] = {"probe": probe, "dump_sha256": hashlib.sha256(dump).hexdigest(), "dump_len": len(dump)}
-        W, H, spp = SMALL
-        rgb, acc, info = render(sc, W, H, spp)
-        np.savez_compressed(os.path.join(HERE, f"render_{sc}_{W}x{H}x{spp}.npz"), rgb=rgb, acc=acc,
-                            segments=np.int64(info["segments"]), W=W, H=H, spp=spp)
-        print(sc, info)
+    scenes = {sc: scene_fixtures(sc) for sc in SCENES}
     with open(os.path.join(HERE, "scenes.json"), "w") as f:
         json.dump(scenes, f, indent=1)
 

@@ -16,7 +16,7 @@ from tests.oracle_lib import oracle_render
 
 pytestmark = pytest.mark.gpu
 
-SCENES = ["c1", "1", "2", "3", "4", "5", "6", "7", "8", "cow", "dino"]
+SCENES = ["c1", "1", "2", "3", "4", "5", "6", "7", "8", "cow", "dino", "9"]
 
 
 def gpu_render(scene, W, H, spp, precision="f64", seed=0, band=None, accum=True, global_scene=False, split_shade=False,

@@ -10,7 +10,7 @@ import pytest
 from tests.oracle_lib import REF_HARNESS, oracle_dump, oracle_kat, oracle_probe, oracle_render, oracle_render_adaptive
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
-SCENES = ["c1", "1", "2", "3", "4", "5", "6", "7", "8", "cow", "dino"]
+SCENES = ["c1", "1", "2", "3", "4", "5", "6", "7", "8", "cow", "dino", "9"]
 
 
 def test_mt19937_known_answers():
