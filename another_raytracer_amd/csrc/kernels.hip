@@ -192,7 +192,7 @@ struct Work {
     double* acc;                // local pixels * 3
 };
 template <class R>
-__device__ __forceinline__ uint32_t* counter(const Work<R>& w, int d, int kind, int s) {
+__host__ __device__ __forceinline__ uint32_t* counter(const Work<R>& w, int d, int kind, int s) {
     return w.counters + (static_cast<size_t>((d * kQueueKinds + kind) * kShards + s)) * kCounterStride;
 }
 
@@ -577,6 +577,92 @@ __global__ __launch_bounds__(L ? kBlockL : kBlock, L ? 1 : ART_EXTEND_MIN_WAVES)
         atomicAdd(&g_art_stats[11], tm_app);
     }
 #endif
+}
+
+// Persistent-path variant of the fused LDS scene (EXT_MEGA): one launch traces a whole pass.  Every lane owns one
+// path at a time and keeps it in registers from its camera ray to its end (engine.h:447-466 flattened: trace,
+// shade_hit_lds, repeat until a miss, an absorption, a light or max_depth), then writes the slot's radiance and takes
+// the next slot -- no path records, queues or per-depth launches, and the deep bounces of old paths share the waves
+// with the first bounces of new ones instead of running as a tail of nearly empty launches.  Slots are claimed in
+// increasing order in wave chunks of kPathChunk from one counter (one atomic per chunk: ~10 M/s at full rate, far
+// below the ~88 M/s a single word sustains).  The bounce arithmetic and the RNG draws are those of the fused
+// k_extend, so images are bit-identical to the wavefront variants.
+constexpr uint32_t kPathChunk = 256;
+__global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S, PassGeom g, CameraRec<double> cam, Work<double> w, uint32_t* next_slot) {
+    using R = double;
+    constexpr int B = kBlockL;
+    extern __shared__ __align__(16) uint8_t smem[];
+    const uint8_t* lds = smem;
+    StackT<true>* stk = reinterpret_cast<StackT<true>*>(smem + kLdsImageBytes) + B + threadIdx.x;
+    stk[-B] = static_cast<StackT<true>>(kNodeEmpty);
+    load_lds_image<B>(S.lds_image, smem);
+    __syncthreads();
+    const uint32_t lane = __lane_id();
+    const uint64_t below = (1ull << lane) - 1ull;
+    const V3<R> bg = mk(S.bg[0], S.bg[1], S.bg[2]);
+    uint32_t cur = 0, end = 0;  // this wave's claimed slots [cur, end): wave-uniform
+    bool busy = false, drained = false;
+    uint32_t q = 0;
+    int depth = 0;
+    PathState<R> st;
+    unsigned long long segs = 0;
+    for (;;) {
+        // every idle lane takes the next slot of the wave's chunk (padding slots of partial tiles stay idle a round)
+        const uint64_t idle = __ballot(!busy && !drained);
+        if (idle) {
+            const uint32_t n = static_cast<uint32_t>(__popcll(idle));
+            const uint32_t rank = static_cast<uint32_t>(__popcll(idle & below));
+            uint32_t slot;
+            if (cur + n > end) {
+                uint32_t nb = 0;
+                if (lane == 0) nb = atomicAdd(next_slot, kPathChunk);
+                nb = __shfl(nb, 0);
+                const uint32_t left = end - cur;
+                slot = rank < left ? cur + rank : nb + (rank - left);
+                cur = nb + (n - left);
+                end = nb + kPathChunk;
+            } else {
+                slot = cur + rank;
+                cur += n;
+            }
+            if (!busy && !drained) {
+                if (slot >= g.P) {
+                    drained = true;
+                } else {
+                    int lx, ly;
+                    q = slot;
+                    if (slot_pixel(g, slot % g.npix_pad, lx, ly)) {
+                        gen_ray(g, cam, q, lx, ly, st);
+                        busy = true;
+                        depth = 0;
+                    }
+                }
+            }
+        }
+        if (__ballot(busy) == 0) {
+            if (__ballot(!drained) == 0) break;
+            continue;
+        }
+        if (busy) {
+            R t;
+            HitOut h{0, 0, kMatUnknown};
+            ++segs;
+            bool cont = false;
+            if (trace_world<R, kFeatSpheres, B, true>(S, lds, st.ray, stk, st.rng, t, h)) {
+                cont = shade_hit_lds(lds, h.obj >> 16, h.mt, t, depth + 1 >= g.max_depth, st);
+            } else {  // engine.h:455-456: miss -> background
+                st.L = st.L + st.T * bg;
+            }
+            if (cont) {
+                ++depth;
+            } else {
+                store_res(w.res, q, st.L);
+                busy = false;
+            }
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) segs += __shfl_xor(segs, off);
+    if (lane == 0) atomicAdd(w.segments, segs);
 }
 
 // Input: the kShards shards of material queue M at depth d (the extend stage sorted hits by material type).
@@ -1091,8 +1177,9 @@ static void launch_extend(int num_cu, hipStream_t st, const DevScene<R>& S, cons
     }
     hipLaunchKernelGGL((k_extend<R, F, L, FUSE>), dim3(blocks), dim3(L ? kBlockL : kBlock), lds, st, S, g, cam, w, d);
 }
-// Extend variant of one bounce: 0 = HBM scene, 1 = LDS scene, 2 = LDS scene with fused shading (no k_shade launches).
-enum ExtendVariant { EXT_GLOBAL = 0, EXT_LDS = 1, EXT_FUSED = 2 };
+// Extend variant: 0 = HBM scene, 1 = LDS scene, 2 = LDS scene with fused shading (no k_shade launches), 3 = persistent
+// paths (k_paths: the fused LDS bounce loop in registers, one launch per pass).
+enum ExtendVariant { EXT_GLOBAL = 0, EXT_LDS = 1, EXT_FUSED = 2, EXT_MEGA = 3 };
 // One bounce (extend + one shade launch per material type present, unless fused) of the smallest kernel
 // instantiation that covers the scene's features.
 template <class R, uint32_t F>
@@ -1116,12 +1203,23 @@ static void launch_bounce(uint32_t mat_types, bool tex_basic, int variant, int n
     }
     if (mark) mark();
 }
-// Extend variant for this scene and these flags (RT_GLOBAL_SCENE / RT_SPLIT_SHADE force the general kernels).
+// Extend variant for this scene and these flags (RT_GLOBAL_SCENE / RT_SPLIT_SHADE / RT_WAVEFRONT force the general
+// kernels).
 template <class R>
 static int extend_variant(const DeviceScene<R>& ds, int flags) {
     if (!ds.lds_scene || (flags & RT_GLOBAL_SCENE) || (ds.features & ~kFeatSpheres) != 0) return EXT_GLOBAL;
-    const bool fusable = ds.lds_shade;
-    return (fusable && !(flags & RT_SPLIT_SHADE)) ? EXT_FUSED : EXT_LDS;
+    if (!ds.lds_shade || (flags & RT_SPLIT_SHADE)) return EXT_LDS;
+    return (flags & RT_WAVEFRONT) ? EXT_FUSED : EXT_MEGA;
+}
+static void launch_paths(int num_cu, hipStream_t st, const DevScene<double>& S, const PassGeom& g, const CameraRec<double>& cam,
+                         const Work<double>& w, uint32_t* next_slot) {
+    const size_t lds = extend_lds_bytes(true, g.stack);
+    static size_t attr_lds = 0;
+    if (lds > 64 * 1024 && lds != attr_lds) {
+        HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_paths), hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
+        attr_lds = lds;
+    }
+    hipLaunchKernelGGL(k_paths, dim3(num_cu), dim3(kBlockL), lds, st, S, g, cam, w, next_slot);
 }
 template <class R>
 static void bounce(const DeviceScene<R>& ds, int variant, int num_cu, hipStream_t st, const PassGeom& g, const CameraRec<R>& cam, const Work<R>& w,
@@ -1163,10 +1261,13 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     g.max_depth = p.max_depth;
     g.seed = p.seed;
     g.stack = stack_rows(ds.max_stack);
+    const int variant = extend_variant(ds, p.flags);
+    const bool mega = variant == EXT_MEGA;
     // Samples per pass: as many path slots as half of the free HBM holds (plus the workspace this renderer already
     // owns).  Every pass pays max_depth bounces of fixed launch/tail cost whatever its size, so on a 288 GB part the
     // 1080p x 1024 spp frame runs in 3 passes instead of ~40 (5.6 -> 6.9 Gsamples/s measured); spread evenly.
-    const size_t slot_bytes = sizeof(PathRec<R>) + sizeof(HitRecD<R>) + sizeof(ResRec<R>) + 4u * (2u + kNumMatTypes) + 8u;
+    // (persistent paths keep the path state in registers: a slot is its radiance record only)
+    const size_t slot_bytes = mega ? sizeof(ResRec<R>) : sizeof(PathRec<R>) + sizeof(HitRecD<R>) + sizeof(ResRec<R>) + 4u * (2u + kNumMatTypes) + 8u;
     size_t free_b = 0, total_b = 0;
     HIP_OK(hipMemGetInfo(&free_b, &total_b));
     const uint64_t target = std::min<uint64_t>((free_b + I.ws_bytes) / 2 / slot_bytes, kMaxPassSlots);  // fixed point: no regrowth
@@ -1182,12 +1283,13 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
 
     auto al = [](size_t x) { return (x + 255) & ~static_cast<size_t>(255); };
     size_t off = 0;
-    const size_t o_paths = off; off += al(sizeof(PathRec<R>) * Pmax);
-    const size_t o_hits = off; off += al(sizeof(HitRecD<R>) * Pmax);
+    const size_t wf = mega ? 0u : 1u;  // wavefront-only buffers
+    const size_t o_paths = off; off += wf * al(sizeof(PathRec<R>) * Pmax);
+    const size_t o_hits = off; off += wf * al(sizeof(HitRecD<R>) * Pmax);
     const size_t o_res = off; off += al(sizeof(ResRec<R>) * Pmax);
-    const size_t o_a0 = off; off += al(4ull * kShards * g.cap);
-    const size_t o_a1 = off; off += al(4ull * kShards * g.cap);
-    const size_t o_mq = off; off += al(4ull * kMatSegs * g.cap);
+    const size_t o_a0 = off; off += wf * al(4ull * kShards * g.cap);
+    const size_t o_a1 = off; off += wf * al(4ull * kShards * g.cap);
+    const size_t o_mq = off; off += wf * al(4ull * kMatSegs * g.cap);
     const size_t cnt_words = static_cast<size_t>(depth_slots) * kQueueKinds * kShards * kCounterStride;
     const size_t o_cnt = off; off += al(4ull * cnt_words);
     const size_t o_seg = off; off += al(sizeof(unsigned long long));
@@ -1229,7 +1331,6 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     cam.time0 = R(camd.time0);
     cam.time1 = R(camd.time1);
 
-    const int variant = extend_variant(ds, p.flags);
     const bool prof = (p.flags & RT_PROFILE) != 0;
     const bool adaptive = (p.flags & RT_ADAPTIVE) != 0;
     const int levels = adaptive ? 4 : 1;
@@ -1243,6 +1344,7 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     size_t ev_next = 0;
     auto mark = [&]() { HIP_OK(hipEventRecord(evs[ev_next++], stream)); };
     int passes_run = 0;
+    uint64_t ext_launches = 0;
     // Traces spp samples of every local pixel (list == nullptr) or of every entry of a device pixel list, into
     // w.acc (per local pixel, or per list entry).
     auto trace = [&](const uint32_t* list, uint32_t nlist) {
@@ -1261,8 +1363,22 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
             g.P = g.k * g.npix_pad;
             g.live = g.k * npix;
             HIP_OK(hipMemsetAsync(w.counters, 0, 4ull * cnt_words, stream));
+            if constexpr (std::is_same<R, double>::value) {
+                if (mega) {
+                    if (p.max_depth > 0) {
+                        if (prof) mark();
+                        launch_paths(I.num_cu, stream, ds.view, g, cam, w, counter(w, 0, 0, 0));
+                        if (prof) { mark(); mark(); }
+                        ++ext_launches;
+                    }
+                    hipLaunchKernelGGL(k_accum<R>, dim3((g.npix_pad + 255) / 256), dim3(256), 0, stream, g, w);
+                    ++passes_run;
+                    continue;
+                }
+            }
             for (int d = 0; d < p.max_depth; ++d)
                 bounce<R>(ds, variant, I.num_cu, stream, g, cam, w, d, prof ? std::function<void()>(mark) : std::function<void()>());
+            ext_launches += static_cast<uint64_t>(p.max_depth);
             hipLaunchKernelGGL(k_accum<R>, dim3((g.npix_pad + 255) / 256), dim3(256), 0, stream, g, w);
             ++passes_run;
         }
@@ -1341,8 +1457,8 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
         }
         stats.extend_ms = ext_ms;
         stats.shade_ms = sh_ms;
-        stats.extend_launches = static_cast<uint64_t>(passes_run) * p.max_depth;
-        stats.shade_launches = stats.extend_launches;
+        stats.extend_launches = ext_launches;
+        stats.shade_launches = variant == EXT_GLOBAL || variant == EXT_LDS ? ext_launches : 0;
         for (auto e : evs) (void)hipEventDestroy(e);
     }
 }

@@ -10,7 +10,7 @@ import enum
 
 import numpy as np
 
-from ._lib import RT_ADAPTIVE, RT_FP32, RT_FP64, RT_GLOBAL_SCENE, RT_OUT_DEVICE, RT_PROFILE, RT_SPLIT_SHADE, check, dvec, lib, rt_camera, rt_params, rt_stats
+from ._lib import RT_ADAPTIVE, RT_FP32, RT_FP64, RT_GLOBAL_SCENE, RT_OUT_DEVICE, RT_PROFILE, RT_SPLIT_SHADE, RT_WAVEFRONT, check, dvec, lib, rt_camera, rt_params, rt_stats
 from .scene import compile_world
 
 
@@ -67,6 +67,8 @@ class engine:
         self.global_scene = False
         # True keeps shading in separate per-material k_shade launches even when it could be fused (A/B, tests)
         self.split_shade = False
+        # True runs the fused LDS kernel once per bounce depth instead of the persistent-path kernel (A/B, tests)
+        self.wavefront = False
         self.world = None
         self.background = (0.0, 0.0, 0.0)
         self._scene = None
@@ -105,7 +107,8 @@ class engine:
         if adaptive and accum is not None:
             raise ValueError("engine_mode.adaptive interpolates most pixels: there are no radiance sums to return")
         flags = ((RT_PROFILE if profile else 0) | (RT_GLOBAL_SCENE if self.global_scene else 0)
-                 | (RT_SPLIT_SHADE if self.split_shade else 0) | (RT_ADAPTIVE if adaptive else 0))
+                 | (RT_SPLIT_SHADE if self.split_shade else 0) | (RT_ADAPTIVE if adaptive else 0)
+                 | (RT_WAVEFRONT if self.wavefront else 0))
         p = self.params(band_rows, band_count, band_index, flags, stream)
         rows = check(lib.rt_local_rows(ctypes.byref(p), None), "rt_local_rows")
         nbytes = rows * self.width * 3

@@ -9,8 +9,10 @@ max-over-ranks wall time of the K timed steps.  A segment is one ray traced thro
 engine.h:453), counted exactly on the device from the wavefront queue sizes.
 
 Extra fields:
-  roofline      dominant kernel (k_extend): algorithmic bytes per segment x segments / summed launch time
-                measured live with HIP events on the render stream during the timed steps; HBM peak 8 TB/s.
+  roofline      dominant kernel (k_paths, or k_extend for the per-depth variants): SURVEY.md §8(d) algorithmic bytes
+                (128 B per segment + 12 B per pixel + the flat scene once per launch) / summed launch time measured live
+                with HIP events on the render stream during the timed steps; HBM peak 8 TB/s.  moved_bytes_per_segment
+                is what the variant really moves by construction.
                 `traffic` = FETCH_SIZE*2 + WRITE_SIZE per segment from the committed rocprofv3 PMC summary
                 (profiles/, MI355X_MICROARCH.md "HBM") scaled to this run, or null.
   cpu_baseline  the reference itself (oracle/_ref/ref_harness = /root/reference/src compiled unmodified), its own
@@ -29,22 +31,33 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# k_extend algorithmic bytes per segment: queue index 4 + ray (origin, time, direction) + hit record 16
-# + material-queue entry 4.  f32 path record: ray = 32 B; f64: 64 B.
+# algorithmic bytes of the path = 128 B per segment (a 64-B fp32 path record read once and written
+# once per bounce) + 12 B per pixel (f32 RGB accumulator write) + one pass over the flat scene.  The same figure for
+# every kernel variant, so `achieved` compares variants and rounds on one scale.
+SURVEY_SEG_BYTES = 128
+SURVEY_PIX_BYTES = 12
+# Bytes the extend kernel of each variant really moves per unit, reported beside it:
+#   0/1 (split shading): queue id 4 + ray line (f32 32 B / f64 64 B) + hit record 16 + material-queue id 4 per segment;
+#   2 (fused, one launch per depth): a non-primary segment reads its queue id and whole path record and, when it
+#     continues, writes the record back plus the next queue id; every path ends with one radiance record;
+#   3 (persistent paths): the path lives in registers; only the final radiance record of every path is written.
 EXTEND_BYTES = {"f32": 4 + 32 + 16 + 4, "f64": 4 + 64 + 16 + 4}
-# Fused variant (extend_variant 2: shading inside k_extend): a non-primary segment reads its queue id and
-# whole path record and, when it continues, writes the record back plus the next queue id; every path ends exactly
-# once with a radiance record.  Depth-0 (primary) segments generate their ray in registers and read nothing.
 PATH_BYTES = {"f32": 64, "f64": 128}
 RES_BYTES = {"f32": 16, "f64": 32}
 
 
-def extend_algorithmic_bytes(precision, variant, segments, primary):
-    """Algorithmic HBM bytes of all k_extend launches of the timed region."""
+def extend_moved_bytes(precision, variant, segments, primary):
+    """Bytes the extend launches of the timed region move by construction (variant-specific)."""
+    if variant == 3:
+        return primary * RES_BYTES[precision]
     if variant == 2:
         rec = PATH_BYTES[precision]
         return (segments - primary) * (4 + rec + rec + 4) + primary * RES_BYTES[precision]
     return EXTEND_BYTES[precision] * segments
+
+
+def survey_algorithmic_bytes(segments, pixels, scene_bytes):
+    return SURVEY_SEG_BYTES * segments + SURVEY_PIX_BYTES * pixels + scene_bytes
 
 
 def parse():
@@ -63,6 +76,7 @@ def parse():
     ap.add_argument("--no-profile", action="store_true", help="skip per-launch HIP events (no roofline)")
     ap.add_argument("--global-scene", action="store_true", help="force the global-memory extend kernel (A/B vs LDS scene)")
     ap.add_argument("--split-shade", action="store_true", help="keep per-material k_shade launches (A/B vs fused shading)")
+    ap.add_argument("--wavefront", action="store_true", help="one fused extend launch per depth (A/B vs persistent paths)")
     ap.add_argument("--cpu-baseline-spp", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -127,6 +141,7 @@ def main():
     from another_raytracer_amd.distributed import band_rows_of, render_frame
 
     world_scene = art.scene_manager(device=dev.index).build(args.scene)
+    scene_bytes = int(world_scene.info["device_bytes_f64" if args.precision == "f64" else "device_bytes_f32"])
     cam = art.camera(world_scene.lookfrom, world_scene.lookat, (0, 1, 0), world_scene.vfov, args.width / args.height,
                      world_scene.aperture, 10.0, 0.0, 1.0)
     eng = art.engine(cam, art.engine_mode.parallel_stripes, width=args.width, height=args.height,
@@ -135,6 +150,7 @@ def main():
     eng.set_scene(world_scene.objects, world_scene.background)
     eng.global_scene = args.global_scene
     eng.split_shade = args.split_shade
+    eng.wavefront = args.wavefront
     rows = band_rows_of(args.height, args.band_rows, world, rank)
     local = torch.empty((len(rows), args.width, 3), dtype=torch.uint8, device=dev)
     profile = not args.no_profile
@@ -191,19 +207,25 @@ def main():
                        "mprimary_per_s": round(primary / elapsed / 1e6, 3)},
         }
         if profile and ext_ms > 0:
-            per_launch_ms = ext_ms / max(ext_launches, 1)
-            alg = extend_algorithmic_bytes(args.precision, variant, segs, primary_segs)
+            launches = max(ext_launches, 1)
+            per_launch_ms = ext_ms / launches
+            pixels = args.width * args.height * args.steps
+            alg = survey_algorithmic_bytes(segs, pixels, scene_bytes * ext_launches)
             achieved = alg / (ext_ms * 1e-3) / 1e9
+            moved = extend_moved_bytes(args.precision, variant, segs, primary_segs)
             tr = latest_traffic(args.precision, args.scene, variant)
             line["roofline"] = {
-                "bound": "hbm", "kernel": "k_extend", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                "traffic": (round(tr["extend_bytes_per_segment"] * segs / max(ext_launches, 1)) if tr else None),
-                "algorithmic_bytes_per_launch": round(alg / max(ext_launches, 1)),
-                "algorithmic_bytes_per_segment": round(alg / max(segs, 1), 2), "extend_variant": variant,
+                "bound": "hbm", "kernel": "k_paths" if variant == 3 else "k_extend", "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                "traffic": (round(tr["extend_bytes_per_segment"] * segs / launches) if tr else None),
+                "algorithmic_bytes_per_launch": round(alg / launches),
+                "algorithmic_bytes": "SURVEY 8(d): 128 B/segment + 12 B/pixel + scene bytes per launch",
+                "moved_bytes_per_segment": round(moved / max(segs, 1), 2), "extend_variant": variant,
                 "avg_launch_ms": round(per_launch_ms, 4), "launches": int(ext_launches),
                 "extend_ms_total": round(ext_ms, 2), "shade_ms_total": round(shade_ms, 2),
             }
+            if tr and tr.get("valu_busy") is not None:
+                line["roofline"]["valu_busy_pmc"] = tr["valu_busy"]
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(line), flush=True)

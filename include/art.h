@@ -58,6 +58,8 @@ extern "C" {
                                the rest.  Width and local rows must be multiples of 12 (the reference throws
                                std::logic_error otherwise: RT_E_INVALID here), band_rows a multiple of 12 when
                                band_count > 1, and out_accum NULL (interpolated pixels have no radiance sums). */
+#define RT_WAVEFRONT 32     /* LDS-scene renders: one fused extend launch per bounce depth (paths stored in HBM between
+                               bounces) instead of the persistent-path kernel (A/B and parity tests) */
 
 typedef struct rt_scene rt_scene;
 typedef struct rt_graph rt_graph;
@@ -96,7 +98,8 @@ typedef struct rt_stats {
     uint64_t extend_launches, shade_launches;
     int32_t passes, samples_per_pass, local_rows;
     int32_t extend_variant;     /* 0: scene read from HBM; 1: LDS-resident scene (spheres-only scene that fits);
-                                   2: LDS-resident scene with shading fused into the extend kernel */
+                                   2: LDS-resident scene with shading fused into the extend kernel (one launch per
+                                   depth); 3: persistent paths (the fused bounce loop in registers, one launch per pass) */
 } rt_stats;
 
 typedef struct rt_scene_info {  /* scene_manager.h:6-14 */

@@ -20,14 +20,15 @@ SCENES = ["c1", "1", "2", "3", "4", "5", "6", "7", "8", "cow", "dino", "9"]
 
 
 def gpu_render(scene, W, H, spp, precision="f64", seed=0, band=None, accum=True, global_scene=False, split_shade=False,
-               max_depth=50):
+               wavefront=False, max_depth=50, samples_per_pass=0):
     world = art.scene_manager().build(scene)
     cam = art.camera(world.lookfrom, world.lookat, (0, 1, 0), world.vfov, W / H, world.aperture, 10.0, 0.0, 1.0)
     eng = art.engine(cam, art.engine_mode.single, width=W, height=H, samples_per_pixel=spp, precision=precision,
-                     seed=seed, max_depth=max_depth)
+                     seed=seed, max_depth=max_depth, samples_per_pass=samples_per_pass)
     eng.set_scene(world.objects, world.background)
     eng.global_scene = global_scene
     eng.split_shade = split_shade
+    eng.wavefront = wavefront
     band_rows, band_count, band_index = band or (None, 1, 0)
     rows = H if band is None else len(eng.local_rows(band_rows, band_count, band_index))
     img = np.zeros((rows, W, 3), np.uint8)
@@ -88,17 +89,27 @@ def test_band_partition_is_bit_identical(gpu, precision):
 
 @pytest.mark.parametrize("max_depth", [1, 3, 50])
 def test_extend_variants_are_bit_identical(gpu, max_depth):
-    # the benchmark scene runs the LDS-resident extend kernel with fused shading (variant 2); it must reproduce the
-    # split-shade LDS kernel (1) and the HBM kernel (0) bit for bit, including the last-bounce cut-off
+    # the benchmark scene runs the persistent-path kernel (variant 3); it must reproduce the per-depth fused LDS kernel
+    # (2), the split-shade LDS kernel (1) and the HBM kernel (0) bit for bit, including the last-bounce cut-off
     W, H, spp = 160, 90, 8
-    fused = gpu_render("1", W, H, spp, "f64", max_depth=max_depth)
+    mega = gpu_render("1", W, H, spp, "f64", max_depth=max_depth)
+    fused = gpu_render("1", W, H, spp, "f64", wavefront=True, max_depth=max_depth)
     split = gpu_render("1", W, H, spp, "f64", split_shade=True, max_depth=max_depth)
     glb = gpu_render("1", W, H, spp, "f64", global_scene=True, max_depth=max_depth)
-    assert (fused["stats"]["extend_variant"], split["stats"]["extend_variant"], glb["stats"]["extend_variant"]) == (2, 1, 0)
-    for other in (split, glb):
-        assert np.array_equal(fused["acc"], other["acc"])
-        assert np.array_equal(fused["rgb"], other["rgb"])
-        assert fused["segments"] == other["segments"]
+    assert tuple(r["stats"]["extend_variant"] for r in (mega, fused, split, glb)) == (3, 2, 1, 0)
+    for other in (fused, split, glb):
+        assert np.array_equal(mega["acc"], other["acc"])
+        assert np.array_equal(mega["rgb"], other["rgb"])
+        assert mega["segments"] == other["segments"]
+
+
+def test_persistent_paths_pass_split_is_bit_identical(gpu):
+    # several passes (samples_per_pass) and one pass, with partial 8x8 tiles (padding slots): identical sums
+    W, H, spp = 100, 52, 12
+    one = gpu_render("1", W, H, spp, "f64")
+    many = gpu_render("1", W, H, spp, "f64", samples_per_pass=5)
+    assert one["stats"]["extend_variant"] == 3 and many["stats"]["passes"] == 3
+    assert np.array_equal(one["acc"], many["acc"]) and one["segments"] == many["segments"]
 
 
 def test_general_scenes_use_the_hbm_kernels(gpu):
