@@ -301,6 +301,9 @@ __device__ __forceinline__ void stat_lane(int k) { atomicAdd(&g_art_stats[k], 1u
 #define ART_STAT_LANE(k)
 #endif
 
+#ifndef ART_SPECULATIVE
+#define ART_SPECULATIVE 1
+#endif
 // Traversal stack entry: node/leaf codes, 16 bits in the LDS-scene variant (layout.h lds_leaf), 32 bits otherwise.
 template <bool L> using StackT = typename std::conditional<L, int16_t, int32_t>::type;
 
@@ -316,6 +319,12 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
     bool hit = false;
     int sp = 0;
     int32_t node = root;
+#if ART_SPECULATIVE
+    // Speculative while-while (Aila & Laine 2009): a lane that reaches a leaf parks it and keeps walking inner nodes
+    // until every lane of the wave holds a leaf, so the node loop runs with more lanes active; parked leaves are then
+    // tested together.  Nodes visited past a parked leaf used the older (larger) tmax: extra visits, same closest hit.
+    int32_t parked = kNodeEmpty;
+#endif
     ART_STAT_LANE(6);
     for (;;) {
         ART_STAT_WAVE(4);
@@ -357,16 +366,41 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
             const bool near = k0 < inf;
             node = near ? c0 : top;
             sp -= (!near && sp > 0) ? 1 : 0;
+#if ART_SPECULATIVE
+            if (node < kNodeEmpty && parked == kNodeEmpty) {  // a leaf (codes below -1) and none parked yet: park it
+                parked = node;
+                node = stk[(sp - 1) * B];
+                sp -= sp > 0 ? 1 : 0;
+            }
+            if (!__any(parked == kNodeEmpty)) break;  // every lane still walking holds a leaf: test them together
+#endif
         }
+#if ART_SPECULATIVE
+        // leaf phase: the parked leaf, else the current node when it is a leaf (a lane that left the node loop on the
+        // wave-wide break still has an inner node to return to)
+        int32_t leaf = parked;
+        if (leaf != kNodeEmpty) {
+            parked = kNodeEmpty;
+        } else {
+            if (node == kNodeEmpty) break;
+            leaf = node;
+            node = stk[(sp - 1) * B];
+            sp -= sp > 0 ? 1 : 0;
+        }
+#else
         if (node == kNodeEmpty) break;
+        const int32_t leaf = node;
+        node = stk[(sp - 1) * B];
+        sp -= sp > 0 ? 1 : 0;
+#endif
         uint32_t first, cnt;
         if constexpr (L) {
-            const uint32_t x = ~static_cast<uint32_t>(node);
+            const uint32_t x = ~static_cast<uint32_t>(leaf);
             first = x & ((1u << kLdsLeafShift) - 1);
             cnt = x >> kLdsLeafShift;
         } else {
-            first = leaf_first(node);
-            cnt = leaf_count(node);
+            first = leaf_first(leaf);
+            cnt = leaf_count(leaf);
         }
         for (uint32_t k = 0; k < cnt; ++k) {
             ART_STAT_WAVE(2);
@@ -391,8 +425,6 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                 tmaxf = f_hi(tt);
             }
         }
-        node = stk[(sp - 1) * B];
-        sp -= sp > 0 ? 1 : 0;
     }
     return hit;
 }
