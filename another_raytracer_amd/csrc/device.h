@@ -129,8 +129,19 @@ __device__ __forceinline__ bool hit_sphere_at(V3<R> center, R radius, const Ray<
     return true;
 }
 // moving_sphere.h:72-74 center(time) = center0 + ((time - time0) / (time1 - time0)) * (center1 - center0)
+// (time - time0) / (time1 - time0): x / 1 == x exactly, so the divide is skipped for the common unit shutter span
+// (every moving sphere of the reference scenes) without changing a bit.
 template <class R>
-__device__ __forceinline__ V3<R> moving_center(V3<R> c0, V3<R> d, R t0, R dt, R tm) { return c0 + ((tm - t0) / dt) * d; }
+__device__ __forceinline__ R motion_fraction(R tm, R t0, R dt) {
+    R x = tm - t0;
+    if (dt != R(1)) {
+        __asm__ volatile("" : "+v"(x));  // keeps the divide inside the branch (no if-conversion into a select)
+        x = x / dt;
+    }
+    return x;
+}
+template <class R>
+__device__ __forceinline__ V3<R> moving_center(V3<R> c0, V3<R> d, R t0, R dt, R tm) { return c0 + motion_fraction(tm, t0, dt) * d; }
 template <class R>
 __device__ __forceinline__ bool hit_sphere(const SphereRec<R>& s, const Ray<R>& r, R tmin, R tmax, R& t) {
     V3<R> center = ld3(s.c);
@@ -256,6 +267,47 @@ __device__ __forceinline__ void slab4(const float4& lx, const float4& hx, const 
     k2 = slab_key(x0b.x, x1b.x, y0b.x, y1b.x, z0b.x, z1b.x, ch.z, tminf, tmaxf);
     k3 = slab_key(x0b.y, x1b.y, y0b.y, y1b.y, z0b.y, z1b.y, ch.w, tminf, tmaxf);
 }
+// Packed keys of the LDS variant: the entry distance's f32 bits with the low 16 bits replaced by the 16-bit child
+// code.  Entry distances are >= tminf > 0 there (world rays start at t = 0.001; the LDS variant has no media, whose
+// boundary tests start at -inf), so unsigned order is distance order to 2^-7 relative -- it only orders the pushes;
+// misses get kKeyMiss, above every finite key.
+constexpr uint32_t kKeyMiss = 0x7F800000u;
+__device__ __forceinline__ uint32_t slab_key_packed(float x0, float x1, float y0, float y1, float z0, float z1, int32_t child, float tminf,
+                                                    float tmaxf) {
+    // z slab clipped to [tminf, tmaxf] by a median: med3(z0, z1, t) differs from max(min(z0, z1), tminf) (resp.
+    // min(max(z0, z1), tmaxf)) only when the whole z slab lies outside [tminf, tmaxf], where the box can then pass
+    // only with lo == hi exactly -- a conservative extra visit, never a missed box
+#if ART_MED3
+    const float lo = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), __builtin_amdgcn_fmed3f(z0, z1, tminf));
+    const float hi = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), __builtin_amdgcn_fmed3f(z0, z1, tmaxf));
+#else
+    const float lo = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), tminf));
+    const float hi = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), tmaxf));
+#endif
+    const uint32_t key = (__float_as_uint(lo) & 0xFFFF0000u) | (static_cast<uint32_t>(child) & 0xFFFFu);
+    return lo <= hi ? key : kKeyMiss;  // empty slots carry a box no ray enters (layout.h kLdsEmptyChild)
+}
+__device__ __forceinline__ void slab4_packed(const float4& lx, const float4& hx, const float4& ly, const float4& hy, const float4& lz,
+                                             const float4& hz, const int4& ch, float ix, float iy, float iz, float oix, float oiy,
+                                             float oiz, float tminf, float tmaxf, uint32_t& q0, uint32_t& q1, uint32_t& q2, uint32_t& q3) {
+    const f2v vx = {ix, ix}, vy = {iy, iy}, vz = {iz, iz};
+    const f2v nx = {-oix, -oix}, ny = {-oiy, -oiy}, nz = {-oiz, -oiz};
+    const f2v x0a = __builtin_elementwise_fma(f2v{lx.x, lx.y}, vx, nx), x0b = __builtin_elementwise_fma(f2v{lx.z, lx.w}, vx, nx);
+    const f2v x1a = __builtin_elementwise_fma(f2v{hx.x, hx.y}, vx, nx), x1b = __builtin_elementwise_fma(f2v{hx.z, hx.w}, vx, nx);
+    const f2v y0a = __builtin_elementwise_fma(f2v{ly.x, ly.y}, vy, ny), y0b = __builtin_elementwise_fma(f2v{ly.z, ly.w}, vy, ny);
+    const f2v y1a = __builtin_elementwise_fma(f2v{hy.x, hy.y}, vy, ny), y1b = __builtin_elementwise_fma(f2v{hy.z, hy.w}, vy, ny);
+    const f2v z0a = __builtin_elementwise_fma(f2v{lz.x, lz.y}, vz, nz), z0b = __builtin_elementwise_fma(f2v{lz.z, lz.w}, vz, nz);
+    const f2v z1a = __builtin_elementwise_fma(f2v{hz.x, hz.y}, vz, nz), z1b = __builtin_elementwise_fma(f2v{hz.z, hz.w}, vz, nz);
+    q0 = slab_key_packed(x0a.x, x1a.x, y0a.x, y1a.x, z0a.x, z1a.x, ch.x, tminf, tmaxf);
+    q1 = slab_key_packed(x0a.y, x1a.y, y0a.y, y1a.y, z0a.y, z1a.y, ch.y, tminf, tmaxf);
+    q2 = slab_key_packed(x0b.x, x1b.x, y0b.x, y1b.x, z0b.x, z1b.x, ch.z, tminf, tmaxf);
+    q3 = slab_key_packed(x0b.y, x1b.y, y0b.y, y1b.y, z0b.y, z1b.y, ch.w, tminf, tmaxf);
+}
+__device__ __forceinline__ void ucas(uint32_t& a, uint32_t& b) {
+    const uint32_t lo = a < b ? a : b;
+    b = a < b ? b : a;
+    a = lo;
+}
 __device__ __forceinline__ void cas(float& ka, int32_t& ca, float& kb, int32_t& cb) {
     const bool s = kb < ka;
     const float k = s ? kb : ka;
@@ -304,6 +356,9 @@ __device__ __forceinline__ void stat_lane(int k) { atomicAdd(&g_art_stats[k], 1u
 #ifndef ART_SPECULATIVE
 #define ART_SPECULATIVE 1
 #endif
+#ifndef ART_MED3
+#define ART_MED3 1
+#endif
 // Traversal stack entry: node/leaf codes, 16 bits in the LDS-scene variant (layout.h lds_leaf), 32 bits otherwise.
 template <bool L> using StackT = typename std::conditional<L, int16_t, int32_t>::type;
 
@@ -311,6 +366,7 @@ template <bool L> using StackT = typename std::conditional<L, int16_t, int32_t>:
 template <class R, uint32_t F, int B, bool L>
 __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* lds, int32_t root, const Ray<R>& r, R tmin, R tmax,
                                          StackT<L>* stk, R& t, uint32_t& prim, uint32_t& face, uint32_t& mt) {
+    static_assert(!(L && (F & F_MEDIA)), "packed LDS keys need tmin > 0: no medium boundary tests in the LDS variant");
     const float ox = static_cast<float>(r.o.x), oy = static_cast<float>(r.o.y), oz = static_cast<float>(r.o.z);
     const float ix = 1.0f / static_cast<float>(r.d.x), iy = 1.0f / static_cast<float>(r.d.y), iz = 1.0f / static_cast<float>(r.d.z);
     const float oix = ox * ix, oiy = oy * iy, oiz = oz * iz;
@@ -344,27 +400,50 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                 lx = np[0]; hx = np[1]; ly = np[2]; hy = np[3]; lz = np[4]; hz = np[5];
                 ch = reinterpret_cast<const int4*>(np)[6];
             }
-            float k0, k1, k2, k3;
-            slab4(lx, hx, ly, hy, lz, hz, ch, ix, iy, iz, oix, oiy, oiz, tminf, tmaxf, k0, k1, k2, k3);
-            int32_t c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
-            // sorting network: ascending entry distance, misses (+inf) last
-            cas(k0, c0, k1, c1);
-            cas(k2, c2, k3, c3);
-            cas(k0, c0, k2, c2);
-            cas(k1, c1, k3, c3);
-            cas(k1, c1, k2, c2);
-            // branchless pushes (far to near): every write lands at or below the final top, which the stack's spare row
-            // covers; the pop reads the entry under the top, the per-lane sentinel row (kNodeEmpty) when the stack is empty
-            const float inf = __builtin_inff();
-            stk[sp * B] = static_cast<StackT<L>>(c3);
-            sp += k3 < inf;
-            stk[sp * B] = static_cast<StackT<L>>(c2);
-            sp += k2 < inf;
-            stk[sp * B] = static_cast<StackT<L>>(c1);
-            sp += k1 < inf;
+            // branchless pushes (far to near) after a sorting network (ascending entry distance, misses last): every
+            // write lands at or below the final top, which the stack's spare row covers; the pop reads the entry under
+            // the top, the per-lane sentinel row (kNodeEmpty) when the stack is empty
+            bool near;
+            int32_t near_child;
+            if constexpr (L) {
+                // 16-bit child codes ride in the low half of the entry-distance keys: the network is 5 integer
+                // min/max pairs and each code comes back with one bit-field extract
+                uint32_t q0, q1, q2, q3;
+                slab4_packed(lx, hx, ly, hy, lz, hz, ch, ix, iy, iz, oix, oiy, oiz, tminf, tmaxf, q0, q1, q2, q3);
+                ucas(q0, q1);
+                ucas(q2, q3);
+                ucas(q0, q2);
+                ucas(q1, q3);
+                ucas(q1, q2);
+                stk[sp * B] = static_cast<StackT<L>>(q3);
+                sp += q3 < kKeyMiss;
+                stk[sp * B] = static_cast<StackT<L>>(q2);
+                sp += q2 < kKeyMiss;
+                stk[sp * B] = static_cast<StackT<L>>(q1);
+                sp += q1 < kKeyMiss;
+                near = q0 < kKeyMiss;
+                near_child = static_cast<int16_t>(q0);
+            } else {
+                float k0, k1, k2, k3;
+                slab4(lx, hx, ly, hy, lz, hz, ch, ix, iy, iz, oix, oiy, oiz, tminf, tmaxf, k0, k1, k2, k3);
+                int32_t c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
+                cas(k0, c0, k1, c1);
+                cas(k2, c2, k3, c3);
+                cas(k0, c0, k2, c2);
+                cas(k1, c1, k3, c3);
+                cas(k1, c1, k2, c2);
+                const float inf = __builtin_inff();
+                stk[sp * B] = static_cast<StackT<L>>(c3);
+                sp += k3 < inf;
+                stk[sp * B] = static_cast<StackT<L>>(c2);
+                sp += k2 < inf;
+                stk[sp * B] = static_cast<StackT<L>>(c1);
+                sp += k1 < inf;
+                near = k0 < inf;
+                near_child = c0;
+            }
             const int32_t top = stk[(sp - 1) * B];
-            const bool near = k0 < inf;
-            node = near ? c0 : top;
+            node = near ? near_child : top;
             sp -= (!near && sp > 0) ? 1 : 0;
 #if ART_SPECULATIVE
             if (node < kNodeEmpty && parked == kNodeEmpty) {  // a leaf (codes below -1) and none parked yet: park it
@@ -559,7 +638,7 @@ __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref,
             const SphereRec<R>& sp = S.spheres[idx];
             V3<R> center = ld3(sp.c);
             const bool moving = (sp.flags & SPH_MOVING) != 0;
-            if (moving) center = center + ((r.tm - sp.t0) / sp.dt) * ld3(sp.d);
+            if (moving) center = center + motion_fraction(r.tm, sp.t0, sp.dt) * ld3(sp.d);
             s.p = r.at(t);
             const V3<R> outward = divs(s.p - center, sp.r);
             set_face_normal(s, r, outward);

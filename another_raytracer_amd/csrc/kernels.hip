@@ -375,7 +375,7 @@ __device__ __forceinline__ bool shade_hit_lds(const uint8_t* lds, uint32_t slot,
     if (mv) {  // moving_sphere.h:72-74, as prim_surface
         const double2* mp = reinterpret_cast<const double2*>(lds + kLdsOffMov) + (mv - 1);
         const double2 m0 = mp[0], m1 = mp[kLdsMovCap], m2 = mp[2 * kLdsMovCap];
-        center = center + ((st.ray.tm - m1.y) / m2.x) * V3<R>{m0.x, m0.y, m1.x};
+        center = center + motion_fraction(st.ray.tm, m1.y, m2.x) * V3<R>{m0.x, m0.y, m1.x};
     }
     Surf<R> s;
     s.p = st.ray.at(t);
@@ -387,25 +387,31 @@ __device__ __forceinline__ bool shade_hit_lds(const uint8_t* lds, uint32_t slot,
         return false;
     }
     if (last) return false;
+    // The three materials of a wave share their costly steps (each lane still draws exactly its own material's
+    // sequence): lambertian and metal both start with random_in_unit_sphere() (material.h:33, :55 -- metal's
+    // unit_vector(r_in.direction()) draws nothing), and all three need one unit_vector (of that sample for
+    // lambertian, of the ray direction for metal and dielectric), so the wave runs one rejection loop and one
+    // sqrt + divide sequence instead of one per material present.
+    const bool lamb = mtype == MAT_LAMBERTIAN;
+    V3<R> ps = mk(R(0), R(0), R(0));
+    if (mtype != MAT_DIELECTRIC) ps = in_unit_sphere<R>(st.rng);
+    const V3<R> u = unit(lamb ? ps : st.ray.d);
     V3<R> att, dir;
-    if (mtype == MAT_LAMBERTIAN) {  // material.h:20-43
-        const V3<R> rv = unit(in_unit_sphere<R>(st.rng));
-        dir = s.n + rv;
+    if (lamb) {  // material.h:20-43
+        dir = s.n + u;
         if (near_zero(dir)) dir = s.n;
         att = lds_mat_color(lds, (checker && checker_odd(s.p)) ? e + 1 : e);
     } else if (mtype == MAT_METAL) {  // material.h:45-61
         const double2* m = reinterpret_cast<const double2*>(lds + kLdsOffMat) + 2 * e;
         const double2 ma = m[0], mb = m[1];
-        const V3<R> reflected = reflect(unit(st.ray.d), s.n);
-        dir = reflected + mb.y * in_unit_sphere<R>(st.rng);
+        dir = reflect(u, s.n) + mb.y * ps;
         att = mk(ma.x, ma.y, mb.x);
         if (!(dot(dir, s.n) > R(0))) return false;
     } else {  // dielectric, material.h:63-99
         const R ir = (reinterpret_cast<const double2*>(lds + kLdsOffMat) + 2 * e)[1].y;
         att = mk(R(1), R(1), R(1));
         const R ratio = s.ff ? (R(1) / ir) : ir;
-        const V3<R> ud = unit(st.ray.d);
-        const R cos_theta = fmin(dot(-ud, s.n), R(1));
+        const R cos_theta = fmin(dot(-u, s.n), R(1));
         const R sin_theta = sqrt(R(1) - cos_theta * cos_theta);
         const bool cannot = ratio * sin_theta > R(1);
         bool refl = cannot;
@@ -415,7 +421,7 @@ __device__ __forceinline__ bool shade_hit_lds(const uint8_t* lds, uint32_t slot,
             const R refl_p = r0 + (R(1) - r0) * pow((R(1) - cos_theta), R(5));
             refl = refl_p > uniform<R>(st.rng);
         }
-        dir = refl ? reflect(ud, s.n) : refract(ud, s.n, ratio);
+        dir = refl ? reflect(u, s.n) : refract(u, s.n, ratio);
     }
     st.T = st.T * att;
     st.ray.o = s.p;
@@ -592,10 +598,18 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S, PassGe
     using R = double;
     constexpr int B = kBlockL;
     extern __shared__ __align__(16) uint8_t smem[];
+    // the camera and pass geometry are read from LDS where a new path starts instead of being held in registers for
+    // the whole kernel (as kernel arguments they pin ~60 SGPRs, which spill)
+    __shared__ CameraRec<double> s_cam;
+    __shared__ PassGeom s_g;
     const uint8_t* lds = smem;
     StackT<true>* stk = reinterpret_cast<StackT<true>*>(smem + kLdsImageBytes) + B + threadIdx.x;
     stk[-B] = static_cast<StackT<true>>(kNodeEmpty);
     load_lds_image<B>(S.lds_image, smem);
+    if (threadIdx.x == 0) {
+        s_cam = cam;
+        s_g = g;
+    }
     __syncthreads();
     const uint32_t lane = __lane_id();
     const uint64_t below = (1ull << lane) - 1ull;
@@ -631,8 +645,11 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S, PassGe
                 } else {
                     int lx, ly;
                     q = slot;
-                    if (slot_pixel(g, slot % g.npix_pad, lx, ly)) {
-                        gen_ray(g, cam, q, lx, ly, st);
+                    // compiler barrier: the LDS camera/geometry loads stay here instead of being hoisted out of
+                    // the loop into ~40 long-lived registers
+                    __asm__ volatile("" ::: "memory");
+                    if (slot_pixel(s_g, slot % g.npix_pad, lx, ly)) {
+                        gen_ray(s_g, s_cam, q, lx, ly, st);
                         busy = true;
                         depth = 0;
                     }
@@ -941,11 +958,17 @@ static std::vector<uint8_t> lds_scene_image(const FlatScene& f, uint32_t& nmov, 
     auto put = [&](uint32_t off, const void* v, size_t n) { std::memcpy(img.data() + off, v, n); };
     for (size_t n = 0; n < f.nodes.size(); ++n) {
         const BvhNode& b = f.nodes[n];
-        const float* planes[6] = {b.lox, b.hix, b.loy, b.hiy, b.loz, b.hiz};
-        for (uint32_t j = 0; j < 6; ++j) put(kLdsOffNodes + (j * kLdsNodeCap + static_cast<uint32_t>(n)) * 16, planes[j], 16);
+        float planes[6][4];
+        const float* src[6] = {b.lox, b.hix, b.loy, b.hiy, b.loz, b.hiz};
         int32_t child[4];
-        for (int c = 0; c < 4; ++c)
-            child[c] = (b.child[c] >= 0 || b.child[c] == kNodeEmpty) ? b.child[c] : lds_leaf(leaf_first(b.child[c]), leaf_count(b.child[c]));
+        for (int c = 0; c < 4; ++c) {
+            // an empty slot becomes an empty leaf behind a point box at (3e38, 3e38, 3e38): no slab test of it needs
+            // a child check, and the astronomically rare ray whose three slab times coincide there finds no primitives
+            const bool empty = b.child[c] == kNodeEmpty;
+            for (int j = 0; j < 6; ++j) planes[j][c] = empty ? kLdsEmptyBox : src[j][c];
+            child[c] = empty ? kLdsEmptyChild : b.child[c] >= 0 ? b.child[c] : lds_leaf(leaf_first(b.child[c]), leaf_count(b.child[c]));
+        }
+        for (uint32_t j = 0; j < 6; ++j) put(kLdsOffNodes + (j * kLdsNodeCap + static_cast<uint32_t>(n)) * 16, planes[j], 16);
         put(kLdsOffNodes + (6 * kLdsNodeCap + static_cast<uint32_t>(n)) * 16, child, 16);
     }
     // shading table: one entry per material (two for a checker of solid colours); anything else keeps the scene off

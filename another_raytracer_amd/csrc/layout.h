@@ -109,6 +109,10 @@ constexpr uint32_t kLdsLeafShift = 10;
 constexpr uint32_t kLdsLeafMaxCount = 31;
 ART_HD int32_t lds_leaf(uint32_t first, uint32_t count) { return ~static_cast<int32_t>((count << kLdsLeafShift) | first); }
 constexpr uint32_t kLdsRefIndexMask = (1u << kLdsRefMovShift) - 1;
+// Empty child slots of the image: a count-0 leaf (distinct from the kNodeEmpty stack sentinel) behind a point box far
+// outside any scene, so the traversal needs no per-child empty test.
+constexpr int32_t kLdsEmptyChild = ~static_cast<int32_t>(1u);
+constexpr float kLdsEmptyBox = 3.0e38f;
 static_assert(kLdsMovCap + 1 < (1u << (kLdsRefMatShift - kLdsRefMovShift)), "moving index field");
 static_assert(kLdsImageBytes % 16 == 0, "LDS image is copied in 16-B pieces");
 

@@ -43,12 +43,19 @@ def main(tag, scene, prec, segments_per_step, variant=2, root="gpurun_out"):
             e["hbm_write_bytes"] = v["WRITE_SIZE"] * 1024
         if "SQ_INSTS_VALU" in v and "SQ_WAVES" in v and v["SQ_WAVES"]:
             e["valu_insts_per_wave"] = v["SQ_INSTS_VALU"] / v["SQ_WAVES"]
+        if "SQ_INSTS_VALU" in v and v.get("GRBM_GUI_ACTIVE"):
+            # VALU issue share: 4 cycles per wave64 instruction over 1024 SIMDs x per-XCD busy cycles (GRBM_GUI_ACTIVE
+            # is summed over the 8 XCDs); transcendentals take longer, so this is a lower estimate
+            e["valu_busy"] = v["SQ_INSTS_VALU"] * 4 / (1024 * v["GRBM_GUI_ACTIVE"] / 8)
         kernels[short] = e
-    ext = {k: v for k, v in kernels.items() if k.startswith("art::k_extend")}
+    ext = {k: v for k, v in kernels.items() if k.startswith("art::k_extend") or k.startswith("art::k_paths")}
     total = lambda key: sum(v.get(key, 0) for v in ext.values())
     res = {"tag": tag, "scene": scene, "precision": prec, "segments": segments_per_step, "extend_variant": variant,
            "kernels": kernels,
            "note": "hbm_read_bytes_corrected = 2*FETCH_SIZE*1024 (gfx950 half-count correction), hbm_write_bytes = WRITE_SIZE*1024"}
+    busy = [v["valu_busy"] for v in ext.values() if "valu_busy" in v]
+    if busy:
+        res["valu_busy"] = round(max(busy), 4)
     if segments_per_step and ext:
         res["extend_bytes_per_segment"] = (total("hbm_read_bytes_corrected") + total("hbm_write_bytes")) / segments_per_step
         res["extend_read_bytes_per_segment"] = total("hbm_read_bytes_corrected") / segments_per_step
