@@ -74,13 +74,24 @@ __device__ __forceinline__ R uniform(uint64_t& s) {
     return static_cast<R>(x >> 8) * static_cast<R>(1.0 / 16777216.0);
 }
 template <class R> __device__ __forceinline__ R uniform(uint64_t& s, R lo, R hi) { return lo + (hi - lo) * uniform<R>(s); }
+// uniform(s, -1, 1) = -1 + 2 * (k * 2^-24) with k < 2^24: every step is exact, so the single fma k * 2^-23 - 1 is the
+// same value
+template <class R>
+__device__ __forceinline__ R uniform_pm1(uint64_t& s) {
+    const uint64_t old = s;
+    s = old * 6364136223846793005ull + 1442695040888963407ull;
+    const uint32_t xs = static_cast<uint32_t>(((old >> 18u) ^ old) >> 27u);
+    const uint32_t rot = static_cast<uint32_t>(old >> 59u);
+    const uint32_t x = (xs >> rot) | (xs << ((32u - rot) & 31u));
+    return fma(static_cast<R>(x >> 8), static_cast<R>(1.0 / 8388608.0), R(-1));
+}
 template <class R>
 __device__ __forceinline__ V3<R> in_unit_sphere(uint64_t& s) {  // vec3.h:117-123, draws x, y, z
     for (;;) {
         V3<R> p;
-        p.x = uniform<R>(s, R(-1), R(1));
-        p.y = uniform<R>(s, R(-1), R(1));
-        p.z = uniform<R>(s, R(-1), R(1));
+        p.x = uniform_pm1<R>(s);
+        p.y = uniform_pm1<R>(s);
+        p.z = uniform_pm1<R>(s);
         if (len2(p) >= R(1)) continue;
         return p;
     }
@@ -112,11 +123,11 @@ constexpr uint32_t kMediumHit = 0xFFFFFFFFu;  // hit.prim value of a constant_me
 // ------------------------------------------------------------------------------------------------ primitives
 // sphere.h:39-65 / moving_sphere.h:41-58 (root selection only; the surface is rebuilt in shade).
 template <class R>
-__device__ __forceinline__ bool hit_sphere_at(V3<R> center, R radius, const Ray<R>& r, R tmin, R tmax, R& t) {
+__device__ __forceinline__ bool hit_sphere_r2(V3<R> center, R r2, const Ray<R>& r, R tmin, R tmax, R& t) {  // r2 = radius * radius
     const V3<R> oc = r.o - center;
     const R a = len2(r.d);
     const R half_b = dot(oc, r.d);
-    const R c = len2(oc) - radius * radius;
+    const R c = len2(oc) - r2;
     const R disc = half_b * half_b - a * c;
     if (disc < R(0)) return false;
     const R sqrtd = sqrt(disc);
@@ -127,6 +138,10 @@ __device__ __forceinline__ bool hit_sphere_at(V3<R> center, R radius, const Ray<
     }
     t = root;
     return true;
+}
+template <class R>
+__device__ __forceinline__ bool hit_sphere_at(V3<R> center, R radius, const Ray<R>& r, R tmin, R tmax, R& t) {
+    return hit_sphere_r2(center, radius * radius, r, tmin, tmax, t);
 }
 // moving_sphere.h:72-74 center(time) = center0 + ((time - time0) / (time1 - time0)) * (center1 - center0)
 // (time - time0) / (time1 - time0): x / 1 == x exactly, so the divide is skipped for the common unit shutter span
@@ -333,7 +348,7 @@ __device__ __forceinline__ bool hit_lds_slot(const uint8_t* lds, uint32_t slot, 
     }
     prim = make_primref(PRIM_SPHERE, code & kLdsRefIndexMask);
     mt = code >> kLdsRefMatShift;
-    return hit_sphere_at(center, b.y, r, tmin, tmax, t);
+    return hit_sphere_r2(center, b.y, r, tmin, tmax, t);
 }
 
 #ifdef ART_STATS

@@ -299,8 +299,8 @@ __device__ __forceinline__ void gen_ray(const PassGeom& g, const CameraRec<R>& c
     const R t = (R(g.H - 1 - gy) + rv) / R(g.H - 1);
     V3<R> p;
     for (;;) {  // random_in_unit_disk (vec3.h:137-143): x, then y
-        p.x = uniform<R>(rng, R(-1), R(1));
-        p.y = uniform<R>(rng, R(-1), R(1));
+        p.x = uniform_pm1<R>(rng);
+        p.y = uniform_pm1<R>(rng);
         p.z = R(0);
         if (len2(p) >= R(1)) continue;
         break;
@@ -379,7 +379,7 @@ __device__ __forceinline__ bool shade_hit_lds(const uint8_t* lds, uint32_t slot,
     }
     Surf<R> s;
     s.p = st.ray.at(t);
-    set_face_normal(s, st.ray, divs(s.p - center, b.y));
+    set_face_normal(s, st.ray, reinterpret_cast<const double*>(lds + kLdsOffInvR)[slot] * (s.p - center));  // (p - c) / r
     const uint32_t e = mi & ~kLdsMatChecker;
     const bool checker = (mi & kLdsMatChecker) != 0;
     if (mtype == MAT_LIGHT) {  // material.h:114-116; diffuse_light never scatters
@@ -986,10 +986,11 @@ static std::vector<uint8_t> lds_scene_image(const FlatScene& f, uint32_t& nmov, 
     for (size_t slot = 0; slot < f.primrefs.size(); ++slot) {
         const uint32_t idx = primref_index(f.primrefs[slot]);
         const auto& sp = f.spheres[idx];
-        const double p0[2] = {sp.c[0], sp.c[1]}, p1[2] = {sp.c[2], sp.r};
+        const double p0[2] = {sp.c[0], sp.c[1]}, p1[2] = {sp.c[2], sp.r * sp.r}, inv_r = 1.0 / sp.r;
         const uint32_t sl = static_cast<uint32_t>(slot);
         put(kLdsOffSph + sl * 16, p0, 16);
         put(kLdsOffSph + (kLdsSlotCap + sl) * 16, p1, 16);
+        put(kLdsOffInvR + sl * 8, &inv_r, 8);
         uint32_t code = idx | (f.mats[sp.mat].type << kLdsRefMatShift);
         if (sp.flags & SPH_MOVING) {
             const double m0[2] = {sp.d[0], sp.d[1]}, m1[2] = {sp.d[2], sp.t0}, m2[2] = {sp.dt, 0.0};

@@ -99,7 +99,11 @@ constexpr uint32_t kLdsOffMatIdx = kLdsOffRef + kLdsSlotCap * 4;
 constexpr uint32_t kLdsMatCap = 512;
 constexpr uint32_t kLdsMatChecker = 0x8000u;
 constexpr uint32_t kLdsOffMat = kLdsOffMatIdx + kLdsSlotCap * 2;
-constexpr uint32_t kLdsImageBytes = kLdsOffMat + kLdsMatCap * 32;
+// 1/r per slot (f64): sphere.h's outward normal (p - c) / r is (1/r) * (p - c) in vec3.h, so the host-side
+// reciprocal is the same value the device would compute; the hit test's r*r is precomputed the same way (the
+// second sphere plane holds (cz, r*r)).
+constexpr uint32_t kLdsOffInvR = kLdsOffMat + kLdsMatCap * 32;
+constexpr uint32_t kLdsImageBytes = kLdsOffInvR + kLdsSlotCap * 8;
 constexpr uint32_t kLdsRefMovShift = 19;
 constexpr uint32_t kLdsRefMatShift = 29;
 constexpr uint32_t kMatUnknown = 0xFFu;  // HitOut::mt when the hit did not come from the LDS image
