@@ -1,7 +1,8 @@
-// bvh.cpp — binned SAH binary tree, collapsed into the 4-wide node array of layout.h (see bvh.h).
+// bvh.cpp — full-sweep SAH binary tree, collapsed into the 4-wide node array of layout.h (see bvh.h).
 #include "bvh.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <limits>
 #include <stdexcept>
@@ -10,9 +11,23 @@ namespace art {
 
 namespace {
 
-constexpr int kBins = 16;
 constexpr double kCostTraverse = 1.0;
-constexpr double kCostIntersect = 1.5;
+// SAH primitive-test cost relative to a (binary) node step; ART_SAH_CI / ART_SAH_LEAF override it and the leaf size
+// for builder experiments (tools/, not part of the product contract)
+double sah_ci() {
+    static const double v = [] {
+        const char* e = std::getenv("ART_SAH_CI");
+        return e ? std::atof(e) : 1.5;
+    }();
+    return v;
+}
+int sah_leaf() {
+    static const int v = [] {
+        const char* e = std::getenv("ART_SAH_LEAF");
+        return e ? std::max(1, std::min(16, std::atoi(e))) : kMaxLeafPrims;
+    }();
+    return v;
+}
 
 double area(const AABBd& b) {
     double dx = b.mx[0] - b.mn[0], dy = b.mx[1] - b.mn[1], dz = b.mx[2] - b.mn[2];
@@ -67,59 +82,45 @@ struct Builder {
         const int n = e - b;
         if (n == 1 || depth >= kMaxBvhDepth - 1) return make_leaf_node(b, e, box);
 
-        int axis = 0;  // binned SAH over the widest centroid axis
+        // full-sweep SAH over all three centroid axes (the scenes are small: ~1e3 - 1e4 primitives)
+        int axis = 0;
         double ext[3];
         for (int k = 0; k < 3; ++k) ext[k] = cb.mx[k] - cb.mn[k];
         if (ext[1] > ext[axis]) axis = 1;
         if (ext[2] > ext[axis]) axis = 2;
         int mid = -1;
-        if (ext[axis] > 0) {
-            AABBd bin_box[kBins];
-            int bin_n[kBins] = {0};
-            for (auto& bb : bin_box) bb = empty_box();
-            const double scale = kBins / ext[axis];
-            auto bin_of = [&](uint32_t p) {
-                int bi = static_cast<int>((cent[p][axis] - cb.mn[axis]) * scale);
-                return std::min(kBins - 1, std::max(0, bi));
-            };
-            for (int i = b; i < e; ++i) {
-                int bi = bin_of(idx[i]);
-                bin_n[bi]++;
-                grow(bin_box[bi], boxes[idx[i]]);
-            }
-            double right_area[kBins];
-            int right_n[kBins];
+        double best = std::numeric_limits<double>::infinity();
+        int best_axis = -1, best_split = -1;
+        const double parent = std::max(area(box), 1e-300);
+        std::vector<uint32_t> order[3];
+        std::vector<double> right_area(static_cast<size_t>(n) + 1);
+        for (int k = 0; k < 3; ++k) {
+            if (!(ext[k] > 0)) continue;
+            order[k].assign(idx.begin() + b, idx.begin() + e);
+            std::stable_sort(order[k].begin(), order[k].end(), [&](uint32_t x, uint32_t y) { return cent[x][k] < cent[y][k]; });
             AABBd acc = empty_box();
-            int cnt = 0;
-            for (int i = kBins - 1; i > 0; --i) {
-                grow(acc, bin_box[i]);
-                cnt += bin_n[i];
-                right_area[i] = area(acc);
-                right_n[i] = cnt;
+            for (int i = n - 1; i > 0; --i) {
+                grow(acc, boxes[order[k][static_cast<size_t>(i)]]);
+                right_area[static_cast<size_t>(i)] = area(acc);
             }
             acc = empty_box();
-            cnt = 0;
-            int best_split = -1;
-            double best = std::numeric_limits<double>::infinity();
-            const double parent = std::max(area(box), 1e-300);
-            for (int i = 1; i < kBins; ++i) {
-                grow(acc, bin_box[i - 1]);
-                cnt += bin_n[i - 1];
-                if (cnt == 0 || right_n[i] == 0) continue;
-                double cost = kCostTraverse + kCostIntersect * (area(acc) * cnt + right_area[i] * right_n[i]) / parent;
+            for (int i = 1; i < n; ++i) {
+                grow(acc, boxes[order[k][static_cast<size_t>(i - 1)]]);
+                const double cost = kCostTraverse + sah_ci() * (area(acc) * i + right_area[static_cast<size_t>(i)] * (n - i)) / parent;
                 if (cost < best) {
                     best = cost;
+                    best_axis = k;
                     best_split = i;
                 }
             }
-            if (best_split > 0) {
-                if (n <= kMaxLeafPrims && kCostIntersect * n <= best) return make_leaf_node(b, e, box);
-                auto it = std::partition(idx.begin() + b, idx.begin() + e, [&](uint32_t p) { return bin_of(p) < best_split; });
-                mid = static_cast<int>(it - idx.begin());
-            }
+        }
+        if (best_axis >= 0) {
+            if (n <= sah_leaf() && sah_ci() * n <= best) return make_leaf_node(b, e, box);
+            std::copy(order[best_axis].begin(), order[best_axis].end(), idx.begin() + b);
+            mid = b + best_split;
         }
         if (mid <= b || mid >= e) {  // degenerate centroids: object median
-            if (n <= kMaxLeafPrims) return make_leaf_node(b, e, box);
+            if (n <= sah_leaf()) return make_leaf_node(b, e, box);
             mid = b + n / 2;
             std::nth_element(idx.begin() + b, idx.begin() + mid, idx.begin() + e,
                              [&](uint32_t x, uint32_t y) { return cent[x][axis] < cent[y][axis]; });

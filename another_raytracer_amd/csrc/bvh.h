@@ -1,4 +1,4 @@
-// bvh.h — binned-SAH BVH over primitive boxes, emitted as the flat 64-B two-child node array of layout.h.
+// bvh.h — full-sweep SAH BVH over primitive boxes, collapsed into the flat 128-B four-child node array of layout.h.
 //
 // Replaces the reference's bvh_node (primitives/bvh.cpp:3-42: random split axis, median split, O(N^2) object
 // copies, 1-spans tested twice).  Closest-hit results do not depend on the tree, so the product builds the tree
