@@ -383,7 +383,9 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                                          StackT<L>* stk, R& t, uint32_t& prim, uint32_t& face, uint32_t& mt) {
     static_assert(!(L && (F & F_MEDIA)), "packed LDS keys need tmin > 0: no medium boundary tests in the LDS variant");
     const float ox = static_cast<float>(r.o.x), oy = static_cast<float>(r.o.y), oz = static_cast<float>(r.o.z);
-    const float ix = 1.0f / static_cast<float>(r.d.x), iy = 1.0f / static_cast<float>(r.d.y), iz = 1.0f / static_cast<float>(r.d.z);
+    // hardware reciprocal (1 ulp): the box test is conservative by its 2e-6 relative padding, far above that
+    const float ix = __builtin_amdgcn_rcpf(static_cast<float>(r.d.x)), iy = __builtin_amdgcn_rcpf(static_cast<float>(r.d.y)),
+                iz = __builtin_amdgcn_rcpf(static_cast<float>(r.d.z));
     const float oix = ox * ix, oiy = oy * iy, oiz = oz * iz;
     const float tminf = f_lo(tmin);
     float tmaxf = f_hi(tmax);
