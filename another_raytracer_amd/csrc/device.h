@@ -287,18 +287,12 @@ __device__ __forceinline__ void slab4(const float4& lx, const float4& hx, const 
 // boundary tests start at -inf), so unsigned order is distance order to 2^-7 relative -- it only orders the pushes;
 // misses get kKeyMiss, above every finite key.
 constexpr uint32_t kKeyMiss = 0x7F800000u;
+// x0/y0/z0: entry distances at the near planes, x1/y1/z1: exit distances at the far planes (planes picked by the
+// direction's sign, so no per-axis min/max; a NaN plane distance (0 * inf) drops out of max/min as before).
 __device__ __forceinline__ uint32_t slab_key_packed(float x0, float x1, float y0, float y1, float z0, float z1, int32_t child, float tminf,
                                                     float tmaxf) {
-    // z slab clipped to [tminf, tmaxf] by a median: med3(z0, z1, t) differs from max(min(z0, z1), tminf) (resp.
-    // min(max(z0, z1), tmaxf)) only when the whole z slab lies outside [tminf, tmaxf], where the box can then pass
-    // only with lo == hi exactly -- a conservative extra visit, never a missed box
-#if ART_MED3
-    const float lo = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), __builtin_amdgcn_fmed3f(z0, z1, tminf));
-    const float hi = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), __builtin_amdgcn_fmed3f(z0, z1, tmaxf));
-#else
-    const float lo = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), tminf));
-    const float hi = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), tmaxf));
-#endif
+    const float lo = fmaxf(fmaxf(x0, y0), fmaxf(z0, tminf));
+    const float hi = fminf(fminf(x1, y1), fminf(z1, tmaxf));
     const uint32_t key = (__float_as_uint(lo) & 0xFFFF0000u) | (static_cast<uint32_t>(child) & 0xFFFFu);
     return lo <= hi ? key : kKeyMiss;  // empty slots carry a box no ray enters (layout.h kLdsEmptyChild)
 }
@@ -371,9 +365,18 @@ __device__ __forceinline__ void stat_lane(int k) { atomicAdd(&g_art_stats[k], 1u
 #ifndef ART_SPECULATIVE
 #define ART_SPECULATIVE 1
 #endif
-#ifndef ART_MED3
-#define ART_MED3 1
-#endif
+// The LDS scene image lives at LDS address 0 (k_extend and k_paths allocate LDS dynamically only), so node fetches
+// take a plain 32-bit LDS byte address: no base add per load.
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef int i4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 lds_f4(uint32_t addr) {
+    const f4v v = *(__attribute__((address_space(3))) const f4v*)(size_t)addr;
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ int4 lds_i4(uint32_t addr) {
+    const i4v v = *(__attribute__((address_space(3))) const i4v*)(size_t)addr;
+    return make_int4(v.x, v.y, v.z, v.w);
+}
 // Traversal stack entry: node/leaf codes, 16 bits in the LDS-scene variant (layout.h lds_leaf), 32 bits otherwise.
 template <bool L> using StackT = typename std::conditional<L, int16_t, int32_t>::type;
 
@@ -387,6 +390,14 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
     const float ix = __builtin_amdgcn_rcpf(static_cast<float>(r.d.x)), iy = __builtin_amdgcn_rcpf(static_cast<float>(r.d.y)),
                 iz = __builtin_amdgcn_rcpf(static_cast<float>(r.d.z));
     const float oix = ox * ix, oiy = oy * iy, oiz = oz * iz;
+    // LDS variant: the near and far plane of each axis follow from the direction's sign, so the slab test reads them
+    // directly (near plane offset per axis; the far plane is the neighbouring plane, one kLdsPlane away) and needs no
+    // per-axis min/max
+    constexpr uint32_t kLdsPlane = kLdsNodeCap * 16;
+    static_assert((kLdsPlane & (kLdsPlane - 1)) == 0 && kLdsOffNodes % (2 * kLdsPlane) == 0, "plane pairs differ in one address bit");
+    const uint32_t off_nx = kLdsOffNodes + (0u + (__float_as_uint(ix) >> 31)) * kLdsPlane;
+    const uint32_t off_ny = kLdsOffNodes + (2u + (__float_as_uint(iy) >> 31)) * kLdsPlane;
+    const uint32_t off_nz = kLdsOffNodes + (4u + (__float_as_uint(iz) >> 31)) * kLdsPlane;
     const float tminf = f_lo(tmin);
     float tmaxf = f_hi(tmax);
     bool hit = false;
@@ -405,13 +416,18 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
         while (node >= 0) {
             ART_STAT_WAVE(0);
             ART_STAT_LANE(1);
-            float4 lx, hx, ly, hy, lz, hz;
+            float4 lx, hx, ly, hy, lz, hz;  // L: near (lx, ly, lz) and far (hx, hy, hz) planes
             int4 ch;
             if constexpr (L) {
-                const float4* np = reinterpret_cast<const float4*>(lds + kLdsOffNodes) + node;
-                lx = np[0]; hx = np[kLdsNodeCap]; ly = np[2 * kLdsNodeCap]; hy = np[3 * kLdsNodeCap];
-                lz = np[4 * kLdsNodeCap]; hz = np[5 * kLdsNodeCap];
-                ch = reinterpret_cast<const int4*>(np)[6 * kLdsNodeCap];
+                const uint32_t n16 = static_cast<uint32_t>(node) * 16u;
+                const uint32_t ax = n16 | off_nx, ay = n16 | off_ny, az = n16 | off_nz;
+                lx = lds_f4(ax);
+                hx = lds_f4(ax ^ kLdsPlane);
+                ly = lds_f4(ay);
+                hy = lds_f4(ay ^ kLdsPlane);
+                lz = lds_f4(az);
+                hz = lds_f4(az ^ kLdsPlane);
+                ch = lds_i4(kLdsOffNodes + 6 * kLdsPlane + n16);
             } else {
                 const float4* np = reinterpret_cast<const float4*>(S.nodes + node);
                 lx = np[0]; hx = np[1]; ly = np[2]; hy = np[3]; lz = np[4]; hz = np[5];

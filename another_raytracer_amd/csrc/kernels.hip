@@ -434,6 +434,10 @@ __device__ __forceinline__ bool shade_hit_lds(const uint8_t* lds, uint32_t slot,
 #endif
 // Blocks of the LDS-scene variant: one block per CU holds the scene image once for 16 waves (4 per SIMD).
 constexpr int kBlockL = ART_LDS_BLOCK;
+// LDS bytes of one k_extend block: scene image (L) + per-lane stack + the shard prefix array.
+__host__ __device__ constexpr size_t extend_pre_offset(bool L, uint32_t stack) {
+    return ((L ? kLdsImageBytes + sizeof(int16_t) * stack * kBlockL : sizeof(int32_t) * stack * kBlock) + 15u) & ~size_t(15);
+}
 
 // Copies the LDS scene image (layout.h) into LDS in one round: every lane issues all of its 16-B loads before its
 // first store, so the block pays one global-load latency instead of one per plane.
@@ -465,8 +469,9 @@ __global__ __launch_bounds__(L ? kBlockL : kBlock, L ? 1 : ART_EXTEND_MIN_WAVES)
                                                                                                  Work<R> w, int d) {
     constexpr int B = L ? kBlockL : kBlock;
     // dynamic LDS: [scene image (L only)][traversal stack: g.stack entries x B lanes] (sized per scene at launch)
+    // dynamic LDS only, so the scene image starts at LDS address 0 (device.h lds_f4)
     extern __shared__ __align__(16) uint8_t smem[];
-    __shared__ uint32_t pre[kShards + 1];
+    uint32_t* pre = reinterpret_cast<uint32_t*>(smem + extend_pre_offset(L, g.stack));
     const uint8_t* lds = smem;
     // row 0 of the stack region is this lane's sentinel (device.h traverse), entries start at row 1
     StackT<L>* stk = reinterpret_cast<StackT<L>*>(smem + (L ? kLdsImageBytes : 0u)) + B + threadIdx.x;
@@ -594,16 +599,22 @@ __global__ __launch_bounds__(L ? kBlockL : kBlock, L ? 1 : ART_EXTEND_MIN_WAVES)
 // below the ~88 M/s a single word sustains).  The bounce arithmetic and the RNG draws are those of the fused
 // k_extend, so images are bit-identical to the wavefront variants.
 constexpr uint32_t kPathChunk = 256;
+__host__ __device__ constexpr size_t paths_stack_bytes(uint32_t stack) { return (sizeof(int16_t) * stack * kBlockL + 15u) & ~size_t(15); }
+__host__ __device__ constexpr size_t paths_lds_bytes(uint32_t stack) {
+    return kLdsImageBytes + paths_stack_bytes(stack) + sizeof(CameraRec<double>) + sizeof(PassGeom);
+}
 __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S, PassGeom g, CameraRec<double> cam, Work<double> w, uint32_t* next_slot) {
     using R = double;
     constexpr int B = kBlockL;
+    // dynamic LDS only (no static __shared__, so the image starts at LDS address 0 and every image offset is an
+    // immediate): [scene image][traversal stack][camera][pass geometry] -- the camera and pass geometry are read
+    // from LDS where a new path starts instead of being held in registers for the whole kernel (as kernel arguments
+    // they pin ~60 SGPRs, which spill)
     extern __shared__ __align__(16) uint8_t smem[];
-    // the camera and pass geometry are read from LDS where a new path starts instead of being held in registers for
-    // the whole kernel (as kernel arguments they pin ~60 SGPRs, which spill)
-    __shared__ CameraRec<double> s_cam;
-    __shared__ PassGeom s_g;
     const uint8_t* lds = smem;
     StackT<true>* stk = reinterpret_cast<StackT<true>*>(smem + kLdsImageBytes) + B + threadIdx.x;
+    CameraRec<double>& s_cam = *reinterpret_cast<CameraRec<double>*>(smem + kLdsImageBytes + paths_stack_bytes(g.stack));
+    PassGeom& s_g = *reinterpret_cast<PassGeom*>(smem + kLdsImageBytes + paths_stack_bytes(g.stack) + sizeof(CameraRec<double>));
     stk[-B] = static_cast<StackT<true>>(kNodeEmpty);
     load_lds_image<B>(S.lds_image, smem);
     if (threadIdx.x == 0) {
@@ -932,10 +943,7 @@ constexpr size_t kLdsPerCu = 160 * 1024;  // gfx950
 
 // Traversal stack rows per lane: the worst-case depth + the sentinel row + the spare row of branchless pushes.
 static uint32_t stack_rows(int max_stack) { return static_cast<uint32_t>(std::max(1, max_stack)) + 2u; }
-// LDS bytes of one k_extend block: scene image (L) + per-lane stack.
-static size_t extend_lds_bytes(bool L, uint32_t stack) {
-    return L ? kLdsImageBytes + sizeof(int16_t) * stack * kBlockL : sizeof(int32_t) * stack * kBlock;
-}
+static size_t extend_lds_bytes(bool L, uint32_t stack) { return extend_pre_offset(L, stack) + 4 * (kShards + 1); }
 
 // Builds the layout.h LDS scene image when the f64 scene qualifies: spheres only, every BVH node and leaf slot within
 // the plane capacities, and image + stack within one CU's LDS.  Returns an empty vector otherwise.
@@ -944,7 +952,7 @@ static std::vector<uint8_t> lds_scene_image(const FlatScene& f, uint32_t& nmov, 
     nmov = 0;
     shade_ok = false;
     if ((f.features & ~kFeatSpheres) != 0 || f.nodes.empty() || f.nodes.size() > kLdsNodeCap || f.primrefs.size() > kLdsSlotCap ||
-        f.spheres.size() > kLdsRefIndexMask || extend_lds_bytes(true, stack_rows(f.max_stack)) + 4 * (kShards + 1) > kLdsPerCu)
+        f.spheres.size() > kLdsRefIndexMask || std::max(extend_lds_bytes(true, stack_rows(f.max_stack)), paths_lds_bytes(stack_rows(f.max_stack))) > kLdsPerCu)
         return img;
     for (uint32_t ref : f.primrefs) {
         if (primref_type(ref) != PRIM_SPHERE) return img;
@@ -1160,6 +1168,14 @@ size_t Renderer::scene_bytes(int fp) const {
 }
 const FlatScene& Renderer::flat() const { return impl_->flat; }
 
+// The LDS-scene kernels address the scene image at LDS address 0 (device.h lds_f4): they must declare no static
+// __shared__ variables, which would be placed first.
+static bool static_lds_is_zero(const void* kernel) {
+    hipFuncAttributes a{};
+    HIP_OK(hipFuncGetAttributes(&a, kernel));
+    if (a.sharedSizeBytes != 0) throw std::runtime_error("LDS-scene kernel has static LDS: the scene image would not start at address 0");
+    return true;
+}
 // Persistent extend grid for a given dynamic LDS size: every block the CUs can hold at once.
 template <class R, uint32_t F, bool L, bool FUSE>
 static int extend_blocks(int num_cu, size_t lds) {
@@ -1190,6 +1206,8 @@ static void launch_shade(uint32_t mat_types, bool tex_basic, int num_cu, hipStre
 template <class R, uint32_t F, bool L, bool FUSE>
 static void launch_extend(int num_cu, hipStream_t st, const DevScene<R>& S, const PassGeom& g, const CameraRec<R>& cam, const Work<R>& w, int d) {
     const size_t lds = extend_lds_bytes(L, g.stack);
+    static const bool checked = !L || static_lds_is_zero(reinterpret_cast<const void*>(k_extend<R, F, L, FUSE>));
+    (void)checked;
     static int blocks = 0;
     static size_t blocks_lds = ~size_t(0);
     if (lds != blocks_lds) {
@@ -1237,8 +1255,10 @@ static int extend_variant(const DeviceScene<R>& ds, int flags) {
 }
 static void launch_paths(int num_cu, hipStream_t st, const DevScene<double>& S, const PassGeom& g, const CameraRec<double>& cam,
                          const Work<double>& w, uint32_t* next_slot) {
-    const size_t lds = extend_lds_bytes(true, g.stack);
+    const size_t lds = paths_lds_bytes(g.stack);
     static size_t attr_lds = 0;
+    static const bool checked = static_lds_is_zero(reinterpret_cast<const void*>(k_paths));
+    (void)checked;
     if (lds > 64 * 1024 && lds != attr_lds) {
         HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_paths), hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
         attr_lds = lds;
