@@ -377,6 +377,34 @@ __device__ __forceinline__ int4 lds_i4(uint32_t addr) {
     const i4v v = *(__attribute__((address_space(3))) const i4v*)(size_t)addr;
     return make_int4(v.x, v.y, v.z, v.w);
 }
+// Per-lane traversal stack: entry k of a lane is stk[k * B]; stk[-B] holds the kNodeEmpty sentinel, so peek() on an
+// empty stack returns kNodeEmpty, and the row above the top takes the discarded write of a branchless push.
+template <int B, bool L> struct LaneStack;
+template <int B>
+struct LaneStack<B, true> {  // LDS-scene variant: 16-bit entries, tracked as the LDS byte address of the top row
+    static constexpr uint32_t kRow = 2u * B;
+    uint32_t bottom, top;
+    __device__ __forceinline__ explicit LaneStack(int16_t* stk)
+        : bottom(static_cast<uint32_t>(reinterpret_cast<size_t>((__attribute__((address_space(3))) int16_t*)stk)) - kRow), top(bottom) {}
+    __device__ __forceinline__ void push(int32_t v, bool keep) {
+        *(__attribute__((address_space(3))) int16_t*)(size_t)(top + kRow) = static_cast<int16_t>(v);
+        top += keep ? kRow : 0u;
+    }
+    __device__ __forceinline__ int32_t peek() const { return *(__attribute__((address_space(3))) const int16_t*)(size_t)top; }
+    __device__ __forceinline__ void pop_if(bool c) { top -= (c && top != bottom) ? kRow : 0u; }
+};
+template <int B>
+struct LaneStack<B, false> {  // 32-bit entries
+    int32_t* stk;
+    int sp = 0;
+    __device__ __forceinline__ explicit LaneStack(int32_t* s) : stk(s) {}
+    __device__ __forceinline__ void push(int32_t v, bool keep) {
+        stk[sp * B] = v;
+        sp += keep;
+    }
+    __device__ __forceinline__ int32_t peek() const { return stk[(sp - 1) * B]; }
+    __device__ __forceinline__ void pop_if(bool c) { sp -= (c && sp > 0) ? 1 : 0; }
+};
 // Traversal stack entry: node/leaf codes, 16 bits in the LDS-scene variant (layout.h lds_leaf), 32 bits otherwise.
 template <bool L> using StackT = typename std::conditional<L, int16_t, int32_t>::type;
 
@@ -401,7 +429,7 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
     const float tminf = f_lo(tmin);
     float tmaxf = f_hi(tmax);
     bool hit = false;
-    int sp = 0;
+    LaneStack<B, L> st(stk);
     int32_t node = root;
 #if ART_SPECULATIVE
     // Speculative while-while (Aila & Laine 2009): a lane that reaches a leaf parks it and keeps walking inner nodes
@@ -448,12 +476,9 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                 ucas(q0, q2);
                 ucas(q1, q3);
                 ucas(q1, q2);
-                stk[sp * B] = static_cast<StackT<L>>(q3);
-                sp += q3 < kKeyMiss;
-                stk[sp * B] = static_cast<StackT<L>>(q2);
-                sp += q2 < kKeyMiss;
-                stk[sp * B] = static_cast<StackT<L>>(q1);
-                sp += q1 < kKeyMiss;
+                st.push(static_cast<int32_t>(q3), q3 < kKeyMiss);
+                st.push(static_cast<int32_t>(q2), q2 < kKeyMiss);
+                st.push(static_cast<int32_t>(q1), q1 < kKeyMiss);
                 near = q0 < kKeyMiss;
                 near_child = static_cast<int16_t>(q0);
             } else {
@@ -466,23 +491,20 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                 cas(k1, c1, k3, c3);
                 cas(k1, c1, k2, c2);
                 const float inf = __builtin_inff();
-                stk[sp * B] = static_cast<StackT<L>>(c3);
-                sp += k3 < inf;
-                stk[sp * B] = static_cast<StackT<L>>(c2);
-                sp += k2 < inf;
-                stk[sp * B] = static_cast<StackT<L>>(c1);
-                sp += k1 < inf;
+                st.push(c3, k3 < inf);
+                st.push(c2, k2 < inf);
+                st.push(c1, k1 < inf);
                 near = k0 < inf;
                 near_child = c0;
             }
-            const int32_t top = stk[(sp - 1) * B];
+            const int32_t top = st.peek();
             node = near ? near_child : top;
-            sp -= (!near && sp > 0) ? 1 : 0;
+            st.pop_if(!near);
 #if ART_SPECULATIVE
             if (node < kNodeEmpty && parked == kNodeEmpty) {  // a leaf (codes below -1) and none parked yet: park it
                 parked = node;
-                node = stk[(sp - 1) * B];
-                sp -= sp > 0 ? 1 : 0;
+                node = st.peek();
+                st.pop_if(true);
             }
             if (!__any(parked == kNodeEmpty)) break;  // every lane still walking holds a leaf: test them together
 #endif
@@ -496,14 +518,14 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
         } else {
             if (node == kNodeEmpty) break;
             leaf = node;
-            node = stk[(sp - 1) * B];
-            sp -= sp > 0 ? 1 : 0;
+            node = st.peek();
+            st.pop_if(true);
         }
 #else
         if (node == kNodeEmpty) break;
         const int32_t leaf = node;
-        node = stk[(sp - 1) * B];
-        sp -= sp > 0 ? 1 : 0;
+        node = st.peek();
+        st.pop_if(true);
 #endif
         uint32_t first, cnt;
         if constexpr (L) {
