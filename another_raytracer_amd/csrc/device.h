@@ -146,6 +146,20 @@ template <class R>
 __device__ __forceinline__ bool hit_sphere_at(V3<R> center, R radius, const Ray<R>& r, R tmin, R tmax, R& t) {
     return hit_sphere_r2(center, radius * radius, r, tmin, tmax, t);
 }
+// std::pow(x, 5) of material.h:97 (Schlick reflectance).  x^5 is carried as a double-double product (each step's
+// rounding error recovered exactly by an fma) and rounded once: the correctly rounded x^5.  glibc's pow is within
+// 0.52 ulp of it and differs from it in ~0.09% of arguments (tests/test_pow5.py measures it), but the reflectance
+// only feeds the comparison refl_p > u against a uniform on the 2^-24 grid, so the branch taken is the same unless u
+// lies within 1 ulp of refl_p (probability < 2^-28 per draw).  Ten FLOPs instead of the generic log/exp pow, whose
+// table constants also spilled registers of the persistent kernel.  x = 1 - cos(theta) is 0 or >= 2^-53, so
+// nothing underflows.
+template <class R>
+__host__ __device__ __forceinline__ R pow5(R x) {
+    const R p = x * x, pe = fma(x, x, -p);                  // x^2 = p + pe exactly
+    const R q = p * p, qe = fma(p, p, -q) + (R(2) * p) * pe;  // x^4 = q + qe (pe^2 dropped: 2^-106 relative)
+    const R r = q * x, re = fma(q, x, -r) + qe * x;         // x^5 = r + re
+    return r + re;
+}
 // moving_sphere.h:72-74 center(time) = center0 + ((time - time0) / (time1 - time0)) * (center1 - center0)
 // (time - time0) / (time1 - time0): x / 1 == x exactly, so the divide is skipped for the common unit shutter span
 // (every moving sphere of the reference scenes) without changing a bit.

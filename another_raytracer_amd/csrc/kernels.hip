@@ -341,7 +341,7 @@ __device__ __forceinline__ bool scatter(const DevScene<R>& S, const MatRec<R>& m
         if (!cannot) {
             R r0 = (R(1) - ratio) / (R(1) + ratio);
             r0 = r0 * r0;
-            const R refl_p = r0 + (R(1) - r0) * pow((R(1) - cos_theta), R(5));
+            const R refl_p = r0 + (R(1) - r0) * pow5(R(1) - cos_theta);
             refl = refl_p > uniform<R>(st.rng);
         }
         dir = refl ? reflect(ud, s.n) : refract(ud, s.n, ratio);
@@ -418,7 +418,7 @@ __device__ __forceinline__ bool shade_hit_lds(const uint8_t* lds, uint32_t slot,
         if (!cannot) {
             R r0 = (R(1) - ratio) / (R(1) + ratio);
             r0 = r0 * r0;
-            const R refl_p = r0 + (R(1) - r0) * pow((R(1) - cos_theta), R(5));
+            const R refl_p = r0 + (R(1) - r0) * pow5(R(1) - cos_theta);
             refl = refl_p > uniform<R>(st.rng);
         }
         dir = refl ? reflect(u, s.n) : refract(u, s.n, ratio);
