@@ -124,23 +124,38 @@ struct DevScene {
 constexpr uint32_t kMediumHit = 0xFFFFFFFFu;  // hit.prim value of a constant_medium scattering event
 
 // ------------------------------------------------------------------------------------------------ primitives
-// sphere.h:39-65 / moving_sphere.h:41-58 (root selection only; the surface is rebuilt in shade).
+// x / a from a precomputed reciprocal inv_a = RN(1 / a): q = RN(x * inv_a) is within 1 ulp of x / a, the residual
+// x - q * a is exact in one fma, and RN(q + residual * inv_a) is then the correctly rounded quotient (Markstein's
+// theorem, e.g. Muller et al., Handbook of Floating-Point Arithmetic, 2nd ed., Thm. 4.10) -- the same bits as the
+// division, for a, x and the quotient away from the overflow/underflow ranges: 3 FLOPs instead of the ~10-instruction
+// scaled division sequence.  Callers guarantee the range (see hit_lds_slot and gen_ray).
 template <class R>
-__device__ __forceinline__ bool hit_sphere_r2(V3<R> center, R r2, const Ray<R>& r, R tmin, R tmax, R& t) {  // r2 = radius * radius
+__device__ __forceinline__ R div_rcp(R x, R a, R inv_a) {
+    const R q = x * inv_a;
+    return fma(fma(-q, a, x), inv_a, q);
+}
+
+// sphere.h:39-65 / moving_sphere.h:41-58 (root selection only; the surface is rebuilt in shade).  a = |d|^2 of the
+// ray; RCP: the two root divisions by a use div_rcp with inv_a = 1 / a (same bits).
+template <class R, bool RCP>
+__device__ __forceinline__ bool sphere_root(V3<R> center, R r2, const Ray<R>& r, R a, R inv_a, R tmin, R tmax, R& t) {
     const V3<R> oc = r.o - center;
-    const R a = len2(r.d);
     const R half_b = dot(oc, r.d);
     const R c = len2(oc) - r2;
     const R disc = half_b * half_b - a * c;
     if (disc < R(0)) return false;
     const R sqrtd = sqrt(disc);
-    R root = (-half_b - sqrtd) / a;
+    R root = RCP ? div_rcp(-half_b - sqrtd, a, inv_a) : (-half_b - sqrtd) / a;
     if (root < tmin || tmax < root) {
-        root = (-half_b + sqrtd) / a;
+        root = RCP ? div_rcp(-half_b + sqrtd, a, inv_a) : (-half_b + sqrtd) / a;
         if (root < tmin || tmax < root) return false;
     }
     t = root;
     return true;
+}
+template <class R>
+__device__ __forceinline__ bool hit_sphere_r2(V3<R> center, R r2, const Ray<R>& r, R tmin, R tmax, R& t) {  // r2 = radius * radius
+    return sphere_root<R, false>(center, r2, r, len2(r.d), R(0), tmin, tmax, t);
 }
 template <class R>
 __device__ __forceinline__ bool hit_sphere_at(V3<R> center, R radius, const Ray<R>& r, R tmin, R tmax, R& t) {
@@ -345,8 +360,9 @@ __device__ __forceinline__ void cas(float& ka, int32_t& ca, float& kb, int32_t& 
 }
 
 // Leaf slot test of the LDS scene image (layout.h): the same root selection as hit_sphere on the same f64 values.
-__device__ __forceinline__ bool hit_lds_slot(const uint8_t* lds, uint32_t slot, const Ray<double>& r, double tmin, double tmax,
-                                             double& t, uint32_t& prim, uint32_t& mt) {
+// d_a = |d|^2 and d_inv_a = 1 / d_a come from the traversal (once per ray).
+__device__ __forceinline__ bool hit_lds_slot(const uint8_t* lds, uint32_t slot, const Ray<double>& r, double d_a, double d_inv_a,
+                                             double tmin, double tmax, double& t, uint32_t& prim, uint32_t& mt) {
     const double2* sp = reinterpret_cast<const double2*>(lds + kLdsOffSph) + slot;
     const double2 a = sp[0], b = sp[kLdsSlotCap];
     const uint32_t code = reinterpret_cast<const uint32_t*>(lds + kLdsOffRef)[slot];
@@ -359,7 +375,7 @@ __device__ __forceinline__ bool hit_lds_slot(const uint8_t* lds, uint32_t slot, 
     }
     prim = make_primref(PRIM_SPHERE, code & kLdsRefIndexMask);
     mt = code >> kLdsRefMatShift;
-    return hit_sphere_r2(center, b.y, r, tmin, tmax, t);
+    return sphere_root<double, true>(center, b.y, r, d_a, d_inv_a, tmin, tmax, t);
 }
 
 #ifdef ART_STATS
@@ -445,6 +461,11 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
     const uint32_t off_nz = kLdsOffNodes + (4u + (__float_as_uint(iz) >> 31)) * kLdsPlane;
     const float tminf = f_lo(tmin);
     float tmaxf = f_hi(tmax);
+    // L: |d|^2 and its reciprocal for the leaf root divisions (div_rcp).  A traced direction is never zero (camera
+    // rays point at the focus plane, scatter directions pass near_zero / dot(d, n) > 0) and its components are 0 or
+    // differences of scene-scale doubles, so |d|^2 lies far inside div_rcp's range (> 2^-500, < 2^16).
+    const R d_a = L ? len2(r.d) : R(0);
+    const R d_inv_a = L ? R(1) / d_a : R(0);
     bool hit = false;
     LaneStack<B, L> st(stk);
     int32_t node = root;
@@ -560,7 +581,7 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
             uint32_t fc = 0, ref, m = kMatUnknown;
             bool h;
             if constexpr (L) {
-                h = hit_lds_slot(lds, first + k, r, tmin, tmax, tt, ref, m);
+                h = hit_lds_slot(lds, first + k, r, d_a, d_inv_a, tmin, tmax, tt, ref, m);
                 fc = first + k;  // the leaf slot travels in the face field (spheres have no face): LDS shading reads it
             } else {
                 ref = S.primrefs[first + k];

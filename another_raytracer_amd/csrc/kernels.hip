@@ -177,6 +177,7 @@ struct PassGeom {
     uint32_t stack;             // LDS traversal stack rows per lane (stack_rows)
     int32_t max_depth;
     uint64_t seed;
+    double inv_w1, inv_h1;      // RN(1 / (W - 1)), RN(1 / (H - 1)) for gen_ray's div_rcp (rt_render rejects W or H < 2)
     const uint32_t* list;       // pixel-list mode (engine_mode::adaptive levels): slot pixel = list[qi] (local ly*W+lx)
     uint32_t nlist;             //   for qi < nlist; nullptr = every local pixel in 8x8 tile order
 };
@@ -295,8 +296,8 @@ __device__ __forceinline__ void gen_ray(const PassGeom& g, const CameraRec<R>& c
     uint64_t rng = path_seed(g.seed, pixel, g.sample_base + j);
     const R ru = uniform<R>(rng);
     const R rv = uniform<R>(rng);
-    const R s = (R(lx) + ru) / R(g.W - 1);
-    const R t = (R(g.H - 1 - gy) + rv) / R(g.H - 1);
+    const R s = div_rcp(R(lx) + ru, R(g.W - 1), static_cast<R>(g.inv_w1));  // == (lx + ru) / (W - 1), same bits
+    const R t = div_rcp(R(g.H - 1 - gy) + rv, R(g.H - 1), static_cast<R>(g.inv_h1));
     V3<R> p;
     for (;;) {  // random_in_unit_disk (vec3.h:137-143): x, then y
         p.x = uniform_pm1<R>(rng);
@@ -1325,6 +1326,8 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     g.npix_pad = g.tiles_x * tiles_y * 64u;
     g.max_depth = p.max_depth;
     g.seed = p.seed;
+    g.inv_w1 = 1.0 / static_cast<double>(p.width - 1);
+    g.inv_h1 = 1.0 / static_cast<double>(p.height - 1);
     g.stack = stack_rows(ds.max_stack);
     const int variant = extend_variant(ds, p.flags);
     const bool mega = variant == EXT_MEGA;
