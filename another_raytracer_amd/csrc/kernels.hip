@@ -632,18 +632,6 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S, PassGe
     int depth = 0;
     PathState<R> st;
     unsigned long long segs = 0;
-#ifdef ART_STATS
-    // wave cycles per phase (s_memtime, no forced waits): [12] slot claim + camera rays, [13] traversal, [14] shading
-    unsigned long long tp[3] = {0, 0, 0}, tprev = __builtin_amdgcn_s_memtime();
-#define ART_PTICK(k)                                                        \
-    do {                                                                    \
-        const unsigned long long now_ = __builtin_amdgcn_s_memtime();       \
-        tp[k] += now_ - tprev;                                              \
-        tprev = now_;                                                       \
-    } while (0)
-#else
-#define ART_PTICK(k)
-#endif
     for (;;) {
         // every idle lane takes the next slot of the wave's chunk (padding slots of partial tiles stay idle a round)
         const uint64_t idle = __ballot(!busy && !drained);
@@ -680,7 +668,6 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S, PassGe
                 }
             }
         }
-        ART_PTICK(0);
         if (__ballot(busy) == 0) {
             if (__ballot(!drained) == 0) break;
             continue;
@@ -691,7 +678,6 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S, PassGe
             ++segs;
             bool cont = false;
             const bool hitw = trace_world<R, kFeatSpheres, B, true>(S, lds, st.ray, stk, st.rng, t, h);
-            ART_PTICK(1);
             if (hitw) {
                 cont = shade_hit_lds(lds, h.obj >> 16, h.mt, t, depth + 1 >= g.max_depth, st);
             } else {  // engine.h:455-456: miss -> background
@@ -704,15 +690,9 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S, PassGe
                 busy = false;
             }
         }
-        ART_PTICK(2);
     }
     for (int off = 32; off > 0; off >>= 1) segs += __shfl_xor(segs, off);
     if (lane == 0) atomicAdd(w.segments, segs);
-#ifdef ART_STATS
-    if (lane == 0)
-        for (int k = 0; k < 3; ++k) atomicAdd(&g_art_stats[12 + k], tp[k]);
-#endif
-#undef ART_PTICK
 }
 
 // Input: the kShards shards of material queue M at depth d (the extend stage sorted hits by material type).
@@ -1494,9 +1474,7 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
                      st[0], st[1], st[1] / (64.0 * st[0]), st[2], st[3], st[3] / (64.0 * st[2]), st[4], st[5], st[5] / (64.0 * st[4]), st[6],
                      double(st[1]) / st[6], double(st[3]) / st[6]);
         const double tt = double(st[8] + st[9] + st[10] + st[11]);
-        std::fprintf(stderr, "ART_STATS cycles: load %.3f trace %.3f shade %.3f append %.3f\n", st[8] / tt, st[9] / tt, st[10] / tt, st[11] / tt);
-        const double tq = double(st[12] + st[13] + st[14]);
-        if (tq > 0) std::fprintf(stderr, "ART_STATS k_paths wave cycles: claim+camera %.3f trace %.3f shade %.3f\n", st[12] / tq, st[13] / tq, st[14] / tq);
+        if (tt > 0) std::fprintf(stderr, "ART_STATS k_extend cycles: load %.3f trace %.3f shade %.3f append %.3f\n", st[8] / tt, st[9] / tt, st[10] / tt, st[11] / tt);
         std::memset(st, 0, sizeof st);
         HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(g_art_stats), st, sizeof st));
     }
