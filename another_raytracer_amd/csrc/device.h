@@ -53,40 +53,37 @@ struct Ray {
 };
 
 // ------------------------------------------------------------------------------------------------ RNG contract
-// xoroshiro64** (Blackman & Vigna), one 64-bit state per path, seeded from (seed, global pixel, sample) through
-// splitmix64 so the stream depends only on what is rendered, never on tiling or GPU count.  One step is one 32-bit
-// multiply plus shifts, rotates and xors (full-rate VALU ops; the 64-bit LCG multiply of PCG32 costs three
-// quarter-rate multiplies).  Uniforms carry the top 24 bits of the output: exact in f32/f64.
+// PCG32 (O'Neill), one 64-bit state per path, seeded from (seed, global pixel, sample) through splitmix64 so the
+// stream depends only on what is rendered, never on tiling or GPU count.  Uniforms carry 24 bits: exact in f32/f64.
 __host__ __device__ inline uint64_t splitmix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ull;
     x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
     x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
     return x ^ (x >> 31);
 }
-__host__ __device__ inline uint64_t path_seed(uint64_t seed, uint32_t pixel, uint32_t sample) {
-    const uint64_t z = splitmix64(((static_cast<uint64_t>(pixel) << 32) | sample) ^ splitmix64(seed));
-    return z ? z : 0x9E3779B97F4A7C15ull;  // the all-zero state is xoroshiro's fixed point
-}
-__host__ __device__ __forceinline__ uint32_t rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
-__host__ __device__ __forceinline__ uint32_t rng_next(uint64_t& s) {
-    uint32_t s0 = static_cast<uint32_t>(s), s1 = static_cast<uint32_t>(s >> 32);
-    const uint32_t r = rotl32(s0 * 0x9E3779BBu, 5) * 5u;
-    s1 ^= s0;
-    s0 = rotl32(s0, 26) ^ s1 ^ (s1 << 9);
-    s1 = rotl32(s1, 13);
-    s = (static_cast<uint64_t>(s1) << 32) | s0;
-    return r;
+__host__ __device__ inline uint64_t pcg_seed(uint64_t seed, uint32_t pixel, uint32_t sample) {
+    return splitmix64(((static_cast<uint64_t>(pixel) << 32) | sample) ^ splitmix64(seed));
 }
 template <class R>
 __device__ __forceinline__ R uniform(uint64_t& s) {
-    return static_cast<R>(rng_next(s) >> 8) * static_cast<R>(1.0 / 16777216.0);
+    const uint64_t old = s;
+    s = old * 6364136223846793005ull + 1442695040888963407ull;
+    const uint32_t xs = static_cast<uint32_t>(((old >> 18u) ^ old) >> 27u);
+    const uint32_t rot = static_cast<uint32_t>(old >> 59u);
+    const uint32_t x = (xs >> rot) | (xs << ((32u - rot) & 31u));
+    return static_cast<R>(x >> 8) * static_cast<R>(1.0 / 16777216.0);
 }
 template <class R> __device__ __forceinline__ R uniform(uint64_t& s, R lo, R hi) { return lo + (hi - lo) * uniform<R>(s); }
 // uniform(s, -1, 1) = -1 + 2 * (k * 2^-24) with k < 2^24: every step is exact, so the single fma k * 2^-23 - 1 is the
 // same value
 template <class R>
 __device__ __forceinline__ R uniform_pm1(uint64_t& s) {
-    return fma(static_cast<R>(rng_next(s) >> 8), static_cast<R>(1.0 / 8388608.0), R(-1));
+    const uint64_t old = s;
+    s = old * 6364136223846793005ull + 1442695040888963407ull;
+    const uint32_t xs = static_cast<uint32_t>(((old >> 18u) ^ old) >> 27u);
+    const uint32_t rot = static_cast<uint32_t>(old >> 59u);
+    const uint32_t x = (xs >> rot) | (xs << ((32u - rot) & 31u));
+    return fma(static_cast<R>(x >> 8), static_cast<R>(1.0 / 8388608.0), R(-1));
 }
 template <class R>
 __device__ __forceinline__ V3<R> in_unit_sphere(uint64_t& s) {  // vec3.h:117-123, draws x, y, z

@@ -6,7 +6,7 @@
 //   for depth d < max_depth:
 //     k_extend<R, F>           closest hit over the world list (LDS-stack BVH traversal, f32 boxes, R leaf tests);
 //                              at depth 0 it first generates the camera ray of every (pixel, sample) slot itself
-//                              (xoroshiro64** keyed by (seed, pixel, sample)); F = the scene's feature subset (layout.h),
+//                              (PCG32 keyed by (seed, pixel, sample)); F = the scene's feature subset (layout.h),
 //                              misses finish their path (L += T*background); hits are appended to one of five
 //                              material queues (branch sorting for the shade stage)
 //     k_shade<R, F, M, TF>     one launch per material type M present: emitted + scatter on that material's queue
@@ -293,7 +293,7 @@ __device__ __forceinline__ void gen_ray(const PassGeom& g, const CameraRec<R>& c
     const uint32_t j = q / g.npix_pad;
     const int gy = global_row(g, ly);
     const uint32_t pixel = static_cast<uint32_t>(gy) * static_cast<uint32_t>(g.W) + static_cast<uint32_t>(lx);
-    uint64_t rng = path_seed(g.seed, pixel, g.sample_base + j);
+    uint64_t rng = pcg_seed(g.seed, pixel, g.sample_base + j);
     const R ru = uniform<R>(rng);
     const R rv = uniform<R>(rng);
     const R s = div_rcp(R(lx) + ru, R(g.W - 1), static_cast<R>(g.inv_w1));  // == (lx + ru) / (W - 1), same bits

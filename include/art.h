@@ -23,9 +23,8 @@
  *
  * RNG contract: the reference draws from one global std::mt19937 (tracer_utils.h:27-31).  Scene construction here
  * replays that generator exactly (seed 5489, same draw order), so scenes are bit-identical.  Rendering draws come
- * from xoroshiro64** streams, seeded through splitmix64 from (seed, global pixel j*W+i, sample index): results depend
- * on neither the tiling nor the GPU count, and oracle/restate.cpp (ORC_PCG, "pcg" = per-path counter-based streams)
- * replays the same streams on the CPU.
+ * from PCG32 streams keyed by (seed, global pixel j*W+i, sample index): results depend on neither the tiling nor the
+ * GPU count, and oracle/restate.cpp (ORC_PCG) replays the same streams on the CPU.
  */
 #ifndef ART_H
 #define ART_H

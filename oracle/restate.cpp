@@ -105,17 +105,14 @@ struct Rng {
         if (r >= 1.0) r = std::nextafter(1.0, 0.0);
         return r;
     }
-    // The product's stream contract (include/art.h "RNG contract", csrc/device.h rng_next): xoroshiro64**, top 24
-    // bits of each output as the uniform, exact in f32 and f64.
+    // The product's PCG32 contract (include/art.h "RNG contract"): 24-bit uniforms, exact in f32 and f64.
     double pcg_uniform() {
-        uint32_t s0 = static_cast<uint32_t>(state), s1 = static_cast<uint32_t>(state >> 32);
-        const uint32_t m = s0 * 0x9E3779BBu;
-        const uint32_t r = ((m << 5) | (m >> 27)) * 5u;
-        s1 ^= s0;
-        s0 = ((s0 << 26) | (s0 >> 6)) ^ s1 ^ (s1 << 9);
-        s1 = (s1 << 13) | (s1 >> 19);
-        state = (static_cast<uint64_t>(s1) << 32) | s0;
-        return static_cast<double>(r >> 8) * (1.0 / 16777216.0);
+        uint64_t old = state;
+        state = old * 6364136223846793005ull + 1442695040888963407ull;
+        uint32_t xs = static_cast<uint32_t>(((old >> 18u) ^ old) >> 27u);
+        uint32_t rot = static_cast<uint32_t>(old >> 59u);
+        uint32_t x = (xs >> rot) | (xs << ((32u - rot) & 31u));
+        return static_cast<double>(x >> 8) * (1.0 / 16777216.0);
     }
     double d() { return pcg ? pcg_uniform() : mt_canonical(); }
     double d(double lo, double hi) { return lo + (hi - lo) * d(); }              // tracer_utils.h:33-36
@@ -160,9 +157,8 @@ uint64_t splitmix64(uint64_t x) {
     x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
     return x ^ (x >> 31);
 }
-uint64_t pcg_seed(uint64_t seed, uint32_t pixel, uint32_t sample) {  // csrc/device.h path_seed
-    const uint64_t z = splitmix64(((static_cast<uint64_t>(pixel) << 32) | sample) ^ splitmix64(seed));
-    return z ? z : 0x9E3779B97F4A7C15ull;
+uint64_t pcg_seed(uint64_t seed, uint32_t pixel, uint32_t sample) {
+    return splitmix64(((static_cast<uint64_t>(pixel) << 32) | sample) ^ splitmix64(seed));
 }
 
 // ------------------------------------------------------------------------------------------------ scene graph
