@@ -164,6 +164,19 @@ constexpr uint64_t kMaxPassSlots = 1ull << 31;       // slot ids and batch offse
 // + 2 batches per material kernel: the kNumMatTypes shade launches of one depth all append to the same next-queue shards
 __host__ __device__ inline uint32_t shard_cap(uint32_t P) { return 64u * ((((P + 63u) / 64u) + kShards - 1) / kShards + 2 * kNumMatTypes); }
 
+// n / d for a divisor fixed per launch, as a multiply-high, an add and a shift (Granlund & Montgomery 1994,
+// round-up variant): l = ceil(log2 d), m = floor(2^32 (2^l - d) / d) + 1, n / d = (mulhi(m, n) + n) >> l, exact for
+// every n < 2^31 (the add cannot carry out) -- instead of the ~20-instruction integer division sequence.
+struct FastDiv {
+    uint32_t d, m, l;
+    static FastDiv make(uint32_t d) {
+        uint32_t l = 0;
+        while (l < 32 && (1ull << l) < d) ++l;
+        return FastDiv{d, static_cast<uint32_t>(((1ull << 32) * ((1ull << l) - d)) / d + 1), l};
+    }
+    __device__ __forceinline__ uint32_t div(uint32_t n) const { return (__umulhi(m, n) + n) >> l; }
+};
+
 struct PassGeom {
     int32_t W, H;               // full image
     int32_t rows;               // local rows
@@ -177,6 +190,8 @@ struct PassGeom {
     uint32_t stack;             // LDS traversal stack rows per lane (stack_rows)
     int32_t max_depth;
     uint64_t seed;
+    uint64_t seed_mix;          // splitmix64(seed): the per-frame half of pcg_seed, hoisted to the host
+    FastDiv fd_npix, fd_tiles_x, fd_band_rows, fd_w;  // / npix_pad, / tiles_x, / band_rows, / W
     double inv_w1, inv_h1;      // RN(1 / (W - 1)), RN(1 / (H - 1)) for gen_ray's div_rcp (rt_render rejects W or H < 2)
     const uint32_t* list;       // pixel-list mode (engine_mode::adaptive levels): slot pixel = list[qi] (local ly*W+lx)
     uint32_t nlist;             //   for qi < nlist; nullptr = every local pixel in 8x8 tile order
@@ -198,19 +213,21 @@ __host__ __device__ __forceinline__ uint32_t* counter(const Work<R>& w, int d, i
 }
 
 __device__ __forceinline__ int global_row(const PassGeom& g, int ly) {  // row-interleaved band partition
-    return (ly / g.band_rows) * (g.band_rows * g.band_count) + g.band_index * g.band_rows + (ly % g.band_rows);
+    const uint32_t b = g.fd_band_rows.div(static_cast<uint32_t>(ly));
+    return static_cast<int>(b) * (g.band_rows * g.band_count) + g.band_index * g.band_rows + (ly - static_cast<int>(b) * g.band_rows);
 }
 __device__ __forceinline__ bool slot_pixel(const PassGeom& g, uint32_t qi, int& lx, int& ly) {
     if (g.list) {
         if (qi >= g.nlist) return false;
         const uint32_t p = g.list[qi];
-        ly = static_cast<int>(p / static_cast<uint32_t>(g.W));
+        ly = static_cast<int>(g.fd_w.div(p));
         lx = static_cast<int>(p - static_cast<uint32_t>(ly) * static_cast<uint32_t>(g.W));
         return true;
     }
     const uint32_t tile = qi >> 6, within = qi & 63u;
-    lx = static_cast<int>((tile % g.tiles_x) * 8 + (within & 7u));
-    ly = static_cast<int>((tile / g.tiles_x) * 8 + (within >> 3));
+    const uint32_t ty = g.fd_tiles_x.div(tile);
+    lx = static_cast<int>((tile - ty * g.tiles_x) * 8 + (within & 7u));
+    ly = static_cast<int>(ty * 8 + (within >> 3));
     return lx < g.W && ly < g.rows;
 }
 
@@ -290,10 +307,10 @@ __device__ __forceinline__ int find_segment(const uint32_t* pre, int n, uint32_t
 // Runs inside the depth-0 extend: the camera ray never round-trips through HBM.
 template <class R>
 __device__ __forceinline__ void gen_ray(const PassGeom& g, const CameraRec<R>& cam, uint32_t q, int lx, int ly, PathState<R>& st) {
-    const uint32_t j = q / g.npix_pad;
+    const uint32_t j = g.fd_npix.div(q);
     const int gy = global_row(g, ly);
     const uint32_t pixel = static_cast<uint32_t>(gy) * static_cast<uint32_t>(g.W) + static_cast<uint32_t>(lx);
-    uint64_t rng = pcg_seed(g.seed, pixel, g.sample_base + j);
+    uint64_t rng = splitmix64(((static_cast<uint64_t>(pixel) << 32) | (g.sample_base + j)) ^ g.seed_mix);  // == pcg_seed(g.seed, ...)
     const R ru = uniform<R>(rng);
     const R rv = uniform<R>(rng);
     const R s = div_rcp(R(lx) + ru, R(g.W - 1), static_cast<R>(g.inv_w1));  // == (lx + ru) / (W - 1), same bits
@@ -520,7 +537,7 @@ __global__ __launch_bounds__(L ? kBlockL : kBlock, L ? 1 : ART_EXTEND_MIN_WAVES)
             if (d == 0) {
                 q = i;
                 int lx, ly;
-                live = slot_pixel(g, i % g.npix_pad, lx, ly);
+                live = slot_pixel(g, i - g.fd_npix.div(i) * g.npix_pad, lx, ly);
                 if (live) gen_ray(g, cam, q, lx, ly, st);
             } else {
                 const int s = find_segment(pre, kShards, i);
@@ -660,7 +677,7 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S, PassGe
                     // compiler barrier: the LDS camera/geometry loads stay here instead of being hoisted out of
                     // the loop into ~40 long-lived registers
                     __asm__ volatile("" ::: "memory");
-                    if (slot_pixel(s_g, slot % g.npix_pad, lx, ly)) {
+                    if (slot_pixel(s_g, slot - s_g.fd_npix.div(slot) * s_g.npix_pad, lx, ly)) {
                         gen_ray(s_g, s_cam, q, lx, ly, st);
                         busy = true;
                         depth = 0;
@@ -1306,6 +1323,11 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     g.npix_pad = g.tiles_x * tiles_y * 64u;
     g.max_depth = p.max_depth;
     g.seed = p.seed;
+    g.seed_mix = splitmix64(p.seed);
+    g.fd_tiles_x = FastDiv::make(g.tiles_x);
+    g.fd_band_rows = FastDiv::make(static_cast<uint32_t>(p.band_rows));
+    g.fd_w = FastDiv::make(static_cast<uint32_t>(p.width));
+    g.fd_npix = FastDiv::make(g.npix_pad);
     g.inv_w1 = 1.0 / static_cast<double>(p.width - 1);
     g.inv_h1 = 1.0 / static_cast<double>(p.height - 1);
     g.stack = stack_rows(ds.max_stack);
@@ -1402,6 +1424,7 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
         if (list) {
             npix = nlist;
             g.npix_pad = (nlist + 63u) & ~63u;
+            g.fd_npix = FastDiv::make(g.npix_pad);
             kk = std::max<uint32_t>(1, std::min<uint32_t>(static_cast<uint32_t>(p.spp), Pmax / std::max<uint32_t>(g.npix_pad, 64u)));
         }
         HIP_OK(hipMemsetAsync(w.acc, 0, sizeof(double) * 3 * npix, stream));
