@@ -68,3 +68,22 @@ def test_reflectance_branch_is_unchanged_by_one_ulp():
         u = rng.randrange(1 << 24) * 2.0**-24
         flips += (p1 > u) != (p2 > u)
     assert flips == 0
+
+
+def fastdiv_make(d: int):  # csrc/kernels.hip FastDiv::make
+    l = 0
+    while l < 32 and (1 << l) < d:
+        l += 1
+    return ((1 << 32) * ((1 << l) - d)) // d + 1, l
+
+
+def test_fastdiv_equals_integer_division():
+    rng = random.Random(9)
+    divisors = [1, 2, 3, 7, 8, 16, 64, 135, 240, 1920, 32400, 2073600, (1 << 31) - 1, 1 << 31]
+    divisors += [rng.randint(1, 1 << 31) for _ in range(200)]
+    for d in divisors:
+        m, l = fastdiv_make(d)
+        assert 0 < m < (1 << 32)
+        for n in [0, 1, d - 1, d, d + 1, (1 << 31) - 1] + [rng.randrange(1 << 31) for _ in range(500)]:
+            if 0 <= n < (1 << 31):
+                assert (((m * n) >> 32) + n) >> l == n // d, (d, n)
