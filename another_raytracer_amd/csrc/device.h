@@ -875,17 +875,18 @@ __device__ __forceinline__ V3<R> image_value(const DevScene<R>& S, int32_t im, R
 // is evaluated as a sign parity: sin(y) == 0 exactly iff y == 0 for doubles (pi is irrational), and for y != 0
 // sin(y) < 0 iff floor(y / pi) is odd.  Same predicate as the reference's, without the Payne-Hanek reduction of a
 // full f64 sin (46 VGPRs in the shade kernel); it can only differ when y is within ~1 ulp of a multiple of pi.
+// sin(y) < 0 as a bool (y != 0): floor(y / pi) odd, the parity read in floating point (k / 2 == floor(k / 2) for even
+// k; every double >= 2^53 is even, as its integer conversion would say) -- no f64 -> int64 conversion sequence.
 template <class R>
-__device__ __forceinline__ int sin_sign(R y) {
-    if (y == R(0)) return 0;
+__device__ __forceinline__ bool sin_negative(R y) {
     const R k = floor(y * R(0.31830988618379067154));
-    const long long ki = static_cast<long long>(k);
-    return (ki & 1) ? -1 : 1;
+    return R(0.5) * k != floor(R(0.5) * k);
 }
 template <class R>
-__device__ __forceinline__ bool checker_odd(V3<R> p) {
-    const int a = sin_sign(R(10) * p.x), b = sin_sign(R(10) * p.y), c = sin_sign(R(10) * p.z);
-    return a * b * c < 0;
+__device__ __forceinline__ bool checker_odd(V3<R> p) {  // sin(10x) * sin(10y) * sin(10z) < 0
+    const R x = R(10) * p.x, y = R(10) * p.y, z = R(10) * p.z;
+    const bool nonzero = x != R(0) && y != R(0) && z != R(0);
+    return nonzero && (sin_negative(x) != (sin_negative(y) != sin_negative(z)));
 }
 
 // rendering/texture.h.  TF (layout.h TexFeature bits) prunes the texture kinds a scene cannot contain.
