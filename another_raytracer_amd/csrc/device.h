@@ -97,6 +97,93 @@ __device__ __forceinline__ V3<R> in_unit_sphere(uint64_t& s) {  // vec3.h:117-12
     }
 }
 
+// PCG32 jump-ahead (Brown 1994, "Random number generation with arbitrary strides"): n steps of s -> A s + C are one
+// affine map s -> A_n s + C_n (mod 2^64).  kJumpEntries maps of n = 3 j draws (one random_in_unit_sphere candidate per
+// j) let a lane compute the state at another lane's j-th candidate directly.
+constexpr int kJumpEntries = 64;  // j = 0..63
+struct JumpEntry {
+    uint64_t a, c;
+};
+__host__ __device__ inline JumpEntry pcg_jump(uint32_t steps) {
+    uint64_t a = 1, c = 0;
+    for (uint32_t i = 0; i < steps; ++i) {
+        a = a * 6364136223846793005ull;
+        c = c * 6364136223846793005ull + 1442695040888963407ull;
+    }
+    return JumpEntry{a, c};
+}
+
+// random_in_unit_sphere (vec3.h:117-123) for every lane with `need`, the wave cooperating on the rejection loop.  A
+// lane's result is the first candidate of its own stream inside the unit ball, and its stream ends right after that
+// candidate -- exactly the serial loop's draws -- but the search runs in rounds: round 0 tests every lane's next
+// candidate in place; in each later round the R lanes still searching share the 64 lanes, K = 64 / R consecutive
+// candidates each (a helper lane jumps the owner's state ahead by 3 j draws and tests candidate j), and the owner
+// takes the first accepted one.  A wave needs ~2 rounds instead of the ~6 serial iterations of its unluckiest lane.
+// Must be called by the whole wave (the helpers are every lane, active or not in the path loop).  jt: the jump table
+// in LDS (kJumpEntries JumpEntry).
+template <class R>
+__device__ __forceinline__ V3<R> coop_unit_sphere(bool need, uint64_t& rng, const JumpEntry* jt) {
+    const uint32_t lane = __lane_id();
+    V3<R> p = mk(R(0), R(0), R(0));
+    uint64_t s = rng;  // pending lanes: the state at the next untested candidate
+    bool pending = false;
+    if (need) {
+        p.x = uniform_pm1<R>(s);
+        p.y = uniform_pm1<R>(s);
+        p.z = uniform_pm1<R>(s);
+        if (len2(p) >= R(1)) pending = true;
+        else rng = s;
+    }
+    uint64_t mask = __ballot(pending);
+    while (mask) {
+        const uint32_t nr = static_cast<uint32_t>(__popcll(mask));
+        const uint32_t k = 64u / nr;  // candidates per searching lane this round
+        const uint32_t rank = static_cast<uint32_t>(__popcll(mask & ((1ull << lane) - 1ull)));
+        // owner of rank r -> lane r holds the owner's lane id (push), then helper w reads it from lane w / k
+        // (lanes that own nothing push to lane 63, which is read only when all 64 lanes search and then it is
+        // pushed by its owner alone)
+        const int owner_at_rank = __builtin_amdgcn_ds_permute(static_cast<int>(pending ? rank : 63u) * 4, static_cast<int>(lane));
+        // o = floor(lane / k): (lane + 1/2) / k is >= 1/(2k) >= 2^-7 away from an integer, far above the error of a
+        // 1-ulp reciprocal
+        const uint32_t o = static_cast<uint32_t>((static_cast<float>(lane) + 0.5f) * __builtin_amdgcn_rcpf(static_cast<float>(k)));
+        const uint32_t j = lane - o * k;
+        const bool helper = o < nr;
+        const int owner_lane = __builtin_amdgcn_ds_bpermute(static_cast<int>(helper ? o : 0u) * 4, owner_at_rank);
+        const uint32_t slo = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(owner_lane * 4, static_cast<int>(static_cast<uint32_t>(s))));
+        const uint32_t shi = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(owner_lane * 4, static_cast<int>(static_cast<uint32_t>(s >> 32))));
+        const JumpEntry e = jt[j];
+        uint64_t hs = e.a * ((static_cast<uint64_t>(shi) << 32) | slo) + e.c;
+        V3<R> c;
+        c.x = uniform_pm1<R>(hs);
+        c.y = uniform_pm1<R>(hs);
+        c.z = uniform_pm1<R>(hs);
+        const uint64_t acc = __ballot(helper && len2(c) < R(1));
+        // owners: the first accepted candidate of their k; its helper's state (hs) is the state right after it.
+        // With none accepted, the state after the last helper's candidate is where the next round starts.
+        const uint64_t mine = k == 64u ? acc : (acc >> (rank * k)) & ((1ull << k) - 1ull);
+        const uint32_t jstar = mine ? static_cast<uint32_t>(__ffsll(static_cast<long long>(mine)) - 1) : k - 1u;
+        const int src = static_cast<int>(pending ? rank * k + jstar : lane) * 4;
+        const uint32_t nlo = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(static_cast<uint32_t>(hs))));
+        const uint32_t nhi = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(static_cast<uint32_t>(hs >> 32))));
+        V3<R> got;
+        got.x = __hiloint2double(__builtin_amdgcn_ds_bpermute(src, __double2hiint(c.x)), __builtin_amdgcn_ds_bpermute(src, __double2loint(c.x)));
+        got.y = __hiloint2double(__builtin_amdgcn_ds_bpermute(src, __double2hiint(c.y)), __builtin_amdgcn_ds_bpermute(src, __double2loint(c.y)));
+        got.z = __hiloint2double(__builtin_amdgcn_ds_bpermute(src, __double2hiint(c.z)), __builtin_amdgcn_ds_bpermute(src, __double2loint(c.z)));
+        if (pending) {
+            const uint64_t next = (static_cast<uint64_t>(nhi) << 32) | nlo;
+            if (mine) {
+                p = got;
+                rng = next;
+                pending = false;
+            } else {
+                s = next;
+            }
+        }
+        mask = __ballot(pending);
+    }
+    return p;
+}
+
 // ------------------------------------------------------------------------------------------------ device scene view
 template <class R>
 struct DevScene {

@@ -382,7 +382,9 @@ __device__ __forceinline__ V3<double> lds_mat_color(const uint8_t* lds, uint32_t
     const double2 a = m[0], b = m[1];
     return mk(a.x, a.y, b.x);
 }
-__device__ __forceinline__ bool shade_hit_lds(const uint8_t* lds, uint32_t slot, uint32_t mtype, double t, bool last, PathState<double>& st) {
+// pre_ps: the lane's random_in_unit_sphere() draw, already taken by the wave (coop_unit_sphere) when non-null.
+__device__ __forceinline__ bool shade_hit_lds(const uint8_t* lds, uint32_t slot, uint32_t mtype, double t, bool last, PathState<double>& st,
+                                              const V3<double>* pre_ps = nullptr) {
     using R = double;
     const double2* sp = reinterpret_cast<const double2*>(lds + kLdsOffSph) + slot;
     const double2 a = sp[0], b = sp[kLdsSlotCap];
@@ -412,7 +414,8 @@ __device__ __forceinline__ bool shade_hit_lds(const uint8_t* lds, uint32_t slot,
     // sqrt + divide sequence instead of one per material present.
     const bool lamb = mtype == MAT_LAMBERTIAN;
     V3<R> ps = mk(R(0), R(0), R(0));
-    if (mtype != MAT_DIELECTRIC) ps = in_unit_sphere<R>(st.rng);
+    if (pre_ps) ps = *pre_ps;
+    else if (mtype != MAT_DIELECTRIC) ps = in_unit_sphere<R>(st.rng);
     const V3<R> u = unit(lamb ? ps : st.ray.d);
     V3<R> att, dir;
     if (lamb) {  // material.h:20-43
@@ -618,8 +621,9 @@ __global__ __launch_bounds__(L ? kBlockL : kBlock, L ? 1 : ART_EXTEND_MIN_WAVES)
 // k_extend, so images are bit-identical to the wavefront variants.
 constexpr uint32_t kPathChunk = 256;
 __host__ __device__ constexpr size_t paths_stack_bytes(uint32_t stack) { return (sizeof(int16_t) * stack * kBlockL + 15u) & ~size_t(15); }
+constexpr size_t kJumpBytes = sizeof(JumpEntry) * kJumpEntries;
 __host__ __device__ constexpr size_t paths_lds_bytes(uint32_t stack) {
-    return kLdsImageBytes + paths_stack_bytes(stack) + sizeof(CameraRec<double>) + sizeof(PassGeom);
+    return kLdsImageBytes + paths_stack_bytes(stack) + kJumpBytes + sizeof(CameraRec<double>) + sizeof(PassGeom);
 }
 __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S, PassGeom g, CameraRec<double> cam, Work<double> w, uint32_t* next_slot) {
     using R = double;
@@ -631,10 +635,12 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S, PassGe
     extern __shared__ __align__(16) uint8_t smem[];
     const uint8_t* lds = smem;
     StackT<true>* stk = reinterpret_cast<StackT<true>*>(smem + kLdsImageBytes) + B + threadIdx.x;
-    CameraRec<double>& s_cam = *reinterpret_cast<CameraRec<double>*>(smem + kLdsImageBytes + paths_stack_bytes(g.stack));
-    PassGeom& s_g = *reinterpret_cast<PassGeom*>(smem + kLdsImageBytes + paths_stack_bytes(g.stack) + sizeof(CameraRec<double>));
+    JumpEntry* jt = reinterpret_cast<JumpEntry*>(smem + kLdsImageBytes + paths_stack_bytes(g.stack));
+    CameraRec<double>& s_cam = *reinterpret_cast<CameraRec<double>*>(smem + kLdsImageBytes + paths_stack_bytes(g.stack) + kJumpBytes);
+    PassGeom& s_g = *reinterpret_cast<PassGeom*>(smem + kLdsImageBytes + paths_stack_bytes(g.stack) + kJumpBytes + sizeof(CameraRec<double>));
     stk[-B] = static_cast<StackT<true>>(kNodeEmpty);
     load_lds_image<B>(S.lds_image, smem);
+    if (threadIdx.x < static_cast<uint32_t>(kJumpEntries)) jt[threadIdx.x] = pcg_jump(3u * threadIdx.x);
     if (threadIdx.x == 0) {
         s_cam = cam;
         s_g = g;
@@ -689,14 +695,21 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S, PassGe
             if (__ballot(!drained) == 0) break;
             continue;
         }
+        R t = R(0);
+        HitOut h{0, 0, kMatUnknown};
+        bool hitw = false;
         if (busy) {
-            R t;
-            HitOut h{0, 0, kMatUnknown};
             ++segs;
+            hitw = trace_world<R, kFeatSpheres, B, true>(S, lds, st.ray, stk, st.rng, t, h);
+        }
+        // the whole wave draws random_in_unit_sphere for its lambertian and metal hits (material.h:33, :55), which
+        // scatter with it first; lights and the max_depth bounce draw nothing
+        const bool need = busy && hitw && (h.mt == MAT_LAMBERTIAN || h.mt == MAT_METAL) && depth + 1 < g.max_depth;
+        const V3<R> ps = coop_unit_sphere<R>(need, st.rng, jt);
+        if (busy) {
             bool cont = false;
-            const bool hitw = trace_world<R, kFeatSpheres, B, true>(S, lds, st.ray, stk, st.rng, t, h);
             if (hitw) {
-                cont = shade_hit_lds(lds, h.obj >> 16, h.mt, t, depth + 1 >= g.max_depth, st);
+                cont = shade_hit_lds(lds, h.obj >> 16, h.mt, t, depth + 1 >= g.max_depth, st, &ps);
             } else {  // engine.h:455-456: miss -> background
                 st.L = st.L + st.T * bg;
             }
