@@ -87,3 +87,26 @@ def test_fastdiv_equals_integer_division():
         for n in [0, 1, d - 1, d, d + 1, (1 << 31) - 1] + [rng.randrange(1 << 31) for _ in range(500)]:
             if 0 <= n < (1 << 31):
                 assert (((m * n) >> 32) + n) >> l == n // d, (d, n)
+
+
+PCG_A, PCG_C, M64 = 6364136223846793005, 1442695040888963407, (1 << 64) - 1
+
+
+def pcg_jump(steps: int):  # csrc/device.h pcg_jump: s -> a s + c after `steps` LCG steps
+    a, c = 1, 0
+    for _ in range(steps):
+        a, c = (a * PCG_A) & M64, (c * PCG_A + PCG_C) & M64
+    return a, c
+
+
+def test_pcg_jump_table_matches_stepping():
+    """coop_unit_sphere's helpers jump a stream ahead by 3 j draws; the affine map must equal 3 j LCG steps."""
+    rng = random.Random(10)
+    for _ in range(20):
+        s0 = rng.getrandbits(64)
+        s = s0
+        for j in range(64):
+            a, c = pcg_jump(3 * j)
+            assert (a * s0 + c) & M64 == s, j
+            for _ in range(3):
+                s = (s * PCG_A + PCG_C) & M64
