@@ -725,6 +725,107 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S, PassGe
     if (lane == 0) atomicAdd(w.segments, segs);
 }
 
+// Persistent paths over the HBM scene (EXT_MEGA_G): the k_paths loop for every scene that does not fit the LDS
+// image (triangles, rects, boxes, transforms, media, noise/image textures).  A lane owns one path from its camera
+// ray to its end: trace_world over the global BVHs (the k_extend traversal, LDS stack) and, in place, world_surface +
+// the material's scatter (the k_shade arithmetic, one switch over the material type instead of one launch per type),
+// so the RNG draws and every f64 operation are those of the wavefront kernels and images are bit-identical to them.
+// F / TF: the scene's primitive and texture features (smallest instantiation that covers them).
+template <uint32_t F, uint32_t TF>
+__global__ __launch_bounds__(kBlock) void k_paths_g(DevScene<double> S, PassGeom g, CameraRec<double> cam, Work<double> w, uint32_t* next_slot) {
+    using R = double;
+    constexpr int B = kBlock;
+    extern __shared__ __align__(16) uint8_t smem[];  // traversal stack: g.stack entries x B lanes (+ sentinel row)
+    StackT<false>* stk = reinterpret_cast<StackT<false>*>(smem) + B + threadIdx.x;
+    stk[-B] = static_cast<StackT<false>>(kNodeEmpty);
+    const uint32_t lane = __lane_id();
+    const uint64_t below = (1ull << lane) - 1ull;
+    const V3<R> bg = mk(S.bg[0], S.bg[1], S.bg[2]);
+    uint32_t cur = 0, end = 0;  // this wave's claimed slots [cur, end): wave-uniform
+    bool busy = false, drained = false;
+    uint32_t q = 0;
+    int depth = 0;
+    PathState<R> st;
+    unsigned long long segs = 0;
+    for (;;) {
+        const uint64_t idle = __ballot(!busy && !drained);
+        if (idle) {
+            const uint32_t n = static_cast<uint32_t>(__popcll(idle));
+            const uint32_t rank = static_cast<uint32_t>(__popcll(idle & below));
+            uint32_t slot;
+            if (cur + n > end) {
+                uint32_t nb = 0;
+                if (lane == 0) nb = atomicAdd(next_slot, kPathChunk);
+                nb = __shfl(nb, 0);
+                const uint32_t left = end - cur;
+                slot = rank < left ? cur + rank : nb + (rank - left);
+                cur = nb + (n - left);
+                end = nb + kPathChunk;
+            } else {
+                slot = cur + rank;
+                cur += n;
+            }
+            if (!busy && !drained) {
+                if (slot >= g.P) {
+                    drained = true;
+                } else {
+                    int lx, ly;
+                    q = slot;
+                    if (slot_pixel(g, slot - g.fd_npix.div(slot) * g.npix_pad, lx, ly)) {
+                        gen_ray(g, cam, q, lx, ly, st);
+                        busy = true;
+                        depth = 0;
+                    }
+                }
+            }
+        }
+        if (__ballot(busy) == 0) {
+            if (__ballot(!drained) == 0) break;
+            continue;
+        }
+        if (busy) {
+            R t;
+            HitOut h{0, 0, kMatUnknown};
+            ++segs;
+            bool cont = false;
+            if (trace_world<R, F, B, false>(S, nullptr, st.ray, stk, st.rng, t, h)) {
+                Surf<R> s;
+                world_surface<R, F, (TF & TF_IMAGE) != 0>(S, h, st.ray, t, s);
+                const MatRec<R>& mat = S.mats[s.mat];
+                if (mat.type == MAT_LIGHT) {  // material.h:114-116; diffuse_light never scatters
+                    st.L = st.L + st.T * tex_value<R, TF>(S, mat.tex, s.u, s.v, s.p);
+                } else if (depth + 1 < g.max_depth) {
+                    V3<R> att, dir;
+                    bool sc = false;
+                    switch (mat.type) {
+                        case MAT_LAMBERTIAN: sc = scatter<R, MAT_LAMBERTIAN, TF>(S, mat, s, st, att, dir); break;
+                        case MAT_METAL: sc = scatter<R, MAT_METAL, TF>(S, mat, s, st, att, dir); break;
+                        case MAT_DIELECTRIC: sc = scatter<R, MAT_DIELECTRIC, TF>(S, mat, s, st, att, dir); break;
+                        case MAT_ISOTROPIC: sc = scatter<R, MAT_ISOTROPIC, TF>(S, mat, s, st, att, dir); break;
+                        default: break;
+                    }
+                    if (sc) {
+                        st.T = st.T * att;
+                        st.ray.o = s.p;
+                        st.ray.d = dir;
+                        cont = true;
+                    }
+                }
+            } else {  // engine.h:455-456: miss -> background
+                st.L = st.L + st.T * bg;
+            }
+            if (cont) {
+                ++depth;
+            } else {
+                store_res(w.res, q, st.L);
+                busy = false;
+            }
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) segs += __shfl_xor(segs, off);
+    if (lane == 0) atomicAdd(w.segments, segs);
+}
+
 // Input: the kShards shards of material queue M at depth d (the extend stage sorted hits by material type).
 template <class R, uint32_t F, uint32_t M, uint32_t TF>
 __global__ __launch_bounds__(kBlock) void k_shade(DevScene<R> S, PassGeom g, Work<R> w, int d) {
@@ -1253,7 +1354,8 @@ static void launch_extend(int num_cu, hipStream_t st, const DevScene<R>& S, cons
 }
 // Extend variant: 0 = HBM scene, 1 = LDS scene, 2 = LDS scene with fused shading (no k_shade launches), 3 = persistent
 // paths (k_paths: the fused LDS bounce loop in registers, one launch per pass).
-enum ExtendVariant { EXT_GLOBAL = 0, EXT_LDS = 1, EXT_FUSED = 2, EXT_MEGA = 3 };
+// 4 = persistent paths over the HBM scene (k_paths_g: every other scene, f64).
+enum ExtendVariant { EXT_GLOBAL = 0, EXT_LDS = 1, EXT_FUSED = 2, EXT_MEGA = 3, EXT_MEGA_G = 4 };
 // One bounce (extend + one shade launch per material type present, unless fused) of the smallest kernel
 // instantiation that covers the scene's features.
 template <class R, uint32_t F>
@@ -1281,9 +1383,36 @@ static void launch_bounce(uint32_t mat_types, bool tex_basic, int variant, int n
 // kernels).
 template <class R>
 static int extend_variant(const DeviceScene<R>& ds, int flags) {
-    if (!ds.lds_scene || (flags & RT_GLOBAL_SCENE) || (ds.features & ~kFeatSpheres) != 0) return EXT_GLOBAL;
+    if (!ds.lds_scene || (flags & RT_GLOBAL_SCENE) || (ds.features & ~kFeatSpheres) != 0)
+        return (std::is_same<R, double>::value && !(flags & RT_WAVEFRONT)) ? EXT_MEGA_G : EXT_GLOBAL;
     if (!ds.lds_shade || (flags & RT_SPLIT_SHADE)) return EXT_LDS;
     return (flags & RT_WAVEFRONT) ? EXT_FUSED : EXT_MEGA;
+}
+template <uint32_t F, uint32_t TF>
+static void launch_paths_g_ft(int num_cu, hipStream_t st, const DevScene<double>& S, const PassGeom& g, const CameraRec<double>& cam,
+                              const Work<double>& w, uint32_t* next_slot) {
+    const size_t lds = sizeof(int32_t) * g.stack * kBlock;  // stack_rows: sentinel + entries + spare row
+    static int blocks = 0;
+    static size_t blocks_lds = ~size_t(0);
+    if (lds != blocks_lds) {  // a persistent grid: exactly the blocks the CUs hold at once
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_paths_g<F, TF>, kBlock, lds) != hipSuccess || per_cu < 1) per_cu = 1;
+        blocks = per_cu * num_cu;
+        blocks_lds = lds;
+    }
+    hipLaunchKernelGGL((k_paths_g<F, TF>), dim3(blocks), dim3(kBlock), lds, st, S, g, cam, w, next_slot);
+}
+static void launch_paths_g(uint32_t feat, bool tex_basic, int num_cu, hipStream_t st, const DevScene<double>& S, const PassGeom& g,
+                           const CameraRec<double>& cam, const Work<double>& w, uint32_t* next_slot) {
+    if ((feat & ~kFeatSpheres) == 0) {
+        if (tex_basic) launch_paths_g_ft<kFeatSpheres, kTexBasic>(num_cu, st, S, g, cam, w, next_slot);
+        else launch_paths_g_ft<kFeatSpheres, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
+    } else if ((feat & ~kFeatMesh) == 0) {
+        if (tex_basic) launch_paths_g_ft<kFeatMesh, kTexBasic>(num_cu, st, S, g, cam, w, next_slot);
+        else launch_paths_g_ft<kFeatMesh, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
+    } else {
+        launch_paths_g_ft<F_ALL, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
+    }
 }
 static void launch_paths(int num_cu, hipStream_t st, const DevScene<double>& S, const PassGeom& g, const CameraRec<double>& cam,
                          const Work<double>& w, uint32_t* next_slot) {
@@ -1345,7 +1474,7 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     g.inv_h1 = 1.0 / static_cast<double>(p.height - 1);
     g.stack = stack_rows(ds.max_stack);
     const int variant = extend_variant(ds, p.flags);
-    const bool mega = variant == EXT_MEGA;
+    const bool mega = variant == EXT_MEGA || variant == EXT_MEGA_G;
     // Samples per pass: as many path slots as half of the free HBM holds (plus the workspace this renderer already
     // owns).  Every pass pays max_depth bounces of fixed launch/tail cost whatever its size, so on a 288 GB part the
     // 1080p x 1024 spp frame runs in 3 passes instead of ~40 (5.6 -> 6.9 Gsamples/s measured); spread evenly.
@@ -1451,7 +1580,8 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
                 if (mega) {
                     if (p.max_depth > 0) {
                         if (prof) mark();
-                        launch_paths(I.num_cu, stream, ds.view, g, cam, w, counter(w, 0, 0, 0));
+                        if (variant == EXT_MEGA) launch_paths(I.num_cu, stream, ds.view, g, cam, w, counter(w, 0, 0, 0));
+                        else launch_paths_g(ds.features, ds.tex_basic, I.num_cu, stream, ds.view, g, cam, w, counter(w, 0, 0, 0));
                         if (prof) { mark(); mark(); }
                         ++ext_launches;
                     }

@@ -9,7 +9,7 @@ max-over-ranks wall time of the K timed steps.  A segment is one ray traced thro
 engine.h:453), counted exactly on the device from the wavefront queue sizes.
 
 Extra fields:
-  roofline      dominant kernel (k_paths, or k_extend for the per-depth variants): SURVEY.md §8(d) algorithmic bytes
+  roofline      dominant kernel (k_paths / k_paths_g, or k_extend for the per-depth variants): SURVEY.md §8(d) algorithmic bytes
                 (128 B per segment + 12 B per pixel + the flat scene once per launch) / summed launch time measured live
                 with HIP events on the render stream during the timed steps; HBM peak 8 TB/s.  moved_bytes_per_segment
                 is what the variant really moves by construction.
@@ -48,7 +48,7 @@ RES_BYTES = {"f32": 16, "f64": 32}
 
 def extend_moved_bytes(precision, variant, segments, primary):
     """Bytes the extend launches of the timed region move by construction (variant-specific)."""
-    if variant == 3:
+    if variant in (3, 4):  # persistent paths: the radiance record per path only
         return primary * RES_BYTES[precision]
     if variant == 2:
         rec = PATH_BYTES[precision]
@@ -215,7 +215,7 @@ def main():
             moved = extend_moved_bytes(args.precision, variant, segs, primary_segs)
             tr = latest_traffic(args.precision, args.scene, variant)
             line["roofline"] = {
-                "bound": "hbm", "kernel": "k_paths" if variant == 3 else "k_extend", "achieved": round(achieved, 2),
+                "bound": "hbm", "kernel": {3: "k_paths", 4: "k_paths_g"}.get(variant, "k_extend"), "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                 "traffic": (round(tr["extend_bytes_per_segment"] * segs / launches) if tr else None),
                 "algorithmic_bytes_per_launch": round(alg / launches),

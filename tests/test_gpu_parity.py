@@ -90,14 +90,16 @@ def test_band_partition_is_bit_identical(gpu, precision):
 @pytest.mark.parametrize("max_depth", [1, 3, 50])
 def test_extend_variants_are_bit_identical(gpu, max_depth):
     # the benchmark scene runs the persistent-path kernel (variant 3); it must reproduce the per-depth fused LDS kernel
-    # (2), the split-shade LDS kernel (1) and the HBM kernel (0) bit for bit, including the last-bounce cut-off
+    # (2), the split-shade LDS kernel (1), the persistent HBM-scene kernel (4) and the per-depth HBM kernels (0) bit
+    # for bit, including the last-bounce cut-off
     W, H, spp = 160, 90, 8
     mega = gpu_render("1", W, H, spp, "f64", max_depth=max_depth)
     fused = gpu_render("1", W, H, spp, "f64", wavefront=True, max_depth=max_depth)
     split = gpu_render("1", W, H, spp, "f64", split_shade=True, max_depth=max_depth)
     glb = gpu_render("1", W, H, spp, "f64", global_scene=True, max_depth=max_depth)
-    assert tuple(r["stats"]["extend_variant"] for r in (mega, fused, split, glb)) == (3, 2, 1, 0)
-    for other in (fused, split, glb):
+    glb_wf = gpu_render("1", W, H, spp, "f64", global_scene=True, wavefront=True, max_depth=max_depth)
+    assert tuple(r["stats"]["extend_variant"] for r in (mega, fused, split, glb, glb_wf)) == (3, 2, 1, 4, 0)
+    for other in (fused, split, glb, glb_wf):
         assert np.array_equal(mega["acc"], other["acc"])
         assert np.array_equal(mega["rgb"], other["rgb"])
         assert mega["segments"] == other["segments"]
@@ -113,8 +115,23 @@ def test_persistent_paths_pass_split_is_bit_identical(gpu):
 
 
 def test_general_scenes_use_the_hbm_kernels(gpu):
-    # triangles/rects/media (or no BVH) never take the LDS variants
-    assert gpu_render("cow", 32, 18, 2)["stats"]["extend_variant"] == 0
+    # triangles/rects/media (or no BVH) never take the LDS variants: persistent paths over the HBM scene (4), or the
+    # per-depth HBM kernels (0) with RT_WAVEFRONT
+    assert gpu_render("cow", 32, 18, 2)["stats"]["extend_variant"] == 4
+    assert gpu_render("cow", 32, 18, 2, wavefront=True)["stats"]["extend_variant"] == 0
+
+
+@pytest.mark.parametrize("scene", ["cow", "8", "5", "6", "7", "9", "c1"])
+@pytest.mark.parametrize("max_depth", [1, 50])
+def test_hbm_persistent_paths_match_wavefront(gpu, scene, max_depth):
+    # every feature (triangles, rects, boxes, transforms, media, noise/image textures, lights) through k_paths_g is bit
+    # for bit the per-depth wavefront render
+    W, H, spp = 48, 27, 4
+    a = gpu_render(scene, W, H, spp, "f64", max_depth=max_depth)
+    b = gpu_render(scene, W, H, spp, "f64", wavefront=True, max_depth=max_depth)
+    assert a["stats"]["extend_variant"] == 4 and b["stats"]["extend_variant"] == 0
+    assert np.array_equal(a["acc"], b["acc"]) and np.array_equal(a["rgb"], b["rgb"])
+    assert a["segments"] == b["segments"]
 
 
 def test_statistical_parity_with_reference_config0(gpu):
