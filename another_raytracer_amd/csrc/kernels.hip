@@ -731,8 +731,11 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S, PassGe
 // the material's scatter (the k_shade arithmetic, one switch over the material type instead of one launch per type),
 // so the RNG draws and every f64 operation are those of the wavefront kernels and images are bit-identical to them.
 // F / TF: the scene's primitive and texture features (smallest instantiation that covers them).
+#ifndef ART_PATHS_G_WAVES
+#define ART_PATHS_G_WAVES 3  // 3 waves per SIMD (<= 168 VGPRs): measured best over 2 and 4 (cow +22 %, final +18 %, dino +21 % over 2)
+#endif
 template <uint32_t F, uint32_t TF>
-__global__ __launch_bounds__(kBlock) void k_paths_g(DevScene<double> S, PassGeom g, CameraRec<double> cam, Work<double> w, uint32_t* next_slot) {
+__global__ __launch_bounds__(kBlock, ART_PATHS_G_WAVES) void k_paths_g(DevScene<double> S, PassGeom g, CameraRec<double> cam, Work<double> w, uint32_t* next_slot) {
     using R = double;
     constexpr int B = kBlock;
     extern __shared__ __align__(16) uint8_t smem[];  // traversal stack: g.stack entries x B lanes (+ sentinel row)
