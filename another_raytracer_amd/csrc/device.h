@@ -482,6 +482,7 @@ __device__ __forceinline__ void stat_lane(int k) { atomicAdd(&g_art_stats[k], 1u
 #ifndef ART_SPECULATIVE
 #define ART_SPECULATIVE 1
 #endif
+
 // The LDS scene image lives at LDS address 0 (k_extend and k_paths allocate LDS dynamically only), so node fetches
 // take a plain 32-bit LDS byte address: no base add per load.
 typedef float f4v __attribute__((ext_vector_type(4)));
@@ -634,9 +635,17 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
 #if ART_SPECULATIVE
         // leaf phase: the parked leaf, else the current node when it is a leaf (a lane that left the node loop on the
         // wave-wide break still has an inner node to return to)
+        // L: a lane that left the node loop holding a second leaf (parked + current) tests both in this phase, one
+        // leaf phase instead of two (the wave's leaf loop runs over the longer sum, once)
         int32_t leaf = parked;
+        int32_t leaf2 = kNodeEmpty;
         if (leaf != kNodeEmpty) {
             parked = kNodeEmpty;
+            if (L && node < kNodeEmpty) {
+                leaf2 = node;
+                node = st.peek();
+                st.pop_if(true);
+            }
         } else {
             if (node == kNodeEmpty) break;
             leaf = node;
@@ -650,23 +659,43 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
         st.pop_if(true);
 #endif
         uint32_t first, cnt;
+#if ART_SPECULATIVE
+        uint32_t first2 = 0, cnt12 = 0;
+#endif
         if constexpr (L) {
             const uint32_t x = ~static_cast<uint32_t>(leaf);
             first = x & ((1u << kLdsLeafShift) - 1);
             cnt = x >> kLdsLeafShift;
+#if ART_SPECULATIVE
+            const uint32_t x2 = leaf2 == kNodeEmpty ? 0u : ~static_cast<uint32_t>(leaf2);
+            first2 = (x2 & ((1u << kLdsLeafShift) - 1)) - cnt;  // slot of entry k >= cnt: first2 + k
+            cnt12 = cnt + (x2 >> kLdsLeafShift);
+#endif
         } else {
             first = leaf_first(leaf);
             cnt = leaf_count(leaf);
+#if ART_SPECULATIVE
+            cnt12 = cnt;
+#endif
         }
+#if ART_SPECULATIVE
+        for (uint32_t k = 0; k < cnt12; ++k) {
+#else
         for (uint32_t k = 0; k < cnt; ++k) {
+#endif
             ART_STAT_WAVE(2);
             ART_STAT_LANE(3);
             R tt;
             uint32_t fc = 0, ref, m = kMatUnknown;
             bool h;
             if constexpr (L) {
-                h = hit_lds_slot(lds, first + k, r, d_a, d_inv_a, tmin, tmax, tt, ref, m);
-                fc = first + k;  // the leaf slot travels in the face field (spheres have no face): LDS shading reads it
+#if ART_SPECULATIVE
+                const uint32_t slot = (k < cnt ? first : first2) + k;
+#else
+                const uint32_t slot = first + k;
+#endif
+                h = hit_lds_slot(lds, slot, r, d_a, d_inv_a, tmin, tmax, tt, ref, m);
+                fc = slot;  // the leaf slot travels in the face field (spheres have no face): LDS shading reads it
             } else {
                 ref = S.primrefs[first + k];
                 h = hit_prim<R, F>(S, ref, r, tmin, tmax, tt, fc);
