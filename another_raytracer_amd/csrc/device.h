@@ -219,6 +219,23 @@ __device__ __forceinline__ R div_rcp(R x, R a, R inv_a) {
     return fma(fma(-q, a, x), inv_a, q);
 }
 
+// std::sqrt of sphere.h:44 (correctly rounded).  For x >= 2^-767 this is the compiler's own f64 sqrt expansion
+// (hardware rsq, then two Goldschmidt / two Newton fma steps) without its denormal-range scaling and its zero/inf
+// select, which never apply there: the same operations on the same values, so the same bits.  Smaller x (and 0),
+// inf and NaN take the compiler's full sequence.  Saves 7 VALU per root, the leaf test's second-largest block after the
+// discriminant.
+__device__ __forceinline__ double sqrt_rn(double x) {
+    if (!(x >= 0x1p-767 && x < __builtin_inf())) return sqrt(x);
+    const double y = __builtin_amdgcn_rsq(x);
+    double s = x * y, h = y * 0.5;
+    const double r = fma(-h, s, 0.5);
+    s = fma(s, r, s);
+    h = fma(h, r, h);
+    s = fma(fma(-s, s, x), h, s);
+    return fma(fma(-s, s, x), h, s);
+}
+__device__ __forceinline__ float sqrt_rn(float x) { return sqrtf(x); }
+
 // sphere.h:39-65 / moving_sphere.h:41-58 (root selection only; the surface is rebuilt in shade).  a = |d|^2 of the
 // ray; RCP: the two root divisions by a use div_rcp with inv_a = 1 / a (same bits).
 template <class R, bool RCP>
@@ -228,7 +245,7 @@ __device__ __forceinline__ bool sphere_root(V3<R> center, R r2, const Ray<R>& r,
     const R c = len2(oc) - r2;
     const R disc = half_b * half_b - a * c;
     if (disc < R(0)) return false;
-    const R sqrtd = sqrt(disc);
+    const R sqrtd = sqrt_rn(disc);
     R root = RCP ? div_rcp(-half_b - sqrtd, a, inv_a) : (-half_b - sqrtd) / a;
     if (root < tmin || tmax < root) {
         root = RCP ? div_rcp(-half_b + sqrtd, a, inv_a) : (-half_b + sqrtd) / a;
@@ -408,7 +425,11 @@ constexpr uint32_t kKeyMiss = 0x7F800000u;
 __device__ __forceinline__ uint32_t slab_key_packed(float x0, float x1, float y0, float y1, float z0, float z1, int32_t child, float tminf,
                                                     float tmaxf) {
     const float lo = fmaxf(fmaxf(x0, y0), fmaxf(z0, tminf));
-    const float hi = fminf(fminf(x1, y1), fminf(z1, tmaxf));
+    // min(z1, tmaxf) as the bare instruction: fminf would re-quiet tmaxf (a loop-carried arithmetic result, never a
+    // signalling NaN) on every node visit; a NaN z1 (0 * inf plane distance) still drops out (IEEE-mode v_min)
+    float zt;
+    __asm__("v_min_f32 %0, %1, %2" : "=v"(zt) : "v"(z1), "v"(tmaxf));
+    const float hi = fminf(fminf(x1, y1), zt);
     const uint32_t key = (__float_as_uint(lo) & 0xFFFF0000u) | (static_cast<uint32_t>(child) & 0xFFFFu);
     return lo <= hi ? key : kKeyMiss;  // empty slots carry a box no ray enters (layout.h kLdsEmptyChild)
 }
