@@ -25,13 +25,30 @@ template <class R> __device__ __forceinline__ V3<R> operator-(V3<R> u, V3<R> v) 
 template <class R> __device__ __forceinline__ V3<R> operator-(V3<R> u) { return {-u.x, -u.y, -u.z}; }
 template <class R> __device__ __forceinline__ V3<R> operator*(V3<R> u, V3<R> v) { return {u.x * v.x, u.y * v.y, u.z * v.z}; }
 template <class R> __device__ __forceinline__ V3<R> operator*(R t, V3<R> v) { return {t * v.x, t * v.y, t * v.z}; }
+// std::sqrt, correctly rounded (sphere.h:47, vec3.h:42 length, vec3.h:152 refract, material.h:75 and
+// constant_medium.h:61).  For x >= 2^-767 this is the compiler's own f64 sqrt expansion (hardware rsq, then two
+// Goldschmidt and two Newton fma steps) without its denormal-range scaling and its zero/inf select, which never apply
+// there: the same operations on the same values, so the same bits.  Smaller x (and 0), inf and NaN take the
+// compiler's full sequence.  Saves 7 VALU per call: the leaf test's root, unit_vector and refraction per bounce.
+__device__ __forceinline__ double sqrt_rn(double x) {
+    if (!(x >= 0x1p-767 && x < __builtin_inf())) return sqrt(x);
+    const double y = __builtin_amdgcn_rsq(x);
+    double s = x * y, h = y * 0.5;
+    const double r = fma(-h, s, 0.5);
+    s = fma(s, r, s);
+    h = fma(h, r, h);
+    s = fma(fma(-s, s, x), h, s);
+    return fma(fma(-s, s, x), h, s);
+}
+__device__ __forceinline__ float sqrt_rn(float x) { return sqrtf(x); }
+
 template <class R> __device__ __forceinline__ R dot(V3<R> u, V3<R> v) { return u.x * v.x + u.y * v.y + u.z * v.z; }
 template <class R> __device__ __forceinline__ R len2(V3<R> v) { return v.x * v.x + v.y * v.y + v.z * v.z; }
 template <class R> __device__ __forceinline__ V3<R> cross(V3<R> u, V3<R> v) {
     return {u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x};
 }
 template <class R> __device__ __forceinline__ V3<R> divs(V3<R> v, R t) { return (R(1) / t) * v; }  // vec3.h:97-99
-template <class R> __device__ __forceinline__ V3<R> unit(V3<R> v) { return divs(v, sqrt(len2(v))); }
+template <class R> __device__ __forceinline__ V3<R> unit(V3<R> v) { return divs(v, sqrt_rn(len2(v))); }
 template <class R> __device__ __forceinline__ bool near_zero(V3<R> v) {  // vec3.h:49-53
     const R s = R(1e-8);
     return fabs(v.x) < s && fabs(v.y) < s && fabs(v.z) < s;
@@ -40,7 +57,7 @@ template <class R> __device__ __forceinline__ V3<R> reflect(V3<R> v, V3<R> n) { 
 template <class R> __device__ __forceinline__ V3<R> refract(V3<R> uv, V3<R> n, R eta) {  // vec3.h:149-154
     R cos_theta = fmin(dot(-uv, n), R(1));
     V3<R> perp = eta * (uv + cos_theta * n);
-    V3<R> par = (-sqrt(fabs(R(1) - len2(perp)))) * n;
+    V3<R> par = (-sqrt_rn(fabs(R(1) - len2(perp)))) * n;
     return perp + par;
 }
 template <class R> __device__ __forceinline__ V3<R> ld3(const R* p) { return {p[0], p[1], p[2]}; }
@@ -218,23 +235,6 @@ __device__ __forceinline__ R div_rcp(R x, R a, R inv_a) {
     const R q = x * inv_a;
     return fma(fma(-q, a, x), inv_a, q);
 }
-
-// std::sqrt of sphere.h:44 (correctly rounded).  For x >= 2^-767 this is the compiler's own f64 sqrt expansion
-// (hardware rsq, then two Goldschmidt / two Newton fma steps) without its denormal-range scaling and its zero/inf
-// select, which never apply there: the same operations on the same values, so the same bits.  Smaller x (and 0),
-// inf and NaN take the compiler's full sequence.  Saves 7 VALU per root, the leaf test's second-largest block after the
-// discriminant.
-__device__ __forceinline__ double sqrt_rn(double x) {
-    if (!(x >= 0x1p-767 && x < __builtin_inf())) return sqrt(x);
-    const double y = __builtin_amdgcn_rsq(x);
-    double s = x * y, h = y * 0.5;
-    const double r = fma(-h, s, 0.5);
-    s = fma(s, r, s);
-    h = fma(h, r, h);
-    s = fma(fma(-s, s, x), h, s);
-    return fma(fma(-s, s, x), h, s);
-}
-__device__ __forceinline__ float sqrt_rn(float x) { return sqrtf(x); }
 
 // sphere.h:39-65 / moving_sphere.h:41-58 (root selection only; the surface is rebuilt in shade).  a = |d|^2 of the
 // ray; RCP: the two root divisions by a use div_rcp with inv_a = 1 / a (same bits).
@@ -786,7 +786,7 @@ __device__ __forceinline__ bool hit_medium(const DevScene<R>& S, const uint8_t* 
     if (t2 > tmax) t2 = tmax;
     if (t1 >= t2) return false;
     if (t1 < R(0)) t1 = R(0);
-    const R ray_length = sqrt(len2(r.d));
+    const R ray_length = sqrt_rn(len2(r.d));
     const R inside = (t2 - t1) * ray_length;
     const R hit_distance = m.p[0] * log(uniform<R>(rng));
     if (hit_distance > inside) return false;

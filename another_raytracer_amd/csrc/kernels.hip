@@ -353,7 +353,7 @@ __device__ __forceinline__ bool scatter(const DevScene<R>& S, const MatRec<R>& m
         const R ratio = s.ff ? (R(1) / m.ir) : m.ir;
         const V3<R> ud = unit(st.ray.d);
         const R cos_theta = fmin(dot(-ud, s.n), R(1));
-        const R sin_theta = sqrt(R(1) - cos_theta * cos_theta);
+        const R sin_theta = sqrt_rn(R(1) - cos_theta * cos_theta);
         const bool cannot = ratio * sin_theta > R(1);
         bool refl = cannot;
         if (!cannot) {
@@ -433,7 +433,7 @@ __device__ __forceinline__ bool shade_hit_lds(const uint8_t* lds, uint32_t slot,
         att = mk(R(1), R(1), R(1));
         const R ratio = s.ff ? (R(1) / ir) : ir;
         const R cos_theta = fmin(dot(-u, s.n), R(1));
-        const R sin_theta = sqrt(R(1) - cos_theta * cos_theta);
+        const R sin_theta = sqrt_rn(R(1) - cos_theta * cos_theta);
         const bool cannot = ratio * sin_theta > R(1);
         bool refl = cannot;
         if (!cannot) {
