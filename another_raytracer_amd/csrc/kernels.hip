@@ -135,19 +135,19 @@ template <> struct HitRecD<double> {
 
 template <class R> struct ResRec;  // final per-slot radiance
 template <> struct ResRec<float> { float4 v; };
-template <> struct ResRec<double> { double2 a, b; };
+template <> struct ResRec<double> { double x, y, z; };  // 24 B, unpadded: k_accum streams these at HBM rate
 __device__ __forceinline__ void store_res(ResRec<float>* res, uint32_t q, V3<float> L) { res[q].v = make_float4(L.x, L.y, L.z, 0.0f); }
 __device__ __forceinline__ void store_res(ResRec<double>* res, uint32_t q, V3<double> L) {
-    res[q].a = make_double2(L.x, L.y);
-    res[q].b = make_double2(L.z, 0.0);
+    res[q].x = L.x;
+    res[q].y = L.y;
+    res[q].z = L.z;
 }
 __device__ __forceinline__ void load_res(const ResRec<float>* res, uint32_t q, double& r, double& g, double& b) {
     const float4 v = res[q].v;
     r = v.x; g = v.y; b = v.z;
 }
 __device__ __forceinline__ void load_res(const ResRec<double>* res, uint32_t q, double& r, double& g, double& b) {
-    const double2 a = res[q].a, c = res[q].b;
-    r = a.x; g = a.y; b = c.x;
+    r = res[q].x; g = res[q].y; b = res[q].z;
 }
 
 // ------------------------------------------------------------------------------------------------ work distribution

@@ -43,7 +43,7 @@ SURVEY_PIX_BYTES = 12
 #   3 (persistent paths): the path lives in registers; only the final radiance record of every path is written.
 EXTEND_BYTES = {"f32": 4 + 32 + 16 + 4, "f64": 4 + 64 + 16 + 4}
 PATH_BYTES = {"f32": 64, "f64": 128}
-RES_BYTES = {"f32": 16, "f64": 32}
+RES_BYTES = {"f32": 16, "f64": 24}
 
 
 def extend_moved_bytes(precision, variant, segments, primary):
