@@ -792,6 +792,38 @@ struct Compiler {
 };
 }  // namespace
 
+// Level-major node order: the roots of every BVH first, then all their inner children, level by level (a BFS over all
+// roots).  A relabelling only -- the same trees, boxes and child order, so the same traversals and images -- that puts
+// the levels every traversal walks next to each other at the front of the array.  (An LDS copy of those levels for
+// k_paths_g, read through flat loads, measured -20 % on cow and the Next-Week final scene and +-0 on dino, whose
+// whole tree fitted: node fetch latency is not what bounds k_paths_g.)
+static void relabel_level_major(FlatScene& f) {
+    const size_t n = f.nodes.size();
+    if (n == 0) return;
+    std::vector<int32_t> order, newid(n, -1);
+    order.reserve(n);
+    auto visit = [&](int32_t i) {
+        if (i >= 0 && newid[static_cast<size_t>(i)] < 0) {
+            newid[static_cast<size_t>(i)] = static_cast<int32_t>(order.size());
+            order.push_back(i);
+        }
+    };
+    for (const auto& o : f.objs)
+        if (o.kind == OBJ_BVH) visit(o.a);
+    for (size_t h = 0; h < order.size(); ++h)
+        for (int c = 0; c < 4; ++c) visit(f.nodes[static_cast<size_t>(order[h])].child[c]);
+    for (size_t i = 0; i < n; ++i) visit(static_cast<int32_t>(i));  // unreachable nodes (none expected) go last
+    std::vector<BvhNode> out(n);
+    for (size_t k = 0; k < n; ++k) {
+        out[k] = f.nodes[static_cast<size_t>(order[k])];
+        for (int c = 0; c < 4; ++c)
+            if (out[k].child[c] >= 0) out[k].child[c] = newid[static_cast<size_t>(out[k].child[c])];
+    }
+    f.nodes.swap(out);
+    for (auto& o : f.objs)
+        if (o.kind == OBJ_BVH && o.a >= 0) o.a = newid[static_cast<size_t>(o.a)];
+}
+
 FlatScene compile_scene(const SceneGraph& g) {
     FlatScene f;
     if (g.world.empty()) throw std::runtime_error("Invalid input scene!");  // engine.h:32-36
@@ -850,6 +882,7 @@ FlatScene compile_scene(const SceneGraph& g) {
                  (f.boxes.empty() ? 0u : F_BOX) | (f.has_media ? F_MEDIA : 0u);
     for (const auto& o : f.objs)
         if (o.kind == OBJ_TRANSLATE || o.kind == OBJ_ROTATE_Y) f.features |= F_XFORM;
+    relabel_level_major(f);
     return f;
 }
 
