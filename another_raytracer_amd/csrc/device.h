@@ -779,9 +779,39 @@ __device__ __forceinline__ bool hit_medium(const DevScene<R>& S, const uint8_t* 
                                            StackT<L>* stk, uint64_t& rng, R& t) {
     const R inf = R(__builtin_inf());
     R t1, t2;
-    uint32_t p, f, mt;
-    if (!hit_object<R, F, B, L>(S, lds, m.a, r, -inf, inf, stk, t1, p, f, mt)) return false;
-    if (!hit_object<R, F, B, L>(S, lds, m.a, r, t1 + R(0.0001), inf, stk, t2, p, f, mt)) return false;
+    const ObjRec<R>& bo = S.objs[m.a];
+    if ((F & F_SPHERE) && bo.kind == OBJ_PRIM && primref_type(static_cast<uint32_t>(bo.a)) == PRIM_SPHERE) {
+        // A sphere boundary (every medium of the reference scenes but the Cornell smoke boxes): the two boundary->hit
+        // calls (constant_medium.h:43, :46) compute the same oc, half_b, c, discriminant and sqrt (sphere.h:39-47)
+        // from the same ray and sphere, so both root selections (sphere.h:49-55) run on one quadratic: the same
+        // values, half the arithmetic.
+        const SphereRec<R>& sp = S.spheres[primref_index(static_cast<uint32_t>(bo.a))];
+        V3<R> center = ld3(sp.c);
+        if (sp.flags & SPH_MOVING) center = moving_center(center, ld3(sp.d), sp.t0, sp.dt, r.tm);
+        const V3<R> oc = r.o - center;
+        const R a = len2(r.d);
+        const R half_b = dot(oc, r.d);
+        const R c = len2(oc) - sp.r * sp.r;
+        const R disc = half_b * half_b - a * c;
+        if (disc < R(0)) return false;
+        const R sqrtd = sqrt_rn(disc);
+        const R r_near = (-half_b - sqrtd) / a, r_far = (-half_b + sqrtd) / a;
+        t1 = r_near;  // first call, t in [-inf, inf]
+        if (t1 < -inf || inf < t1) {
+            t1 = r_far;
+            if (t1 < -inf || inf < t1) return false;
+        }
+        const R tmin2 = t1 + R(0.0001);  // second call, t in [t1 + 0.0001, inf]
+        t2 = r_near;
+        if (t2 < tmin2 || inf < t2) {
+            t2 = r_far;
+            if (t2 < tmin2 || inf < t2) return false;
+        }
+    } else {
+        uint32_t p, f, mt;
+        if (!hit_object<R, F, B, L>(S, lds, m.a, r, -inf, inf, stk, t1, p, f, mt)) return false;
+        if (!hit_object<R, F, B, L>(S, lds, m.a, r, t1 + R(0.0001), inf, stk, t2, p, f, mt)) return false;
+    }
     if (t1 < tmin) t1 = tmin;
     if (t2 > tmax) t2 = tmax;
     if (t1 >= t2) return false;
