@@ -465,18 +465,26 @@ __device__ __forceinline__ void cas(float& ka, int32_t& ca, float& kb, int32_t& 
 }
 
 // Leaf slot test of the LDS scene image (layout.h): the same root selection as hit_sphere on the same f64 values.
-// d_a = |d|^2 and d_inv_a = 1 / d_a come from the traversal (once per ray).
+// d_a = |d|^2 and d_inv_a = 1 / d_a come from the traversal (once per ray).  The image sits at LDS address 0, so
+// every read takes an integer LDS byte address (one shift-add, the plane offset folded in).  Moving spheres of the
+// image span the unit shutter (lds_scene_image checks it): moving_sphere.h:72-74's fraction (tm - 0) / 1 is tm.
+typedef double d2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ double2 lds_d2(uint32_t addr) {
+    const d2v v = *(__attribute__((address_space(3))) const d2v*)(size_t)addr;
+    return make_double2(v.x, v.y);
+}
+__device__ __forceinline__ double lds_d1(uint32_t addr) { return *(__attribute__((address_space(3))) const double*)(size_t)addr; }
+__device__ __forceinline__ uint32_t lds_u1(uint32_t addr) { return *(__attribute__((address_space(3))) const uint32_t*)(size_t)addr; }
 __device__ __forceinline__ bool hit_lds_slot(const uint8_t* lds, uint32_t slot, const Ray<double>& r, double d_a, double d_inv_a,
                                              double tmin, double tmax, double& t, uint32_t& prim, uint32_t& mt) {
-    const double2* sp = reinterpret_cast<const double2*>(lds + kLdsOffSph) + slot;
-    const double2 a = sp[0], b = sp[kLdsSlotCap];
-    const uint32_t code = reinterpret_cast<const uint32_t*>(lds + kLdsOffRef)[slot];
+    const double2 a = lds_d2(kLdsOffSph + slot * 16u), b = lds_d2(kLdsOffSph + (kLdsSlotCap + slot) * 16u);
+    const uint32_t code = lds_u1(kLdsOffRef + slot * 4u);
     V3<double> center{a.x, a.y, b.x};
     const uint32_t mv = (code >> kLdsRefMovShift) & ((1u << (kLdsRefMatShift - kLdsRefMovShift)) - 1);
     if (mv) {
-        const double2* mp = reinterpret_cast<const double2*>(lds + kLdsOffMov) + (mv - 1);
-        const double2 m0 = mp[0], m1 = mp[kLdsMovCap], m2 = mp[2 * kLdsMovCap];
-        center = moving_center(center, V3<double>{m0.x, m0.y, m1.x}, m1.y, m2.x, r.tm);
+        const double2 m0 = lds_d2(kLdsOffMov + (mv - 1u) * 16u);
+        const double dz = lds_d1(kLdsOffMov + (kLdsMovCap + mv - 1u) * 16u);
+        center = center + r.tm * V3<double>{m0.x, m0.y, dz};
     }
     prim = make_primref(PRIM_SPHERE, code & kLdsRefIndexMask);
     mt = code >> kLdsRefMatShift;

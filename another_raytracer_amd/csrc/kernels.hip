@@ -394,8 +394,8 @@ __device__ __forceinline__ bool shade_hit_lds(const uint8_t* lds, uint32_t slot,
     const uint32_t mv = (code >> kLdsRefMovShift) & ((1u << (kLdsRefMatShift - kLdsRefMovShift)) - 1);
     if (mv) {  // moving_sphere.h:72-74, as prim_surface
         const double2* mp = reinterpret_cast<const double2*>(lds + kLdsOffMov) + (mv - 1);
-        const double2 m0 = mp[0], m1 = mp[kLdsMovCap], m2 = mp[2 * kLdsMovCap];
-        center = center + motion_fraction(st.ray.tm, m1.y, m2.x) * V3<R>{m0.x, m0.y, m1.x};
+        const double2 m0 = mp[0], m1 = mp[kLdsMovCap];
+        center = center + st.ray.tm * V3<R>{m0.x, m0.y, m1.x};  // unit shutter (lds_scene_image): (tm - 0) / 1 == tm
     }
     Surf<R> s;
     s.p = st.ray.at(t);
@@ -1092,7 +1092,13 @@ static std::vector<uint8_t> lds_scene_image(const FlatScene& f, uint32_t& nmov, 
         return img;
     for (uint32_t ref : f.primrefs) {
         if (primref_type(ref) != PRIM_SPHERE) return img;
-        if (f.spheres[primref_index(ref)].flags & SPH_MOVING) ++nmov;
+        const SphereRec<double>& sp = f.spheres[primref_index(ref)];
+        if (sp.flags & SPH_MOVING) {
+            // the image's moving spheres span the unit shutter (every moving_sphere of the reference scenes,
+            // scene_manager.cpp:35): their centre fraction is the ray time itself (hit_lds_slot)
+            if (sp.t0 != 0.0 || sp.dt != 1.0) return img;
+            ++nmov;
+        }
     }
     if (nmov > kLdsMovCap) return img;
     for (const BvhNode& b : f.nodes)
