@@ -566,13 +566,13 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                 iz = __builtin_amdgcn_rcpf(static_cast<float>(r.d.z));
     const float oix = ox * ix, oiy = oy * iy, oiz = oz * iz;
     // LDS variant: the near and far plane of each axis follow from the direction's sign, so the slab test reads them
-    // directly (near plane offset per axis; the far plane is the neighbouring plane, one kLdsPlane away) and needs no
-    // per-axis min/max
+    // directly (near plane offset per axis; the far plane is always the plane above it, one kLdsPlane away -- an
+    // immediate DS offset -- since each axis stores lo, hi, lo) and needs no per-axis min/max
     constexpr uint32_t kLdsPlane = kLdsNodeCap * 16;
-    static_assert((kLdsPlane & (kLdsPlane - 1)) == 0 && kLdsOffNodes % (2 * kLdsPlane) == 0, "plane pairs differ in one address bit");
+    static_assert((kLdsPlane & (kLdsPlane - 1)) == 0 && kLdsOffNodes % kLdsPlane == 0, "node offsets OR into plane offsets");
     const uint32_t off_nx = kLdsOffNodes + (0u + (__float_as_uint(ix) >> 31)) * kLdsPlane;
-    const uint32_t off_ny = kLdsOffNodes + (2u + (__float_as_uint(iy) >> 31)) * kLdsPlane;
-    const uint32_t off_nz = kLdsOffNodes + (4u + (__float_as_uint(iz) >> 31)) * kLdsPlane;
+    const uint32_t off_ny = kLdsOffNodes + (3u + (__float_as_uint(iy) >> 31)) * kLdsPlane;
+    const uint32_t off_nz = kLdsOffNodes + (6u + (__float_as_uint(iz) >> 31)) * kLdsPlane;
     const float tminf = f_lo(tmin);
     float tmaxf = f_hi(tmax);
     // L: |d|^2 and its reciprocal for the leaf root divisions (div_rcp).  A traced direction is never zero (camera
@@ -602,12 +602,12 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                 const uint32_t n16 = static_cast<uint32_t>(node) * 16u;
                 const uint32_t ax = n16 | off_nx, ay = n16 | off_ny, az = n16 | off_nz;
                 lx = lds_f4(ax);
-                hx = lds_f4(ax ^ kLdsPlane);
+                hx = lds_f4(ax + kLdsPlane);
                 ly = lds_f4(ay);
-                hy = lds_f4(ay ^ kLdsPlane);
+                hy = lds_f4(ay + kLdsPlane);
                 lz = lds_f4(az);
-                hz = lds_f4(az ^ kLdsPlane);
-                ch = lds_i4(kLdsOffNodes + 6 * kLdsPlane + n16);
+                hz = lds_f4(az + kLdsPlane);
+                ch = lds_i4(kLdsOffNodes + 9 * kLdsPlane + n16);
             } else {
                 const float4* np = reinterpret_cast<const float4*>(S.nodes + node);
                 lx = np[0]; hx = np[1]; ly = np[2]; hy = np[3]; lz = np[4]; hz = np[5];

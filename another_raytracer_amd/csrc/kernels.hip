@@ -1118,8 +1118,10 @@ static std::vector<uint8_t> lds_scene_image(const FlatScene& f, uint32_t& nmov, 
             for (int j = 0; j < 6; ++j) planes[j][c] = empty ? kLdsEmptyBox : src[j][c];
             child[c] = empty ? kLdsEmptyChild : b.child[c] >= 0 ? b.child[c] : lds_leaf(leaf_first(b.child[c]), leaf_count(b.child[c]));
         }
-        for (uint32_t j = 0; j < 6; ++j) put(kLdsOffNodes + (j * kLdsNodeCap + static_cast<uint32_t>(n)) * 16, planes[j], 16);
-        put(kLdsOffNodes + (6 * kLdsNodeCap + static_cast<uint32_t>(n)) * 16, child, 16);
+        // per axis: lo, hi, lo (layout.h kLdsNodePlanes), then the child codes
+        const int order[9] = {0, 1, 0, 2, 3, 2, 4, 5, 4};
+        for (uint32_t j = 0; j < 9; ++j) put(kLdsOffNodes + (j * kLdsNodeCap + static_cast<uint32_t>(n)) * 16, planes[order[j]], 16);
+        put(kLdsOffNodes + (9 * kLdsNodeCap + static_cast<uint32_t>(n)) * 16, child, 16);
     }
     // shading table: one entry per material (two for a checker of solid colours); anything else keeps the scene off
     // the fused variant (shade_ok = false), which shades from the global scene records instead
@@ -1143,10 +1145,9 @@ static std::vector<uint8_t> lds_scene_image(const FlatScene& f, uint32_t& nmov, 
         put(kLdsOffInvR + sl * 8, &inv_r, 8);
         uint32_t code = idx | (f.mats[sp.mat].type << kLdsRefMatShift);
         if (sp.flags & SPH_MOVING) {
-            const double m0[2] = {sp.d[0], sp.d[1]}, m1[2] = {sp.d[2], sp.t0}, m2[2] = {sp.dt, 0.0};
+            const double m0[2] = {sp.d[0], sp.d[1]}, m1[2] = {sp.d[2], 0.0};
             put(kLdsOffMov + m * 16, m0, 16);
             put(kLdsOffMov + (kLdsMovCap + m) * 16, m1, 16);
-            put(kLdsOffMov + (2 * kLdsMovCap + m) * 16, m2, 16);
             code |= (m + 1) << kLdsRefMovShift;
             ++m;
         }

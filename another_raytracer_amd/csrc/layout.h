@@ -84,14 +84,17 @@ constexpr int kMaxStackDepth = 64;   // per-lane LDS traversal stack entries (si
 // node and sphere fetches of the traversal never touch the vector-memory (TA/L1) path that bounds the global variant.
 // Every plane is an array of 16-B entries, so lanes fetching different nodes/spheres spread over the 16 four-bank slots
 // of the ds_read_b128 bank row, and the plane strides are compile-time (DS immediate offsets, no address VALU).
-constexpr uint32_t kLdsNodeCap = 256;   // BVH4 nodes: 7 planes (lox, hix, loy, hiy, loz, hiz as float4; child as int4)
+// BVH4 nodes: 10 planes -- per axis (lo, hi, lo again) as float4, so the far plane of either direction sign is one
+// plane above the near one (an immediate DS offset); child codes as int4
+constexpr uint32_t kLdsNodeCap = 256;
+constexpr uint32_t kLdsNodePlanes = 10;
 constexpr uint32_t kLdsSlotCap = 1024;  // leaf slots (= primref array entries): 2 planes (cx, cy), (cz, r) as double2
-constexpr uint32_t kLdsMovCap = 512;    // moving spheres: 3 planes (dx, dy), (dz, t0), (dt, 0) as double2
+constexpr uint32_t kLdsMovCap = 512;    // moving spheres (unit shutter): 2 planes (dx, dy), (dz, 0) as double2
 constexpr uint32_t kLdsOffNodes = 0;
-constexpr uint32_t kLdsOffSph = kLdsOffNodes + 7 * kLdsNodeCap * 16;
+constexpr uint32_t kLdsOffSph = kLdsOffNodes + kLdsNodePlanes * kLdsNodeCap * 16;
 constexpr uint32_t kLdsOffMov = kLdsOffSph + 2 * kLdsSlotCap * 16;
 // u32 per slot: sphere index (19 bits) | (moving index + 1) << 19 (10 bits) | material type << 29 (3 bits)
-constexpr uint32_t kLdsOffRef = kLdsOffMov + 3 * kLdsMovCap * 16;
+constexpr uint32_t kLdsOffRef = kLdsOffMov + 2 * kLdsMovCap * 16;
 // Shading table (fused variant): u16 per slot = material entry e | kLdsMatChecker, and kLdsMatCap 32-B entries
 // (c.x, c.y), (c.z, param): lambertian / diffuse_light colour (a checker of two solid colours takes entries e = even,
 // e + 1 = odd), metal albedo + fuzz, dielectric (-, -, -, ir).  A hit is then shaded without any global load.
