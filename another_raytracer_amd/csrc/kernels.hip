@@ -1095,7 +1095,7 @@ static std::vector<uint8_t> lds_scene_image(const FlatScene& f, uint32_t& nmov, 
         const SphereRec<double>& sp = f.spheres[primref_index(ref)];
         if (sp.flags & SPH_MOVING) {
             // the image's moving spheres span the unit shutter (every moving_sphere of the reference scenes,
-            // scene_manager.cpp:35): their centre fraction is the ray time itself (hit_lds_slot)
+            // scene_manager.cpp:34-35, :201): their centre fraction is the ray time itself (hit_lds_slot)
             if (sp.t0 != 0.0 || sp.dt != 1.0) return img;
             ++nmov;
         }
