@@ -34,6 +34,11 @@
 #define ART_EXTEND_MIN_WAVES 1  // __launch_bounds__ minimum waves per SIMD for k_extend (register budget knob)
 #endif
 
+// ART_SPLIT_PATHS (Makefile): unset = one translation unit; 1 = everything but k_paths and its launcher; 2 = only
+// k_paths and its launcher (kernels_paths.o, compiled with its own scheduler strategy, measured best for it alone).
+#ifndef ART_SPLIT_PATHS
+#define ART_SPLIT_PATHS 0
+#endif
 namespace art {
 
 #define HIP_OK(x)                                                                                         \
@@ -625,6 +630,7 @@ constexpr size_t kJumpBytes = sizeof(JumpEntry) * kJumpEntries;
 __host__ __device__ constexpr size_t paths_lds_bytes(uint32_t stack) {
     return kLdsImageBytes + paths_stack_bytes(stack) + kJumpBytes + sizeof(CameraRec<double>) + sizeof(PassGeom);
 }
+#if ART_SPLIT_PATHS != 1
 __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S, PassGeom g, CameraRec<double> cam, Work<double> w, uint32_t* next_slot) {
     using R = double;
     constexpr int B = kBlockL;
@@ -724,6 +730,8 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S, PassGe
     for (int off = 32; off > 0; off >>= 1) segs += __shfl_xor(segs, off);
     if (lane == 0) atomicAdd(w.segments, segs);
 }
+
+#endif  // ART_SPLIT_PATHS != 1
 
 // Persistent paths over the HBM scene (EXT_MEGA_G): the k_paths loop for every scene that does not fit the LDS
 // image (triangles, rects, boxes, transforms, media, noise/image textures).  A lane owns one path from its camera
@@ -892,6 +900,7 @@ __global__ __launch_bounds__(256) void k_accum(PassGeom g, Work<R> w) {
     a[2] = b;
 }
 
+#if ART_SPLIT_PATHS != 2
 __global__ void k_finalize(const double* acc, uint8_t* rgb, uint32_t n, int spp) {  // color.h:6-22
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -1039,6 +1048,9 @@ __global__ void k_adapt_fill(int32_t* work, uint8_t* rgb, int W, int rows, int s
     for (int c = 0; c < 3; ++c) rgb[3 * static_cast<size_t>(p) + c] = static_cast<uint8_t>(o[c]);
 }
 
+#endif  // ART_SPLIT_PATHS != 2
+
+#if ART_SPLIT_PATHS != 2
 // ------------------------------------------------------------------------------------------------ device scene
 template <class R>
 struct DeviceScene {
@@ -1311,6 +1323,7 @@ size_t Renderer::scene_bytes(int fp) const {
 }
 const FlatScene& Renderer::flat() const { return impl_->flat; }
 
+#endif
 // The LDS-scene kernels address the scene image at LDS address 0 (device.h lds_f4): they must declare no static
 // __shared__ variables, which would be placed first.
 static bool static_lds_is_zero(const void* kernel) {
@@ -1319,6 +1332,7 @@ static bool static_lds_is_zero(const void* kernel) {
     if (a.sharedSizeBytes != 0) throw std::runtime_error("LDS-scene kernel has static LDS: the scene image would not start at address 0");
     return true;
 }
+#if ART_SPLIT_PATHS != 2
 // Persistent extend grid for a given dynamic LDS size: every block the CUs can hold at once.
 template <class R, uint32_t F, bool L, bool FUSE>
 static int extend_blocks(int num_cu, size_t lds) {
@@ -1424,7 +1438,14 @@ static void launch_paths_g(uint32_t feat, bool tex_basic, int num_cu, hipStream_
         launch_paths_g_ft<F_ALL, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
     }
 }
-static void launch_paths(int num_cu, hipStream_t st, const DevScene<double>& S, const PassGeom& g, const CameraRec<double>& cam,
+#endif
+#if ART_SPLIT_PATHS == 0
+#define ART_PATHS_LINKAGE static
+#else
+#define ART_PATHS_LINKAGE
+#endif
+#if ART_SPLIT_PATHS != 1
+ART_PATHS_LINKAGE void launch_paths(int num_cu, hipStream_t st, const DevScene<double>& S, const PassGeom& g, const CameraRec<double>& cam,
                          const Work<double>& w, uint32_t* next_slot) {
     const size_t lds = paths_lds_bytes(g.stack);
     static size_t attr_lds = 0;
@@ -1436,6 +1457,11 @@ static void launch_paths(int num_cu, hipStream_t st, const DevScene<double>& S, 
     }
     hipLaunchKernelGGL(k_paths, dim3(num_cu), dim3(kBlockL), lds, st, S, g, cam, w, next_slot);
 }
+#else
+void launch_paths(int num_cu, hipStream_t st, const DevScene<double>& S, const PassGeom& g, const CameraRec<double>& cam,
+                  const Work<double>& w, uint32_t* next_slot);  // kernels_paths.o
+#endif
+#if ART_SPLIT_PATHS != 2
 template <class R>
 static void bounce(const DeviceScene<R>& ds, int variant, int num_cu, hipStream_t st, const PassGeom& g, const CameraRec<R>& cam, const Work<R>& w,
                    int d, const std::function<void()>& mark) {
@@ -1698,8 +1724,10 @@ void Renderer::render(const CameraRec<double>& cam, const RenderParams& p, uint8
     }
 }
 
+#endif  // ART_SPLIT_PATHS != 2
 }  // namespace art
 
+#if ART_SPLIT_PATHS != 2
 namespace art {
 int device_count() {
     int n = 0;
@@ -1707,3 +1735,4 @@ int device_count() {
     return n;
 }
 }  // namespace art
+#endif
