@@ -511,6 +511,9 @@ __device__ __forceinline__ void stat_lane(int k) { atomicAdd(&g_art_stats[k], 1u
 #ifndef ART_SPECULATIVE
 #define ART_SPECULATIVE 1
 #endif
+#ifndef ART_LEAF2_G
+#define ART_LEAF2_G 1  // the HBM-scene traversal also tests a lane's two pending leaves in one leaf phase
+#endif
 
 // The LDS scene image lives at LDS address 0 (k_extend and k_paths allocate LDS dynamically only), so node fetches
 // take a plain 32-bit LDS byte address: no base add per load.
@@ -670,7 +673,7 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
         int32_t leaf2 = kNodeEmpty;
         if (leaf != kNodeEmpty) {
             parked = kNodeEmpty;
-            if (L && node < kNodeEmpty) {
+            if ((L || ART_LEAF2_G) && node < kNodeEmpty) {
                 leaf2 = node;
                 node = st.peek();
                 st.pop_if(true);
@@ -704,7 +707,9 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
             first = leaf_first(leaf);
             cnt = leaf_count(leaf);
 #if ART_SPECULATIVE
-            cnt12 = cnt;
+            // leaf2 == kNodeEmpty decodes as an empty range (first 0, count 0)
+            first2 = leaf_first(leaf2) - cnt;
+            cnt12 = cnt + leaf_count(leaf2);
 #endif
         }
 #if ART_SPECULATIVE
@@ -726,7 +731,11 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                 h = hit_lds_slot(lds, slot, r, d_a, d_inv_a, tmin, tmax, tt, ref, m);
                 fc = slot;  // the leaf slot travels in the face field (spheres have no face): LDS shading reads it
             } else {
+#if ART_SPECULATIVE
+                ref = S.primrefs[(k < cnt ? first : first2) + k];
+#else
                 ref = S.primrefs[first + k];
+#endif
                 h = hit_prim<R, F>(S, ref, r, tmin, tmax, tt, fc);
             }
             if (h) {
