@@ -18,7 +18,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ART_LIB") or os.path.join(_HERE, "libart.so")  # ART_LIB: A/B another build
 
 RT_OK = 0
-RT_FP32, RT_FP64 = 0, 1
+RT_FP64 = 0  # the only fp_mode since ABI 2 (include/art.h)
+RT_ABI_VERSION = 2
 RT_OUT_DEVICE, RT_PROFILE, RT_GLOBAL_SCENE, RT_SPLIT_SHADE, RT_ADAPTIVE, RT_WAVEFRONT = 1, 2, 4, 8, 16, 32
 ERRORS = {-1: "RT_E_INVALID", -2: "RT_E_SCENE", -3: "RT_E_DEVICE", -4: "RT_E_INTERNAL"}
 
@@ -54,9 +55,11 @@ class rt_scene_info(ctypes.Structure):
                 ("spheres", ctypes.c_int64), ("triangles", ctypes.c_int64), ("rects", ctypes.c_int64),
                 ("boxes", ctypes.c_int64), ("bvh_nodes", ctypes.c_int64), ("objects", ctypes.c_int64),
                 ("materials", ctypes.c_int64), ("textures", ctypes.c_int64), ("has_media", ctypes.c_int32),
-                ("max_bvh_depth", ctypes.c_int32), ("device_bytes_f32", ctypes.c_uint64),
-                ("device_bytes_f64", ctypes.c_uint64)]
+                ("max_bvh_depth", ctypes.c_int32), ("device_bytes_f64", ctypes.c_uint64)]
 
+
+# rt_progress_fn (include/art.h): int (*)(void* user, int32_t samples_done, int32_t spp, const uint8_t*, const double*)
+rt_progress_fn = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p)
 
 # Every symbol include/art.h declares, with its ctypes signature (tests/test_abi.py checks the header agrees).
 _P, _I, _D, _S = ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_size_t
@@ -71,7 +74,13 @@ SIGNATURES = {
     "rt_scene_dump": (_S, [_P, ctypes.c_char_p, _S]),
     "rt_scene_destroy": (None, [_P]),
     "rt_render": (_I, [_P, ctypes.POINTER(rt_camera), ctypes.POINTER(rt_params), _P, _P, ctypes.POINTER(rt_stats)]),
+    "rt_render_progressive": (_I, [_P, ctypes.POINTER(rt_camera), ctypes.POINTER(rt_params), _P, _P, rt_progress_fn, _P,
+                                   ctypes.POINTER(rt_stats)]),
     "rt_local_rows": (_I, [ctypes.POINTER(rt_params), ctypes.POINTER(ctypes.c_int32)]),
+    "rt_multi_create": (_I, [ctypes.c_char_p, ctypes.c_char_p, _IP, _I, ctypes.POINTER(_P)]),
+    "rt_multi_from_graph": (_I, [_P, _IP, _I, ctypes.POINTER(_P)]),
+    "rt_multi_destroy": (None, [_P]),
+    "rt_render_multi": (_I, [_P, ctypes.POINTER(rt_camera), ctypes.POINTER(rt_params), _P, ctypes.POINTER(rt_stats)]),
     "rt_graph_new": (_P, []),
     "rt_graph_free": (None, [_P]),
     "rt_graph_random_double": (_I, [_P, _DP]),
@@ -112,6 +121,8 @@ def _load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.rt_abi_version() != RT_ABI_VERSION:
+        raise ImportError(f"{LIB_PATH} has ABI {lib.rt_abi_version()}, this binding expects {RT_ABI_VERSION}: rebuild it")
     return lib
 
 

@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "art.h"
+#include "multi.h"
 #include "renderer.h"
 #include "objmesh.h"
 #include "scene.h"
@@ -24,6 +25,11 @@ struct rt_scene {
 };
 struct rt_graph {
     art::SceneGraph g;
+};
+struct rt_multi {
+    art::SceneGraph graph;
+    art::FlatScene flat;
+    std::unique_ptr<art::MultiRenderer> renderer;
 };
 
 namespace {
@@ -55,9 +61,53 @@ bool valid_params(const rt_params* p, std::string& why) {
         why = "band partition must satisfy band_rows >= 1, band_count >= 1, 0 <= band_index < band_count";
         return false;
     }
-    if (p->fp_mode != RT_FP32 && p->fp_mode != RT_FP64) { why = "fp_mode must be RT_FP32 or RT_FP64"; return false; }
+    if (p->fp_mode != RT_FP64) { why = "fp_mode must be RT_FP64 (0): the reference's double arithmetic is the only mode"; return false; }
     if (static_cast<int64_t>(p->width) * p->height > (int64_t(1) << 31)) { why = "image too large"; return false; }
     return true;
+}
+art::RenderParams render_params(const rt_params* p) {
+    art::RenderParams rp;
+    rp.width = p->width;
+    rp.height = p->height;
+    rp.spp = p->spp;
+    rp.max_depth = p->max_depth;
+    rp.seed = p->seed;
+    rp.fp_mode = p->fp_mode;
+    rp.band_rows = p->band_rows;
+    rp.band_count = p->band_count;
+    rp.band_index = p->band_index;
+    rp.samples_per_pass = p->samples_per_pass;
+    rp.flags = p->flags;
+    rp.stream = p->stream;
+    for (int c = 0; c < 3; ++c) rp.background[c] = p->background[c];
+    return rp;
+}
+void fill_stats(const art::RenderStats& st, rt_stats* stats) {
+    if (!stats) return;
+    std::memset(stats, 0, sizeof *stats);
+    stats->segments = st.segments;
+    stats->primary = st.primary;
+    stats->ms = st.ms;
+    stats->extend_ms = st.extend_ms;
+    stats->shade_ms = st.shade_ms;
+    stats->extend_launches = st.extend_launches;
+    stats->shade_launches = st.shade_launches;
+    stats->passes = st.passes;
+    stats->samples_per_pass = st.samples_per_pass;
+    stats->local_rows = st.local_rows;
+    stats->extend_variant = st.extend_variant;
+}
+art::CameraRec<double> camera_of(const rt_camera* cam) {
+    return art::make_camera(cam->lookfrom, cam->lookat, cam->vup, cam->vfov, cam->aspect, cam->aperture, cam->focus_dist, cam->time0, cam->time1);
+}
+int multi_from_graph(art::SceneGraph graph, const int* devices, int ngpus, rt_multi** out) {
+    if (!devices || ngpus < 1) return fail(RT_E_INVALID, "devices must list ngpus >= 1 device ids");
+    auto m = std::make_unique<rt_multi>();
+    m->graph = std::move(graph);
+    m->flat = art::compile_scene(m->graph);
+    m->renderer = std::make_unique<art::MultiRenderer>(m->flat, std::vector<int>(devices, devices + ngpus));
+    *out = m.release();
+    return RT_OK;
 }
 int scene_from_graph(art::SceneGraph graph, int device, rt_scene** out) {
     auto s = std::make_unique<rt_scene>();
@@ -108,8 +158,7 @@ int rt_scene_info_get(const rt_scene* s, rt_scene_info* info) {
     info->has_media = s->flat.has_media ? 1 : 0;
     info->max_bvh_depth = s->flat.max_bvh_depth;
     if (s->renderer) {
-        info->device_bytes_f32 = s->renderer->scene_bytes(RT_FP32);
-        info->device_bytes_f64 = s->renderer->scene_bytes(RT_FP64);
+        info->device_bytes_f64 = s->renderer->scene_bytes();
     }
     return RT_OK;
 }
@@ -167,38 +216,64 @@ int rt_render(rt_scene* s, const rt_camera* cam, const rt_params* p, uint8_t* ou
     }
     return guard(RT_E_DEVICE, [&] {
         if (!s->renderer) s->renderer = std::make_unique<art::Renderer>(s->flat, s->device);
-        art::CameraRec<double> c = art::make_camera(cam->lookfrom, cam->lookat, cam->vup, cam->vfov, cam->aspect, cam->aperture,
-                                                    cam->focus_dist, cam->time0, cam->time1);
-        art::RenderParams rp;
-        rp.width = p->width;
-        rp.height = p->height;
-        rp.spp = p->spp;
-        rp.max_depth = p->max_depth;
-        rp.seed = p->seed;
-        rp.fp_mode = p->fp_mode;
-        rp.band_rows = p->band_rows;
-        rp.band_count = p->band_count;
-        rp.band_index = p->band_index;
-        rp.samples_per_pass = p->samples_per_pass;
-        rp.flags = p->flags;
-        rp.stream = p->stream;
-        for (int c = 0; c < 3; ++c) rp.background[c] = p->background[c];
         art::RenderStats st;
-        s->renderer->render(c, rp, out_rgb8, out_accum, st);
-        if (stats) {
-            std::memset(stats, 0, sizeof *stats);
-            stats->segments = st.segments;
-            stats->primary = st.primary;
-            stats->ms = st.ms;
-            stats->extend_ms = st.extend_ms;
-            stats->shade_ms = st.shade_ms;
-            stats->extend_launches = st.extend_launches;
-            stats->shade_launches = st.shade_launches;
-            stats->passes = st.passes;
-            stats->samples_per_pass = st.samples_per_pass;
-            stats->local_rows = st.local_rows;
-            stats->extend_variant = st.extend_variant;
-        }
+        s->renderer->render(camera_of(cam), render_params(p), out_rgb8, out_accum, st);
+        fill_stats(st, stats);
+        return RT_OK;
+    });
+}
+
+int rt_render_progressive(rt_scene* s, const rt_camera* cam, const rt_params* p, uint8_t* out_rgb8, double* out_accum, rt_progress_fn cb,
+                          void* user, rt_stats* stats) {
+    std::string why;
+    if (!s || !cam || !cb || !out_rgb8) return fail(RT_E_INVALID, "scene, camera, callback and out_rgb8 must be non-NULL");
+    if (!valid_params(p, why)) return fail(RT_E_INVALID, why);
+    if (p->flags & RT_ADAPTIVE) return fail(RT_E_INVALID, "progressive rendering traces whole frames (no RT_ADAPTIVE)");
+    return guard(RT_E_DEVICE, [&] {
+        if (!s->renderer) s->renderer = std::make_unique<art::Renderer>(s->flat, s->device);
+        art::RenderParams rp = render_params(p);
+        if (rp.samples_per_pass <= 0) rp.samples_per_pass = (rp.spp + 7) / 8;
+        const int spp = rp.spp;
+        rp.on_pass = [&](int done) { return cb(user, done, spp, out_rgb8, out_accum) == 0; };
+        art::RenderStats st;
+        s->renderer->render(camera_of(cam), rp, out_rgb8, out_accum, st);
+        fill_stats(st, stats);
+        return RT_OK;
+    });
+}
+
+// ---------------------------------------------------------------------------------------------- multi-GPU
+int rt_multi_create(const char* name, const char* asset_dir, const int* devices, int ngpus, rt_multi** out) {
+    if (!name || !out) return fail(RT_E_INVALID, "name and out must be non-NULL");
+    *out = nullptr;
+    art::SceneGraph g;
+    const int rc = guard(RT_E_SCENE, [&] {
+        art::build_builtin_scene(g, name, asset_dir ? asset_dir : "assets");
+        return RT_OK;
+    });
+    if (rc != RT_OK) return rc;
+    return guard(RT_E_DEVICE, [&] { return multi_from_graph(std::move(g), devices, ngpus, out); });
+}
+int rt_multi_from_graph(rt_graph* g, const int* devices, int ngpus, rt_multi** out) {
+    if (!g || !out) return fail(RT_E_INVALID, "graph and out must be non-NULL");
+    *out = nullptr;
+    return guard(RT_E_DEVICE, [&] { return multi_from_graph(g->g, devices, ngpus, out); });
+}
+void rt_multi_destroy(rt_multi* m) {
+    try {
+        delete m;
+    } catch (...) {
+    }
+}
+int rt_render_multi(rt_multi* m, const rt_camera* cam, const rt_params* p, uint8_t* out_rgb8, rt_stats* stats) {
+    std::string why;
+    if (!m || !cam || !out_rgb8) return fail(RT_E_INVALID, "multi, camera and out_rgb8 must be non-NULL");
+    if (!valid_params(p, why)) return fail(RT_E_INVALID, why);
+    if (p->flags & RT_ADAPTIVE) return fail(RT_E_INVALID, "rt_render_multi renders engine_mode::single frames (no RT_ADAPTIVE)");
+    return guard(RT_E_DEVICE, [&] {
+        art::RenderStats st;
+        m->renderer->render(camera_of(cam), render_params(p), out_rgb8, (p->flags & RT_OUT_DEVICE) != 0, st);
+        fill_stats(st, stats);
         return RT_OK;
     });
 }

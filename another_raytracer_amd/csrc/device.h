@@ -91,6 +91,14 @@ __device__ __forceinline__ R uniform(uint64_t& s) {
     return static_cast<R>(x >> 8) * static_cast<R>(1.0 / 16777216.0);
 }
 template <class R> __device__ __forceinline__ R uniform(uint64_t& s, R lo, R hi) { return lo + (hi - lo) * uniform<R>(s); }
+// The 24-bit integer k of the next uniform (uniform<R> == k * 2^-24): indexes DevScene::log_tab.
+__device__ __forceinline__ uint32_t uniform_k(uint64_t& s) {
+    const uint64_t old = s;
+    s = old * 6364136223846793005ull + 1442695040888963407ull;
+    const uint32_t xs = static_cast<uint32_t>(((old >> 18u) ^ old) >> 27u);
+    const uint32_t rot = static_cast<uint32_t>(old >> 59u);
+    return ((xs >> rot) | (xs << ((32u - rot) & 31u))) >> 8;
+}
 // uniform(s, -1, 1) = -1 + 2 * (k * 2^-24) with k < 2^24: every step is exact, so the single fma k * 2^-23 - 1 is the
 // same value
 template <class R>
@@ -218,6 +226,7 @@ struct DevScene {
     const ImageRec* images;
     const uint8_t* texels;
     const uint8_t* lds_image;   // layout.h LDS scene image (nullptr unless the scene qualifies)
+    const double* log_tab;      // scenes with media: log_tab[k] = the C library's log(k * 2^-24), k < 2^24 (hit_medium)
     int32_t nworld;
     R bg[3];
 };
@@ -557,6 +566,19 @@ struct LaneStack<B, false> {  // 32-bit entries
 };
 // Traversal stack entry: node/leaf codes, 16 bits in the LDS-scene variant (layout.h lds_leaf), 32 bits otherwise.
 template <bool L> using StackT = typename std::conditional<L, int16_t, int32_t>::type;
+#ifndef ART_STACK_SWZ
+#define ART_STACK_SWZ 1
+#endif
+// Column of lane t in a stack row.  16-bit entries pack two lanes per dword; a row holds a wave's 64 entries in 32
+// dwords.  Unswizzled, lanes 2i and 2i+1 share dword i, so a wave64 LDS access (serviced as lanes 0-31, then 32-63)
+// puts two lanes on one bank whenever their stack depths differ (a 2-way conflict on most pushes and pops of a
+// divergent traversal).  Swizzled, lane t sits in dword t & 31, half t >> 5: lanes 0-31 take 32 distinct dwords, and
+// so do lanes 32-63, in every row (rows are 2 KiB = 512 dwords apart, a multiple of the 64 banks).
+template <bool L>
+__device__ __forceinline__ uint32_t stack_column(uint32_t t) {
+    if (!L || !ART_STACK_SWZ) return t;
+    return (t & ~63u) | ((t & 31u) << 1) | ((t >> 5) & 1u);
+}
 
 // B: lanes per block (LDS stack stride).  L: nodes and leaf spheres come from the LDS scene image at `lds`.
 template <class R, uint32_t F, int B, bool L>
@@ -835,7 +857,11 @@ __device__ __forceinline__ bool hit_medium(const DevScene<R>& S, const uint8_t* 
     if (t1 < R(0)) t1 = R(0);
     const R ray_length = sqrt_rn(len2(r.d));
     const R inside = (t2 - t1) * ray_length;
-    const R hit_distance = m.p[0] * log(uniform<R>(rng));
+    // log(random_double()) of constant_medium.h:61 is the C library's log (glibc) in the reference; the device's own
+    // f64 log differs from it in the last bit for 445 762 of the 2^24 arguments a uniform can take (tools/log_check),
+    // which moves a scattering path's t and every sum after it.  The uniform's integer k indexes a table of glibc's
+    // values built on the host (build_device_scene), so every draw gives the reference's bits.
+    const R hit_distance = m.p[0] * S.log_tab[uniform_k(rng)];
     if (hit_distance > inside) return false;
     t = t1 + hit_distance / ray_length;
     return true;

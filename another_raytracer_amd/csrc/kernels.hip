@@ -19,8 +19,12 @@
 
 #include <algorithm>
 #include <functional>
+#include <map>
+#include <mutex>
+#include <tuple>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <type_traits>
@@ -500,7 +504,7 @@ __global__ __launch_bounds__(L ? kBlockL : kBlock, L ? 1 : ART_EXTEND_MIN_WAVES)
     uint32_t* pre = reinterpret_cast<uint32_t*>(smem + extend_pre_offset(L, g.stack));
     const uint8_t* lds = smem;
     // row 0 of the stack region is this lane's sentinel (device.h traverse), entries start at row 1
-    StackT<L>* stk = reinterpret_cast<StackT<L>*>(smem + (L ? kLdsImageBytes : 0u)) + B + threadIdx.x;
+    StackT<L>* stk = reinterpret_cast<StackT<L>*>(smem + (L ? kLdsImageBytes : 0u)) + B + stack_column<L>(threadIdx.x);
     stk[-B] = static_cast<StackT<L>>(kNodeEmpty);
 
     // input: depth 0 = every slot (identity; padding slots are skipped), deeper = the kShards active shards
@@ -640,7 +644,7 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S, PassGe
     // they pin ~60 SGPRs, which spill)
     extern __shared__ __align__(16) uint8_t smem[];
     const uint8_t* lds = smem;
-    StackT<true>* stk = reinterpret_cast<StackT<true>*>(smem + kLdsImageBytes) + B + threadIdx.x;
+    StackT<true>* stk = reinterpret_cast<StackT<true>*>(smem + kLdsImageBytes) + B + stack_column<true>(threadIdx.x);
     JumpEntry* jt = reinterpret_cast<JumpEntry*>(smem + kLdsImageBytes + paths_stack_bytes(g.stack));
     CameraRec<double>& s_cam = *reinterpret_cast<CameraRec<double>*>(smem + kLdsImageBytes + paths_stack_bytes(g.stack) + kJumpBytes);
     PassGeom& s_g = *reinterpret_cast<PassGeom*>(smem + kLdsImageBytes + paths_stack_bytes(g.stack) + kJumpBytes + sizeof(CameraRec<double>));
@@ -742,6 +746,12 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S, PassGe
 #ifndef ART_PATHS_G_WAVES
 #define ART_PATHS_G_WAVES 3  // 3 waves per SIMD (<= 168 VGPRs): measured best over 2 and 4 (cow +22 %, final +18 %, dino +21 % over 2)
 #endif
+#ifdef ART_TRACE
+// Path tracing diagnostics (libart_trace.so builds only): ART_TRACE="pixel:sample" prints every segment of that one
+// path from k_paths_g as bit patterns, in the format of the oracle's ORC_TRACE, so the two can be diffed.
+__device__ long long g_trace_pixel = -1, g_trace_sample = -1;
+#define ART_DBITS(x) static_cast<unsigned long long>(__double_as_longlong(x))
+#endif
 template <uint32_t F, uint32_t TF>
 __global__ __launch_bounds__(kBlock, ART_PATHS_G_WAVES) void k_paths_g(DevScene<double> S, PassGeom g, CameraRec<double> cam, Work<double> w, uint32_t* next_slot) {
     using R = double;
@@ -758,6 +768,9 @@ __global__ __launch_bounds__(kBlock, ART_PATHS_G_WAVES) void k_paths_g(DevScene<
     int depth = 0;
     PathState<R> st;
     unsigned long long segs = 0;
+#ifdef ART_TRACE
+    bool tracing = false;
+#endif
     for (;;) {
         const uint64_t idle = __ballot(!busy && !drained);
         if (idle) {
@@ -786,6 +799,10 @@ __global__ __launch_bounds__(kBlock, ART_PATHS_G_WAVES) void k_paths_g(DevScene<
                         gen_ray(g, cam, q, lx, ly, st);
                         busy = true;
                         depth = 0;
+#ifdef ART_TRACE
+                        tracing = static_cast<long long>(global_row(g, ly)) * g.W + lx == g_trace_pixel &&
+                                  static_cast<long long>(g.sample_base + g.fd_npix.div(slot)) == g_trace_sample;
+#endif
                     }
                 }
             }
@@ -799,9 +816,21 @@ __global__ __launch_bounds__(kBlock, ART_PATHS_G_WAVES) void k_paths_g(DevScene<
             HitOut h{0, 0, kMatUnknown};
             ++segs;
             bool cont = false;
+#ifdef ART_TRACE
+            if (tracing)
+                printf("TRACE d=%d o=%016llx,%016llx,%016llx dir=%016llx,%016llx,%016llx tm=%016llx rng=%016llx\n", depth, ART_DBITS(st.ray.o.x),
+                       ART_DBITS(st.ray.o.y), ART_DBITS(st.ray.o.z), ART_DBITS(st.ray.d.x), ART_DBITS(st.ray.d.y), ART_DBITS(st.ray.d.z),
+                       ART_DBITS(st.ray.tm), static_cast<unsigned long long>(st.rng));
+#endif
             if (trace_world<R, F, B, false>(S, nullptr, st.ray, stk, st.rng, t, h)) {
                 Surf<R> s;
                 world_surface<R, F, (TF & TF_IMAGE) != 0>(S, h, st.ray, t, s);
+#ifdef ART_TRACE
+                if (tracing)
+                    printf("TRACE hit t=%016llx p=%016llx,%016llx,%016llx n=%016llx,%016llx,%016llx ff=%d mat=%d prim=%08x obj=%08x\n", ART_DBITS(t),
+                           ART_DBITS(s.p.x), ART_DBITS(s.p.y), ART_DBITS(s.p.z), ART_DBITS(s.n.x), ART_DBITS(s.n.y), ART_DBITS(s.n.z), s.ff ? 1 : 0,
+                           static_cast<int>(s.mat), h.prim, h.obj);
+#endif
                 const MatRec<R>& mat = S.mats[s.mat];
                 if (mat.type == MAT_LIGHT) {  // material.h:114-116; diffuse_light never scatters
                     st.L = st.L + st.T * tex_value<R, TF>(S, mat.tex, s.u, s.v, s.p);
@@ -823,6 +852,9 @@ __global__ __launch_bounds__(kBlock, ART_PATHS_G_WAVES) void k_paths_g(DevScene<
                     }
                 }
             } else {  // engine.h:455-456: miss -> background
+#ifdef ART_TRACE
+                if (tracing) printf("TRACE miss\n");
+#endif
                 st.L = st.L + st.T * bg;
             }
             if (cont) {
@@ -1192,6 +1224,17 @@ static std::vector<uint8_t> lds_scene_image(const FlatScene& f, uint32_t& nmov, 
     return img;
 }
 
+// glibc's log of every uniform the RNG contract can produce, (k * 2^-24) for k < 2^24 (device.h hit_medium): 128 MiB,
+// computed once per process on first use by a scene with media and uploaded once per device.
+static const std::vector<double>& log_table() {
+    static const std::vector<double> tab = [] {
+        std::vector<double> t(size_t(1) << 24);
+        for (size_t k = 0; k < t.size(); ++k) t[k] = std::log(static_cast<double>(k) * (1.0 / 16777216.0));
+        return t;
+    }();
+    return tab;
+}
+
 template <class R>
 static void build_device_scene(const FlatScene& f, DeviceScene<R>& ds) {
     std::vector<SphereRec<R>> sph(f.spheres.size());
@@ -1260,6 +1303,7 @@ static void build_device_scene(const FlatScene& f, DeviceScene<R>& ds) {
             ds.lds_shade = shade_ok;
         }
     }
+    if (f.has_media) ds.view.log_tab = ds.upload(log_table());
     ds.view.nworld = static_cast<int32_t>(f.world.size());
     for (int a = 0; a < 3; ++a) ds.view.bg[a] = R(f.background[a]);
     ds.media = f.has_media;
@@ -1277,26 +1321,42 @@ struct Renderer::Impl {
     int num_cu = 256;
     hipStream_t own_stream = nullptr;
     FlatScene flat;
-    DeviceScene<float> s32;
     DeviceScene<double> s64;
-    bool up32 = false, up64 = false;
+    bool up64 = false;
     // workspace (grow-only)
     void* ws = nullptr;
     size_t ws_bytes = 0;
     hipEvent_t ev[2] = {nullptr, nullptr};
 
     ~Impl() {
-        s32.release();
         s64.release();
         if (ws) (void)hipFree(ws);
         for (auto& e : ev) if (e) (void)hipEventDestroy(e);
         if (own_stream) (void)hipStreamDestroy(own_stream);
     }
+    // Grow-only workspace.  The old buffer is released before the larger one is allocated (both need not fit), and
+    // ws / ws_bytes describe a live allocation at every point: a failed hipMalloc leaves them at {nullptr, 0}, so the
+    // next render allocates again instead of handing out offsets from a null base.
     void* workspace(size_t bytes) {
+        // fault injection (tests): ART_FAULT_WORKSPACE_BYTES=N makes every workspace growth beyond N bytes fail as a
+        // refused hipMalloc would, after the old buffer is released
+        const char* lim = std::getenv("ART_FAULT_WORKSPACE_BYTES");
         if (bytes > ws_bytes) {
-            if (ws) HIP_OK(hipFree(ws));
-            ws = nullptr;
-            HIP_OK(hipMalloc(&ws, bytes));
+            if (lim && bytes > std::strtoull(lim, nullptr, 10)) {
+                if (ws) (void)hipFree(ws);
+                ws = nullptr;
+                ws_bytes = 0;
+                throw std::runtime_error("workspace allocation of " + std::to_string(bytes) + " bytes refused (ART_FAULT_WORKSPACE_BYTES)");
+            }
+            if (ws) {
+                void* old = ws;
+                ws = nullptr;
+                ws_bytes = 0;
+                HIP_OK(hipFree(old));
+            }
+            void* p = nullptr;
+            HIP_OK(hipMalloc(&p, bytes));
+            ws = p;
             ws_bytes = bytes;
         }
         return ws;
@@ -1318,9 +1378,7 @@ Renderer::~Renderer() {
         delete impl_;
     }
 }
-size_t Renderer::scene_bytes(int fp) const {
-    return fp == RT_FP64 ? impl_->s64.bytes : impl_->s32.bytes;
-}
+size_t Renderer::scene_bytes() const { return impl_->s64.bytes; }
 const FlatScene& Renderer::flat() const { return impl_->flat; }
 
 #endif
@@ -1332,20 +1390,35 @@ static bool static_lds_is_zero(const void* kernel) {
     if (a.sharedSizeBytes != 0) throw std::runtime_error("LDS-scene kernel has static LDS: the scene image would not start at address 0");
     return true;
 }
-#if ART_SPLIT_PATHS != 2
-// Persistent extend grid for a given dynamic LDS size: every block the CUs can hold at once.
-template <class R, uint32_t F, bool L, bool FUSE>
-static int extend_blocks(int num_cu, size_t lds) {
+// Launch configuration per (kernel, device, dynamic LDS bytes): the > 64 KiB dynamic-LDS attribute, which
+// hipFuncSetAttribute records per device, and the blocks per CU of a persistent grid (every block the CUs hold at
+// once).  Scenes on different devices may render from different host threads, so the cache is
+// mutex-guarded instead of living in function-local statics shared by all devices.
+struct LaunchKey {
+    const void* kernel;
+    int device;
+    size_t lds;
+    bool operator<(const LaunchKey& o) const { return std::tie(kernel, device, lds) < std::tie(o.kernel, o.device, o.lds); }
+};
+static int blocks_per_cu(const void* kernel, int block, size_t lds) {
+    static std::mutex mtx;
+    static std::map<LaunchKey, int> cache;
+    int dev = 0;
+    HIP_OK(hipGetDevice(&dev));
+    const LaunchKey key{kernel, dev, lds};
+    std::lock_guard<std::mutex> lock(mtx);
+    const auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    if (lds > 64 * 1024) HIP_OK(hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_extend<R, F, L, FUSE>, L ? kBlockL : kBlock, lds) != hipSuccess || per_cu < 1)
-        per_cu = 1;
-    return per_cu * num_cu;  // num_cu (256) is a multiple of 8: the wave count is a multiple of kShards
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, lds) != hipSuccess || per_cu < 1) per_cu = 1;
+    cache.emplace(key, per_cu);
+    return per_cu;
 }
+#if ART_SPLIT_PATHS != 2
 template <class R, uint32_t F, uint32_t M, uint32_t TF>
 static int shade_blocks(int num_cu) {
-    static int per_cu = 0;
-    if (!per_cu && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_shade<R, F, M, TF>, kBlock, 0) != hipSuccess || per_cu < 1)) per_cu = 2;
-    return per_cu * num_cu;
+    return blocks_per_cu(reinterpret_cast<const void*>(k_shade<R, F, M, TF>), kBlock, 0) * num_cu;
 }
 // Textured materials get the "solid + checker" instantiation unless the scene holds noise or image textures.
 template <class R, uint32_t F, uint32_t M>
@@ -1365,15 +1438,8 @@ static void launch_extend(int num_cu, hipStream_t st, const DevScene<R>& S, cons
     const size_t lds = extend_lds_bytes(L, g.stack);
     static const bool checked = !L || static_lds_is_zero(reinterpret_cast<const void*>(k_extend<R, F, L, FUSE>));
     (void)checked;
-    static int blocks = 0;
-    static size_t blocks_lds = ~size_t(0);
-    if (lds != blocks_lds) {
-        if (lds > 64 * 1024)
-            HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_extend<R, F, L, FUSE>), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       static_cast<int>(lds)));
-        blocks = extend_blocks<R, F, L, FUSE>(num_cu, lds);
-        blocks_lds = lds;
-    }
+    // num_cu (256) is a multiple of 8: the wave count is a multiple of kShards
+    const int blocks = blocks_per_cu(reinterpret_cast<const void*>(k_extend<R, F, L, FUSE>), L ? kBlockL : kBlock, lds) * num_cu;
     hipLaunchKernelGGL((k_extend<R, F, L, FUSE>), dim3(blocks), dim3(L ? kBlockL : kBlock), lds, st, S, g, cam, w, d);
 }
 // Extend variant: 0 = HBM scene, 1 = LDS scene, 2 = LDS scene with fused shading (no k_shade launches), 3 = persistent
@@ -1416,14 +1482,7 @@ template <uint32_t F, uint32_t TF>
 static void launch_paths_g_ft(int num_cu, hipStream_t st, const DevScene<double>& S, const PassGeom& g, const CameraRec<double>& cam,
                               const Work<double>& w, uint32_t* next_slot) {
     const size_t lds = sizeof(int32_t) * g.stack * kBlock;  // stack_rows: sentinel + entries + spare row
-    static int blocks = 0;
-    static size_t blocks_lds = ~size_t(0);
-    if (lds != blocks_lds) {  // a persistent grid: exactly the blocks the CUs hold at once
-        int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_paths_g<F, TF>, kBlock, lds) != hipSuccess || per_cu < 1) per_cu = 1;
-        blocks = per_cu * num_cu;
-        blocks_lds = lds;
-    }
+    const int blocks = blocks_per_cu(reinterpret_cast<const void*>(k_paths_g<F, TF>), kBlock, lds) * num_cu;
     hipLaunchKernelGGL((k_paths_g<F, TF>), dim3(blocks), dim3(kBlock), lds, st, S, g, cam, w, next_slot);
 }
 static void launch_paths_g(uint32_t feat, bool tex_basic, int num_cu, hipStream_t st, const DevScene<double>& S, const PassGeom& g,
@@ -1448,13 +1507,9 @@ static void launch_paths_g(uint32_t feat, bool tex_basic, int num_cu, hipStream_
 ART_PATHS_LINKAGE void launch_paths(int num_cu, hipStream_t st, const DevScene<double>& S, const PassGeom& g, const CameraRec<double>& cam,
                          const Work<double>& w, uint32_t* next_slot) {
     const size_t lds = paths_lds_bytes(g.stack);
-    static size_t attr_lds = 0;
     static const bool checked = static_lds_is_zero(reinterpret_cast<const void*>(k_paths));
     (void)checked;
-    if (lds > 64 * 1024 && lds != attr_lds) {
-        HIP_OK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_paths), hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
-        attr_lds = lds;
-    }
+    (void)blocks_per_cu(reinterpret_cast<const void*>(k_paths), kBlockL, lds);  // the LDS attribute; the grid is one block per CU
     hipLaunchKernelGGL(k_paths, dim3(num_cu), dim3(kBlockL), lds, st, S, g, cam, w, next_slot);
 }
 #else
@@ -1519,12 +1574,18 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     size_t free_b = 0, total_b = 0;
     HIP_OK(hipMemGetInfo(&free_b, &total_b));
     const uint64_t target = std::min<uint64_t>((free_b + I.ws_bytes) / 2 / slot_bytes, kMaxPassSlots);  // fixed point: no regrowth
-    uint32_t k = p.samples_per_pass > 0 ? static_cast<uint32_t>(p.samples_per_pass)
-                                        : static_cast<uint32_t>(std::max<uint64_t>(1, target / g.npix_pad));
-    k = std::min<uint32_t>(k, static_cast<uint32_t>(p.spp));
+    // Slot ids, FastDiv operands and shard capacities are u32 and exact below 2^31: a pass never holds more than
+    // kMaxPassSlots slots, whether k comes from free memory or from the caller's samples_per_pass.
+    if (g.npix_pad > kMaxPassSlots) throw std::runtime_error("image too large for one pass (more than 2^31 padded pixels)");
+    const uint64_t k_cap = std::max<uint64_t>(1, kMaxPassSlots / g.npix_pad);
+    uint64_t k64 = p.samples_per_pass > 0 ? static_cast<uint64_t>(p.samples_per_pass) : std::max<uint64_t>(1, target / g.npix_pad);
+    k64 = std::min<uint64_t>(std::min<uint64_t>(k64, k_cap), static_cast<uint64_t>(p.spp));
+    uint32_t k = static_cast<uint32_t>(k64);
     const int npasses = static_cast<int>((p.spp + k - 1) / k);
     k = static_cast<uint32_t>((p.spp + npasses - 1) / npasses);
-    const uint32_t Pmax = k * g.npix_pad;
+    const uint64_t Pmax64 = static_cast<uint64_t>(k) * g.npix_pad;
+    if (Pmax64 > kMaxPassSlots) throw std::runtime_error("internal: pass larger than 2^31 slots");
+    const uint32_t Pmax = static_cast<uint32_t>(Pmax64);
     g.cap = shard_cap(Pmax);
     const int depth_slots = p.max_depth + 1;
     const size_t local_pix = static_cast<size_t>(nrows) * p.width;
@@ -1593,6 +1654,8 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     auto mark = [&]() { HIP_OK(hipEventRecord(evs[ev_next++], stream)); };
     int passes_run = 0;
     uint64_t ext_launches = 0;
+    int spp_done = 0;      // samples traced so far (progressive snapshots)
+    bool stopped = false;  // the progressive callback ended the render early
     // Traces spp samples of every local pixel (list == nullptr) or of every entry of a device pixel list, into
     // w.acc (per local pixel, or per list entry).
     auto trace = [&](const uint32_t* list, uint32_t nlist) {
@@ -1612,8 +1675,10 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
             g.P = g.k * g.npix_pad;
             g.live = g.k * npix;
             HIP_OK(hipMemsetAsync(w.counters, 0, 4ull * cnt_words, stream));
+            bool persistent = false;
             if constexpr (std::is_same<R, double>::value) {
                 if (mega) {
+                    persistent = true;
                     if (p.max_depth > 0) {
                         if (prof) mark();
                         if (variant == EXT_MEGA) launch_paths(I.num_cu, stream, ds.view, g, cam, w, counter(w, 0, 0, 0));
@@ -1621,18 +1686,38 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
                         if (prof) { mark(); mark(); }
                         ++ext_launches;
                     }
-                    hipLaunchKernelGGL(k_accum<R>, dim3((g.npix_pad + 255) / 256), dim3(256), 0, stream, g, w);
-                    ++passes_run;
-                    continue;
                 }
             }
-            for (int d = 0; d < p.max_depth; ++d)
-                bounce<R>(ds, variant, I.num_cu, stream, g, cam, w, d, prof ? std::function<void()>(mark) : std::function<void()>());
-            ext_launches += static_cast<uint64_t>(p.max_depth);
+            if (!persistent) {
+                for (int d = 0; d < p.max_depth; ++d)
+                    bounce<R>(ds, variant, I.num_cu, stream, g, cam, w, d, prof ? std::function<void()>(mark) : std::function<void()>());
+                ext_launches += static_cast<uint64_t>(p.max_depth);
+            }
             hipLaunchKernelGGL(k_accum<R>, dim3((g.npix_pad + 255) / 256), dim3(256), 0, stream, g, w);
             ++passes_run;
+            spp_done = static_cast<int>(sb + g.k);
+            // progressive snapshot (whole-image traces only): write_color of the sums so far, with the samples so far
+            if (!list && p.on_pass) {
+                hipLaunchKernelGGL(k_finalize, dim3((npix + 255) / 256), dim3(256), 0, stream, w.acc, drgb, npix, spp_done);
+                const hipMemcpyKind kind = (p.flags & RT_OUT_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+                if (out_rgb) HIP_OK(hipMemcpyAsync(out_rgb, drgb, 3ull * npix, kind, stream));
+                if (out_acc) HIP_OK(hipMemcpyAsync(out_acc, w.acc, sizeof(double) * 3 * npix, kind, stream));
+                HIP_OK(hipStreamSynchronize(stream));
+                if (!p.on_pass(spp_done)) {
+                    stopped = true;
+                    break;
+                }
+            }
         }
     };
+#ifdef ART_TRACE
+    {
+        long long tp = -1, ts = -1;
+        if (const char* t = std::getenv("ART_TRACE")) std::sscanf(t, "%lld:%lld", &tp, &ts);
+        HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(g_trace_pixel), &tp, sizeof tp));
+        HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(g_trace_sample), &ts, sizeof ts));
+    }
+#endif
     HIP_OK(hipEventRecord(I.ev[0], stream));
     HIP_OK(hipMemsetAsync(w.segments, 0, sizeof(unsigned long long), stream));
     if (p.max_depth == 0) HIP_OK(hipMemsetAsync(w.res, 0, sizeof(ResRec<R>) * Pmax, stream));  // engine.h:451-452
@@ -1640,7 +1725,7 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     if (!adaptive) {
         trace(nullptr, 0);
         const uint32_t npix = static_cast<uint32_t>(local_pix);
-        hipLaunchKernelGGL(k_finalize, dim3((npix + 255) / 256), dim3(256), 0, stream, w.acc, drgb, npix, p.spp);
+        hipLaunchKernelGGL(k_finalize, dim3((npix + 255) / 256), dim3(256), 0, stream, w.acc, drgb, npix, stopped ? spp_done : p.spp);
     } else {
         // engine.h:151-333: levels 0..3 (k_adapt_* above); the list sizes come back to the host between levels
         const int sqx = p.width / kBig;
@@ -1695,7 +1780,7 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     stats.samples_per_pass = static_cast<int>(k);
     stats.segments = segs;
     stats.extend_variant = variant;
-    stats.primary = traced * static_cast<uint64_t>(p.spp);
+    stats.primary = traced * static_cast<uint64_t>(stopped ? spp_done : p.spp);
     if (prof) {
         double ext_ms = 0, sh_ms = 0;
         for (size_t e = 0; e + 2 < ev_next; e += 3) {
@@ -1715,13 +1800,9 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
 
 void Renderer::render(const CameraRec<double>& cam, const RenderParams& p, uint8_t* out_rgb, double* out_acc, RenderStats& stats) {
     HIP_OK(hipSetDevice(impl_->device));
-    if (p.fp_mode == RT_FP64) {
-        if (!impl_->up64) { build_device_scene(impl_->flat, impl_->s64); impl_->up64 = true; }
-        render_impl<double>(*impl_, impl_->s64, cam, p, out_rgb, out_acc, stats);
-    } else {
-        if (!impl_->up32) { build_device_scene(impl_->flat, impl_->s32); impl_->up32 = true; }
-        render_impl<float>(*impl_, impl_->s32, cam, p, out_rgb, out_acc, stats);
-    }
+    if (p.fp_mode != RT_FP64) throw std::runtime_error("fp_mode must be RT_FP64");
+    if (!impl_->up64) { build_device_scene(impl_->flat, impl_->s64); impl_->up64 = true; }
+    render_impl<double>(*impl_, impl_->s64, cam, p, out_rgb, out_acc, stats);
 }
 
 #endif  // ART_SPLIT_PATHS != 2

@@ -1,6 +1,7 @@
 // renderer.h — host-side device renderer (implemented in kernels.hip; no HIP types in this header).
 #pragma once
 #include <cstdint>
+#include <functional>
 
 #include "art.h"
 #include "layout.h"
@@ -11,12 +12,16 @@ namespace art {
 struct RenderParams {
     int width = 0, height = 0, spp = 1, max_depth = 50;
     uint64_t seed = 0;
-    int fp_mode = RT_FP32;
+    int fp_mode = RT_FP64;
     int band_rows = 1, band_count = 1, band_index = 0;
     int samples_per_pass = 0;
     int flags = 0;
     void* stream = nullptr;
     double background[3] = {0, 0, 0};
+    // Progressive rendering (whole-image traces): called after every pass with the samples traced so far, once the
+    // frame write_color'ed with that count (and the sums, when requested) are in the caller's buffers; returning
+    // false ends the render there.
+    std::function<bool(int samples_done)> on_pass;
 };
 
 struct RenderStats {
@@ -35,7 +40,7 @@ public:
     Renderer(const Renderer&) = delete;
     Renderer& operator=(const Renderer&) = delete;
     void render(const CameraRec<double>& cam, const RenderParams& p, uint8_t* out_rgb, double* out_acc, RenderStats& stats);
-    size_t scene_bytes(int fp_mode) const;
+    size_t scene_bytes() const;
     const FlatScene& flat() const;
 
 private:

@@ -1,4 +1,8 @@
-"""Multi-GPU frame rendering: one process per GPU (torch.distributed over RCCL), row-interleaved bands, one gather.
+"""Multi-GPU frame rendering, two drivers of the same partition (row-interleaved bands, one RCCL gather):
+
+* one process per GPU (torch.distributed over RCCL; bench.py under torchrun): render_frame / gather_frame below;
+* one process, one host thread per GPU, RCCL inside libart (rt_render_multi, include/art.h): multi_engine below.
+
 
 The reference splits an image into 4 contiguous row stripes on 4 threads (engine.h:335-376).  Here rank r of N
 renders every global row y with (y // band_rows) % N == r (band_rows = 16: sky rows are cheap and object rows
@@ -6,22 +10,26 @@ expensive, so interleaving balances the load), packs its rows contiguously, and 
 blocks (RCCL over xGMI; the only collective of the path) and un-interleaves them.  Every pixel's RNG stream is keyed
 by (seed, global pixel, sample), so the gathered image is bit-identical to a single-GPU render (tests/).
 """
+import ctypes
+
+import numpy as np
 import torch
 import torch.distributed as dist
+
+from ._lib import RT_OUT_DEVICE, check, lib, rt_params, rt_stats
 
 DEFAULT_BAND_ROWS = 16
 
 
 def band_rows_of(height, band_rows, band_count, band_index):
-    """Global row indices owned by one band partition (same rule as rt_local_rows / kernels.hip global_row)."""
-    rows = []
-    ly = 0
-    while True:
-        gy = (ly // band_rows) * (band_rows * band_count) + band_index * band_rows + (ly % band_rows)
-        if gy >= height:
-            return rows
-        rows.append(gy)
-        ly += 1
+    """Global row indices owned by one band partition: libart's own rule (rt_local_rows, the kernels' global_row)."""
+    p = rt_params()
+    p.width, p.height = 2, int(height)
+    p.band_rows, p.band_count, p.band_index = int(band_rows), int(band_count), int(band_index)
+    n = check(lib.rt_local_rows(ctypes.byref(p), None), "rt_local_rows")
+    rows = (ctypes.c_int32 * max(n, 1))()
+    lib.rt_local_rows(ctypes.byref(p), rows)
+    return list(rows[:n])
 
 
 def gather_frame(local, height, band_rows, group=None, dst=0):
@@ -61,3 +69,51 @@ def render_frame(eng, band_rows=DEFAULT_BAND_ROWS, group=None, dst=0, device=Non
     if world == 1:
         return local, stats
     return gather_frame(local, eng.height, band_rows, group=group, dst=dst), stats
+
+
+class multi_engine:
+    """The engine surface over rt_render_multi: one process drives `devices` (one host thread and one RCCL rank per
+    GPU), each GPU renders the bands b with b % len(devices) == its index, and one ncclGather assembles the frame on
+    devices[0].  `scene` is a builtin scene name (scene_manager names) or a hittable_list built in Python."""
+
+    def __init__(self, scene, devices, cam, width, height, samples_per_pixel, max_depth=50, seed=0,
+                 band_rows=DEFAULT_BAND_ROWS, background=None, asset_dir=None):
+        from .scene import ASSET_DIR, _g
+        self.devices = [int(d) for d in devices]
+        self.cam, self.width, self.height = cam, int(width), int(height)
+        self.samples_per_pixel, self.max_depth, self.seed, self.band_rows = int(samples_per_pixel), int(max_depth), int(seed), int(band_rows)
+        devs = (ctypes.c_int * len(self.devices))(*self.devices)
+        self._m = ctypes.c_void_p()
+        if isinstance(scene, str):
+            check(lib.rt_multi_create(scene.encode(), (asset_dir or ASSET_DIR).encode(), devs, len(self.devices),
+                                      ctypes.byref(self._m)), "rt_multi_create")
+        else:
+            g = _g()
+            check(lib.rt_graph_clear_world(g), "rt_graph_clear_world")
+            for o in scene.objects:
+                check(lib.rt_graph_add_world(g, o.id), "rt_graph_add_world")
+            check(lib.rt_multi_from_graph(g, devs, len(self.devices), ctypes.byref(self._m)), "rt_multi_from_graph")
+        self.background = tuple(background) if background is not None else (0.0, 0.0, 0.0)
+        self.stats = {}
+
+    def run(self, out):
+        """Renders the whole frame into `out` (uint8 H x W x 3: numpy, or a torch tensor on devices[0]); returns ms."""
+        from .engine import _pointer
+        p = rt_params()
+        p.width, p.height, p.spp, p.max_depth, p.seed = self.width, self.height, self.samples_per_pixel, self.max_depth, self.seed
+        p.band_rows, p.band_count, p.band_index = self.band_rows, 1, 0
+        for c in range(3):
+            p.background[c] = self.background[c]
+        ptr, dev = _pointer(out, self.width * self.height * 3)
+        if dev:
+            p.flags |= RT_OUT_DEVICE
+        st = rt_stats()
+        check(lib.rt_render_multi(self._m, ctypes.byref(self.cam.c), ctypes.byref(p), ctypes.c_void_p(ptr), ctypes.byref(st)),
+              "rt_render_multi")
+        self.stats = st.as_dict()
+        return st.ms
+
+    def __del__(self):
+        if getattr(self, "_m", None) and self._m.value and lib is not None:
+            lib.rt_multi_destroy(self._m)
+            self._m = None

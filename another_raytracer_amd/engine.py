@@ -10,7 +10,7 @@ import enum
 
 import numpy as np
 
-from ._lib import RT_ADAPTIVE, RT_FP32, RT_FP64, RT_GLOBAL_SCENE, RT_OUT_DEVICE, RT_PROFILE, RT_SPLIT_SHADE, RT_WAVEFRONT, check, dvec, lib, rt_camera, rt_params, rt_stats
+from ._lib import RT_ADAPTIVE, RT_FP64, rt_progress_fn, RT_GLOBAL_SCENE, RT_OUT_DEVICE, RT_PROFILE, RT_SPLIT_SHADE, RT_WAVEFRONT, check, dvec, lib, rt_camera, rt_params, rt_stats
 from .scene import compile_world
 
 
@@ -59,8 +59,8 @@ class engine:
         self.width, self.height = int(width), int(height)
         self.samples_per_pixel, self.max_depth = int(samples_per_pixel), int(max_depth)
         self.device, self.seed = int(device), int(seed)
-        if precision not in ("f32", "f64"):
-            raise ValueError("precision must be 'f32' or 'f64'")
+        if precision != "f64":
+            raise ValueError("precision must be 'f64': the reference's double arithmetic is the only mode (ABI 2)")
         self.precision = precision
         self.samples_per_pass = int(samples_per_pass)
         # True forces the global-memory extend kernel even when the scene fits the LDS-resident variant (A/B, tests)
@@ -83,7 +83,7 @@ class engine:
         p = rt_params()
         p.width, p.height = self.width, self.height
         p.spp, p.max_depth, p.seed = self.samples_per_pixel, self.max_depth, self.seed
-        p.fp_mode = RT_FP64 if self.precision == "f64" else RT_FP32
+        p.fp_mode = RT_FP64
         p.band_rows = band_rows or self.height
         p.band_count, p.band_index = band_count, band_index
         p.samples_per_pass, p.flags = self.samples_per_pass, flags
@@ -123,6 +123,45 @@ class engine:
         st = rt_stats()
         check(lib.rt_render(self._scene, ctypes.byref(self.cam.c), ctypes.byref(p), ctypes.c_void_p(ptr),
                             ctypes.c_void_p(acc_ptr) if acc_ptr else None, ctypes.byref(st)), "engine.run")
+        self.stats = st.as_dict()
+        return int(round(st.ms))
+
+    def run_progressive(self, output_image, callback, accum=None, samples_per_pass=0):
+        """Progressive render (rt_render_progressive): the frame is traced in passes of samples_per_pass samples
+        (0: spp / 8); after each pass callback(samples_done, spp) runs with output_image (and accum) holding the frame
+        of the samples so far.  A truthy return value stops the render.  Returns elapsed ms, or -1 on an empty world."""
+        if self._scene is None:
+            print("Invalid input scene!")
+            return -1
+        if self.m == engine_mode.adaptive:
+            raise ValueError("progressive rendering traces whole frames (engine_mode.adaptive is not progressive)")
+        p = self.params(None, 1, 0, 0, None)
+        p.samples_per_pass = int(samples_per_pass)
+        nbytes = self.height * self.width * 3
+        ptr, dev = _pointer(output_image, nbytes)
+        acc_ptr = None
+        if accum is not None:
+            acc_ptr, acc_dev = _pointer(accum.view(np.uint8) if isinstance(accum, np.ndarray) else accum, nbytes * 8)
+            if acc_dev != dev:
+                raise ValueError("output_image and accum must both live on the host or both on the device")
+        if dev:
+            p.flags |= RT_OUT_DEVICE
+        errors = []
+
+        def trampoline(_user, done, spp, _rgb, _acc):
+            try:
+                return 1 if callback(int(done), int(spp)) else 0
+            except BaseException as e:  # an exception must not unwind through the C frames: stop and re-raise after
+                errors.append(e)
+                return 1
+
+        cb = rt_progress_fn(trampoline)
+        st = rt_stats()
+        check(lib.rt_render_progressive(self._scene, ctypes.byref(self.cam.c), ctypes.byref(p), ctypes.c_void_p(ptr),
+                                        ctypes.c_void_p(acc_ptr) if acc_ptr else None, cb, None, ctypes.byref(st)),
+              "engine.run_progressive")
+        if errors:
+            raise errors[0]
         self.stats = st.as_dict()
         return int(round(st.ms))
 

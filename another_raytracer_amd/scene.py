@@ -258,8 +258,13 @@ class constant_medium(hittable):  # constant_medium.h
 
 
 def compile_world(world, device):
-    """hittable_list -> native rt_scene handle (c_void_p)."""
+    """hittable_list -> native rt_scene handle (c_void_p) on `device`.  A builtin scene's list is already compiled
+    for the device its scene_manager named: using it on another device is an error (rendering it there would run on
+    the scene's device and copy the frame across)."""
     if world._native is not None:
+        if world._native.device != int(device):
+            raise ValueError(f"this scene was built for device {world._native.device}, not {int(device)}: "
+                             f"build it with scene_manager(device={int(device)})")
         return world._native
     g = _g()
     check(lib.rt_graph_clear_world(g), "rt_graph_clear_world")
@@ -267,14 +272,15 @@ def compile_world(world, device):
         check(lib.rt_graph_add_world(g, o.id), "rt_graph_add_world")
     out = ctypes.c_void_p()
     check(lib.rt_graph_compile(g, int(device), ctypes.byref(out)), "rt_graph_compile")
-    return _SceneHandle(out)
+    return _SceneHandle(out, device)
 
 
 class _SceneHandle(ctypes.c_void_p):
-    """Owns an rt_scene*."""
+    """Owns an rt_scene* (and remembers the device it was built for)."""
 
-    def __init__(self, ptr):
+    def __init__(self, ptr, device=0):
         super().__init__(ptr.value if isinstance(ptr, ctypes.c_void_p) else ptr)
+        self.device = int(device)
 
     def __del__(self):
         if self.value and lib is not None:
@@ -313,7 +319,7 @@ class scene_manager:
         out = ctypes.c_void_p()
         check(lib.rt_scene_build(name.encode(), self.asset_dir.encode(), int(self.device), ctypes.byref(out)),
               f"scene_manager.build({alias})")
-        handle = _SceneHandle(out)
+        handle = _SceneHandle(out, self.device)
         info = rt_scene_info()
         check(lib.rt_scene_info_get(handle, ctypes.byref(info)), "rt_scene_info_get")
         s = scene(tuple(info.lookfrom), tuple(info.lookat), info.vfov, info.aperture, tuple(info.background),

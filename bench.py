@@ -70,7 +70,7 @@ def parse():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=1024)
     ap.add_argument("--max-depth", type=int, default=50)
-    ap.add_argument("--precision", default="f64", choices=["f32", "f64"])
+    ap.add_argument("--precision", default="f64", choices=["f64"])  # the reference's double (ABI 2: the only mode)
     ap.add_argument("--band-rows", type=int, default=16)
     ap.add_argument("--samples-per-pass", type=int, default=0)
     ap.add_argument("--no-profile", action="store_true", help="skip per-launch HIP events (no roofline)")
@@ -141,7 +141,7 @@ def main():
     from another_raytracer_amd.distributed import band_rows_of, render_frame
 
     world_scene = art.scene_manager(device=dev.index).build(args.scene)
-    scene_bytes = int(world_scene.info["device_bytes_f64" if args.precision == "f64" else "device_bytes_f32"])
+    scene_bytes = int(world_scene.info["device_bytes_f64"])
     cam = art.camera(world_scene.lookfrom, world_scene.lookat, (0, 1, 0), world_scene.vfov, args.width / args.height,
                      world_scene.aperture, 10.0, 0.0, 1.0)
     eng = art.engine(cam, art.engine_mode.parallel_stripes, width=args.width, height=args.height,

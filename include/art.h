@@ -36,7 +36,9 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+/* ABI 2: rt_params.fp_mode 0 = RT_FP64 (the only arithmetic: the reference's IEEE double), rt_scene_info's f32 byte count
+ * dropped, rt_multi_* (multi-GPU render over RCCL), rt_render_progressive, rt_scene_save / rt_scene_load, rt_image_load. */
+#define RT_ABI_VERSION 2
 
 /* return codes */
 #define RT_OK 0
@@ -45,9 +47,11 @@ extern "C" {
 #define RT_E_DEVICE (-3)    /* HIP runtime failure or no device */
 #define RT_E_INTERNAL (-4)
 
-/* rt_params.fp_mode: arithmetic of the leaf tests and shading (BVH box tests are always conservative f32) */
-#define RT_FP32 0
-#define RT_FP64 1
+/* rt_params.fp_mode: arithmetic of the leaf tests and shading.  RT_FP64 (= 0, so a zero-initialised rt_params gets it)
+ * is the reference's own IEEE double and the only mode: ABI 1's experimental RT_FP32 self-intersected on the
+ * reference's r = 1000 / r = 5000 spheres and is gone (any other value is RT_E_INVALID).  The BVH box tests are
+ * conservative f32 in every mode; they never decide a hit. */
+#define RT_FP64 0
 /* rt_params.flags */
 #define RT_OUT_DEVICE 1     /* out_rgb8 / out_accum are device pointers (on the scene's device) */
 #define RT_PROFILE 2        /* time every extend/shade launch with HIP events (rt_stats.*_ms) */
@@ -80,7 +84,7 @@ typedef struct rt_params {
     int32_t spp;                /* samples per pixel (tracer_constants.h:12) */
     int32_t max_depth;          /* bounce limit (tracer_constants.h:13; 50) */
     uint64_t seed;              /* render RNG seed */
-    int32_t fp_mode;            /* RT_FP32 | RT_FP64 */
+    int32_t fp_mode;            /* RT_FP64 (0) */
     int32_t band_rows;          /* row-interleaved partition: global row y belongs to band (y / band_rows) and */
     int32_t band_count;         /*   is rendered here when band % band_count == band_index; (H, 1, 0) = whole image */
     int32_t band_index;
@@ -108,7 +112,7 @@ typedef struct rt_scene_info {  /* scene_manager.h:6-14 */
     double background[3];
     int64_t spheres, triangles, rects, boxes, bvh_nodes, objects, materials, textures;
     int32_t has_media, max_bvh_depth;
-    uint64_t device_bytes_f32, device_bytes_f64;
+    uint64_t device_bytes_f64;  /* scene bytes uploaded to the device (0 before the first render) */
 } rt_scene_info;
 
 /* ---- library ---- */
@@ -133,8 +137,33 @@ void rt_scene_destroy(rt_scene* scene);
  * out_accum (optional): local_rows * width * 3 f64 radiance sums (pixel_color before write_color).  Host pointers
  * unless RT_OUT_DEVICE.  Blocking. */
 int rt_render(rt_scene* scene, const rt_camera* cam, const rt_params* params, uint8_t* out_rgb8, double* out_accum, rt_stats* stats);
+/* Progressive rendering: the headless replacement for the reference's live preview (dynamic_gui_impl refreshed after
+ * every row / square, gui.cpp:25-58, engine.h:88,307,353).  The frame is traced in passes of params->samples_per_pass
+ * samples per pixel (0: ceil(spp / 8)); after each pass `cb` gets the samples traced so far and the frame write_color'ed
+ * with that count, already in out_rgb8 (and the f64 sums in out_accum when non-NULL).  A non-zero return from `cb`
+ * stops the render there (RT_OK; stats->primary counts the samples traced).  Every snapshot equals rt_render of that
+ * many samples bit for bit, the last one rt_render's whole frame.  No RT_ADAPTIVE. */
+typedef int (*rt_progress_fn)(void* user, int32_t samples_done, int32_t spp, const uint8_t* rgb8, const double* accum);
+int rt_render_progressive(rt_scene* scene, const rt_camera* cam, const rt_params* params, uint8_t* out_rgb8, double* out_accum,
+                          rt_progress_fn cb, void* user, rt_stats* stats);
 /* Number of rows a band partition owns, and optionally their global indices (rows_out may be NULL). */
 int rt_local_rows(const rt_params* params, int32_t* rows_out);
+
+/* ---- multi-GPU (one process, one host thread per GPU, RCCL) ----
+ * Replaces the reference's CPU-parallel drivers (engine.h:335-376 _run_parallel_stripes: 4 threads on 4 row stripes;
+ * SURVEY.md §8(b) rt_render_multi).  An rt_multi holds the scene uploaded on every listed device and one RCCL
+ * communicator per device (ncclCommInitAll), made once at creation.  rt_render_multi renders the whole frame: device k
+ * renders the row bands b (params->band_rows rows each) with b % ngpus == k -- params->band_count / band_index are
+ * ignored -- packs them into one buffer, and a single ncclGather moves every device's block to devices[0], whose unpack
+ * kernel writes the rows in image order.  out_rgb8: W*H*3 bytes, row 0 = top; host memory, or device memory on
+ * devices[0] with RT_OUT_DEVICE.  The image is bit-identical to rt_render's for any device count (the RNG is keyed by
+ * (seed, global pixel, sample)).  stats: segments/primary summed over the devices, ms = host wall time of the call.
+ * Threading: one rt_multi per process at a time per device set; calls are blocking. */
+typedef struct rt_multi rt_multi;
+int rt_multi_create(const char* name, const char* asset_dir, const int* devices, int ngpus, rt_multi** out);
+int rt_multi_from_graph(rt_graph* g, const int* devices, int ngpus, rt_multi** out);
+void rt_multi_destroy(rt_multi* m);
+int rt_render_multi(rt_multi* m, const rt_camera* cam, const rt_params* params, uint8_t* out_rgb8, rt_stats* stats);
 
 /* ---- scene graph builder (one call per reference constructor; returns an id >= 0 or a negative code) ----
  * Scene-build randomness (noise textures' perlin tables, rt_graph_bvh's node draws) comes from the graph's own

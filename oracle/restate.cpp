@@ -20,6 +20,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <limits>
@@ -913,15 +914,34 @@ V3 ray_color_rec(const Scene& s, const Ray& r, int depth, Rng& rng, long long& s
 }
 
 // The same integrator flattened into the product's iterative form (pcg mode): L += T*e; T *= a.
+// Path tracing diagnostics: ORC_TRACE="pixel:sample" prints every segment of that one path (orc_render_rows) as bit
+// patterns, in the format of the product's ART_TRACE build (kernels.hip k_paths_g), so the two can be diffed.
+static thread_local bool g_tracing = false;
+static uint64_t bits(double x) {
+    uint64_t b;
+    std::memcpy(&b, &x, 8);
+    return b;
+}
 V3 ray_color_iter(const Scene& s, Ray r, int max_depth, Rng& rng, long long& segs) {
     V3 L(0, 0, 0), T(1, 1, 1);
     for (int depth = 0; depth < max_depth; ++depth) {
         HitRec rec;
         ++segs;
+        if (g_tracing)
+            std::fprintf(stderr, "TRACE d=%d o=%016llx,%016llx,%016llx dir=%016llx,%016llx,%016llx tm=%016llx rng=%016llx\n", depth,
+                         (unsigned long long)bits(r.orig[0]), (unsigned long long)bits(r.orig[1]), (unsigned long long)bits(r.orig[2]),
+                         (unsigned long long)bits(r.dir[0]), (unsigned long long)bits(r.dir[1]), (unsigned long long)bits(r.dir[2]),
+                         (unsigned long long)bits(r.tm), (unsigned long long)rng.state);
         if (!hit_list(s, s.world, r, 0.001, kInf, rec, rng)) {
+            if (g_tracing) std::fprintf(stderr, "TRACE miss\n");
             L += T * s.background;
             break;
         }
+        if (g_tracing)
+            std::fprintf(stderr, "TRACE hit t=%016llx p=%016llx,%016llx,%016llx n=%016llx,%016llx,%016llx ff=%d mat=%d\n",
+                         (unsigned long long)bits(rec.t), (unsigned long long)bits(rec.p[0]), (unsigned long long)bits(rec.p[1]),
+                         (unsigned long long)bits(rec.p[2]), (unsigned long long)bits(rec.normal[0]), (unsigned long long)bits(rec.normal[1]),
+                         (unsigned long long)bits(rec.normal[2]), rec.front_face ? 1 : 0, rec.mat);
         Ray sc;
         V3 att;
         V3 e = emitted(s, rec);
@@ -1180,6 +1200,65 @@ int orc_render(const char* scene, int W, int H, int spp, int max_depth, int mode
             });
         for (auto& th : pool) th.join();
     }
+    auto t1 = std::chrono::steady_clock::now();
+    if (segments_out) *segments_out = segs_total.load();
+    if (ms_out) *ms_out = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    return 0;
+} catch (const std::exception& e) {
+    g_err = e.what();
+    return -1;
+}
+
+int orc_render_rows(const char* scene, int W, int H, int spp, int max_depth, uint64_t seed, const int* rows, int nrows, int threads,
+                    uint8_t* rgb_out, double* acc_out, long long* segments_out, double* ms_out) try {
+    if (W < 2 || H < 2 || spp < 1 || max_depth < 0 || nrows < 0 || (nrows > 0 && !rows)) {
+        g_err = "invalid render arguments";
+        return -2;
+    }
+    for (int k = 0; k < nrows; ++k)
+        if (rows[k] < 0 || rows[k] >= H) { g_err = "row out of range"; return -2; }
+    Scene s;
+    Rng scene_rng;
+    build_scene(s, scene, scene_rng);
+    Camera cam(s.lookfrom, s.lookat, V3(0, 1, 0), s.vfov, static_cast<double>(W) / static_cast<double>(H), s.aperture, 10.0, 0.0, 1.0);
+    constexpr int kChunk = 64;
+    const int chunks = (W + kChunk - 1) / kChunk;
+    long long trace_pixel = -1, trace_sample = -1;
+    if (const char* t = std::getenv("ORC_TRACE")) std::sscanf(t, "%lld:%lld", &trace_pixel, &trace_sample);
+    auto t0 = std::chrono::steady_clock::now();
+    std::atomic<long long> segs_total{0};
+    std::atomic<long long> next{0};
+    const long long items = static_cast<long long>(nrows) * chunks;
+    const int nt = threads > 0 ? threads : static_cast<int>(std::max(1u, std::thread::hardware_concurrency()));
+    std::vector<std::thread> pool;
+    for (int t = 0; t < nt; ++t)
+        pool.emplace_back([&]() {
+            Rng rng;
+            rng.pcg = true;
+            long long segs = 0;
+            for (long long it = next++; it < items; it = next++) {
+                const int k = static_cast<int>(it / chunks), j = rows[k];
+                const int i0 = static_cast<int>(it % chunks) * kChunk, i1 = std::min(W, i0 + kChunk);
+                for (int i = i0; i < i1; ++i) {  // the per-pixel loop of orc_render, ORC_PCG
+                    V3 pc(0, 0, 0);
+                    for (int sidx = 0; sidx < spp; ++sidx) {
+                        g_tracing = trace_pixel == static_cast<long long>(j) * W + i && trace_sample == sidx;
+                        rng.state = pcg_seed(seed, static_cast<uint32_t>(j) * static_cast<uint32_t>(W) + static_cast<uint32_t>(i), static_cast<uint32_t>(sidx));
+                        double ru = rng.d();
+                        double rv = rng.d();
+                        double u = (i + ru) / (W - 1);  // engine.h:62-63
+                        double v = ((H - 1 - j) + rv) / (H - 1);
+                        Ray r = cam.get_ray(u, v, rng);
+                        pc += ray_color_iter(s, r, max_depth, rng, segs);
+                    }
+                    const size_t o = 3 * (static_cast<size_t>(k) * W + i);
+                    if (acc_out) { acc_out[o] = pc[0]; acc_out[o + 1] = pc[1]; acc_out[o + 2] = pc[2]; }
+                    if (rgb_out) write_color(rgb_out + o, pc, spp);
+                }
+            }
+            segs_total += segs;
+        });
+    for (auto& th : pool) th.join();
     auto t1 = std::chrono::steady_clock::now();
     if (segments_out) *segments_out = segs_total.load();
     if (ms_out) *ms_out = std::chrono::duration<double, std::milli>(t1 - t0).count();

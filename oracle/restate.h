@@ -37,6 +37,12 @@ int orc_render(const char* scene, int W, int H, int spp, int max_depth, int mode
                int row0, int nrows, int threads, uint8_t* rgb_out, double* acc_out,
                long long* segments_out, double* ms_out);
 
+// ORC_PCG render of an arbitrary list of rows (rows[k] = global row of output row k) of a WxH image, spread over
+// `threads` host threads (<= 0: hardware_concurrency) in work items of (row, 64-pixel column chunk) taken
+// dynamically, so a few expensive rows still use every thread.  Same outputs and arguments as orc_render.
+int orc_render_rows(const char* scene, int W, int H, int spp, int max_depth, uint64_t seed, const int* rows, int nrows,
+                    int threads, uint8_t* rgb_out, double* acc_out, long long* segments_out, double* ms_out);
+
 // engine_mode::adaptive (engine.h:96-333) over the whole WxH image (W, H multiples of 12).  ORC_MT: the
 // reference's draw sequence with its 4 stripes run one after another (bit-exact vs `ref_harness render .. adaptive`);
 // ORC_PCG: the product's streams, every distinct pixel traced once.  rgb_out: H*W*3 u8.  Returns -3 on a size the

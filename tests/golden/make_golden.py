@@ -12,6 +12,10 @@ fixtures pin:
                        scene build incl. BVH-build draws) and the sha256 of the canonical scene dump
   * render_<scene>.npz reference renders (engine_mode::single semantics): RGB8, f64 per-pixel sums and the
                        exact segment count (world.hit calls)
+  * render_stat_1_384x216x16.npz  the headline scene (alias 1) rendered by the reference twice with independent
+                       sample sequences -- engine_mode::single, and parallel_stripes with 4 threads (its shared
+                       global RNG) -- for the statistical parity test of the f64 GPU path (SURVEY.md §8(d)
+                       tolerance 3: the pair's RMSE is the noise floor); `make_golden.py stat` makes only this
   * render_adaptive_<scene>.npz  engine_mode::adaptive renders (engine.h:96-333, its 4 stripes run in order):
                        RGB8 and segment count (`python tests/golden/make_golden.py adaptive` makes only these)
 Assets written by the same harness: assets/*.tris (the reference's post-triangulation triangle lists: cow,
@@ -61,6 +65,21 @@ def adaptive_fixtures():
         print("adaptive", sc, info)
 
 
+STAT = ("1", 384, 216, 16)
+
+
+def stat_fixtures():
+    sc, W, H, spp = STAT
+    rgb, acc, info = render(sc, W, H, spp)
+    tmp = "/tmp/golden_stat_stripes"
+    info2 = json.loads(run("render", sc, W, H, spp, tmp, "stripes", 4).strip().splitlines()[-1])
+    rgb2 = np.fromfile(tmp + ".rgb", np.uint8).reshape(H, W, 3)
+    np.savez_compressed(os.path.join(HERE, f"render_stat_{sc}_{W}x{H}x{spp}.npz"), rgb_single=rgb, rgb_stripes=rgb2,
+                        segments_single=np.int64(info["segments"]), segments_stripes=np.int64(info2["segments"]),
+                        W=W, H=H, spp=spp)
+    print("stat", sc, info, info2)
+
+
 def scene_fixtures(sc):
     """probe + dump hash (scenes.json entry) and the SMALL render of one scene."""
     # the harness may log texture loads on stdout first: the values are the last 8 lines
@@ -96,6 +115,9 @@ def main():
     if sys.argv[1:] == ["adaptive"]:
         adaptive_fixtures()
         return
+    if sys.argv[1:] == ["stat"]:
+        stat_fixtures()
+        return
     if sys.argv[1:2] == ["scene"]:
         path = os.path.join(HERE, "scenes.json")
         scenes = json.load(open(path))
@@ -120,6 +142,7 @@ def main():
                         acc=acc.astype(np.float64), segments=np.int64(info["segments"]), W=W, H=H, spp=spp)
     print(sc, info)
     adaptive_fixtures()
+    stat_fixtures()
 
 
 if __name__ == "__main__":

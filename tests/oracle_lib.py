@@ -26,6 +26,9 @@ def oracle():
         lib.orc_render.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                    ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                    ctypes.c_void_p, ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double)]
+        lib.orc_render_rows.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double)]
         lib.orc_render_adaptive.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                             ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p,
                                             ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double)]
@@ -42,6 +45,21 @@ def oracle_render(scene, W, H, spp, mode="pcg", seed=0, row0=0, nrows=None, thre
     segs, ms = ctypes.c_longlong(), ctypes.c_double()
     r = lib.orc_render(str(scene).encode(), W, H, spp, max_depth, MODES[mode], seed, row0, nrows, threads,
                        rgb.ctypes.data, acc.ctypes.data, ctypes.byref(segs), ctypes.byref(ms))
+    if r != 0:
+        raise RuntimeError(lib.orc_last_error().decode())
+    return {"rgb": rgb, "acc": acc, "segments": segs.value, "ms": ms.value}
+
+
+def oracle_render_rows(scene, W, H, spp, rows, seed=0, threads=0, max_depth=50):
+    """pcg-mode render of the listed global rows of a WxH frame (dynamic (row, column chunk) work items)."""
+    lib = oracle()
+    rows = np.ascontiguousarray(rows, dtype=np.int32)
+    n = len(rows)
+    rgb = np.zeros((n, W, 3), np.uint8)
+    acc = np.zeros((n, W, 3), np.float64)
+    segs, ms = ctypes.c_longlong(), ctypes.c_double()
+    r = lib.orc_render_rows(str(scene).encode(), W, H, spp, max_depth, seed, rows.ctypes.data, n, threads, rgb.ctypes.data,
+                            acc.ctypes.data, ctypes.byref(segs), ctypes.byref(ms))
     if r != 0:
         raise RuntimeError(lib.orc_last_error().decode())
     return {"rgb": rgb, "acc": acc, "segments": segs.value, "ms": ms.value}

@@ -27,7 +27,7 @@ def test_every_declared_symbol_is_exported_and_bound():
     exported = set(re.findall(r" T (rt_\w+)", nm))
     assert set(decl) <= exported, set(decl) - exported
     assert set(decl) == set(_lib.SIGNATURES), set(decl) ^ set(_lib.SIGNATURES)
-    assert _lib.lib.rt_abi_version() == 1
+    assert _lib.lib.rt_abi_version() == _lib.RT_ABI_VERSION == 2
 
 
 def test_struct_layouts_match_the_header(tmp_path):
@@ -132,3 +132,23 @@ def test_adaptive_mode_rejects_off_grid_sizes_like_the_reference():
     eng.set_scene(w.objects, w.background)
     with pytest.raises(ValueError, match="big square"):
         eng.run(np.zeros((36, 50, 3), np.uint8))
+
+
+def test_multi_entry_points_validate_without_a_gpu():
+    # argument errors are reported before any device work; without a GPU the multi-GPU renderer fails loudly
+    # (RT_E_DEVICE), it never falls back to anything
+    import ctypes
+    m = ctypes.c_void_p()
+    devs = (ctypes.c_int * 1)(0)
+    assert _lib.lib.rt_multi_create(b"c1", b"assets", devs, 0, ctypes.byref(m)) == -1
+    assert _lib.lib.rt_multi_create(None, b"assets", devs, 1, ctypes.byref(m)) == -1
+    assert _lib.lib.rt_multi_create(b"no_such_scene", b"assets", devs, 1, ctypes.byref(m)) == -2
+    if not torch_has_gpu():
+        assert _lib.lib.rt_multi_create(b"c1", b"assets", devs, 1, ctypes.byref(m)) == -3
+        assert m.value is None
+    assert _lib.lib.rt_render_multi(None, None, None, None, None) == -1
+
+
+def torch_has_gpu():
+    import torch
+    return torch.cuda.device_count() > 0

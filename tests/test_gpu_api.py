@@ -91,3 +91,101 @@ def test_adaptive_mode_refuses_accum_and_off_grid_sizes(gpu):
     e.m = art.engine_mode.adaptive
     with pytest.raises(ValueError, match="big square"):
         e.run(np.zeros((40, 64, 3), np.uint8))
+
+
+def test_workspace_allocation_failure_leaves_the_scene_usable(gpu, monkeypatch):
+    # a refused workspace allocation (fault injection: ART_FAULT_WORKSPACE_BYTES) is reported as RT_E_DEVICE, and the
+    # next render on the same scene allocates again instead of using a stale size with a null base
+    e = make()
+    first = np.zeros((40, 64, 3), np.uint8)
+    e.run(first)
+    big = make(W=256, H=160)
+    big._scene = e._scene  # same rt_scene (and renderer workspace), larger frame: the workspace must grow
+    monkeypatch.setenv("ART_FAULT_WORKSPACE_BYTES", "1024")
+    with pytest.raises(art.RTError) as err:
+        big.run(np.zeros((160, 256, 3), np.uint8))
+    assert err.value.code == -3 and "ART_FAULT_WORKSPACE_BYTES" in str(err.value)
+    monkeypatch.delenv("ART_FAULT_WORKSPACE_BYTES")
+    again = np.zeros((40, 64, 3), np.uint8)
+    e.run(again)
+    assert np.array_equal(again, first)
+    grown = np.zeros((160, 256, 3), np.uint8)
+    big.run(grown)
+    fresh = np.zeros((160, 256, 3), np.uint8)
+    make(W=256, H=160).run(fresh)
+    assert np.array_equal(grown, fresh)
+
+
+def test_oversized_samples_per_pass_is_clamped(gpu):
+    # samples_per_pass * padded pixels beyond 2^31 slots used to wrap the u32 pass size: it is clamped to the largest
+    # pass that fits (1035 samples of a 1920x1080 frame), and the image equals the automatic pass split's
+    W, H, spp = 1920, 1080, 2100
+    e = make(W=W, H=H, spp=spp, samples_per_pass=2100)
+    acc = np.zeros((H, W, 3), np.float64)
+    e.run(np.zeros((H, W, 3), np.uint8), accum=acc)
+    assert e.stats["samples_per_pass"] * 240 * 135 * 64 <= 2 ** 31 and e.stats["passes"] == 3
+    auto = make(W=W, H=H, spp=spp)
+    acc2 = np.zeros((H, W, 3), np.float64)
+    auto.run(np.zeros((H, W, 3), np.uint8), accum=acc2)
+    assert np.array_equal(acc, acc2) and e.stats["segments"] == auto.stats["segments"]
+
+
+@pytest.mark.parametrize("band_rows", [1, 7, 16])
+def test_render_multi_one_gpu_matches_render(gpu, band_rows):
+    # rt_render_multi through its RCCL path (ncclCommInitAll, ncclGather to devices[0], unpack kernel) with one GPU
+    # reproduces rt_render bit for bit, into host and device memory
+    from another_raytracer_amd.distributed import multi_engine
+    W, H, spp = 160, 90, 8
+    w = art.scene_manager().build("1")
+    cam = art.camera(w.lookfrom, w.lookat, (0, 1, 0), w.vfov, W / H, w.aperture, 10.0, 0.0, 1.0)
+    e = art.engine(cam, art.engine_mode.single, width=W, height=H, samples_per_pixel=spp)
+    e.set_scene(w.objects, w.background)
+    ref = np.zeros((H, W, 3), np.uint8)
+    e.run(ref)
+    m = multi_engine("1", [0], cam, W, H, spp, band_rows=band_rows, background=w.background)
+    host = np.zeros((H, W, 3), np.uint8)
+    m.run(host)
+    assert np.array_equal(host, ref) and m.stats["segments"] == e.stats["segments"] and m.stats["local_rows"] == H
+    dev = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda:0")
+    m.run(dev)
+    assert np.array_equal(dev.cpu().numpy(), ref)
+
+
+def test_render_multi_rejects_duplicate_devices(gpu):
+    from another_raytracer_amd.distributed import multi_engine
+    w = art.scene_manager().build("c1")
+    cam = art.camera(w.lookfrom, w.lookat, (0, 1, 0), w.vfov, 2.0, w.aperture, 10.0, 0.0, 1.0)
+    with pytest.raises(art.RTError, match="only once"):
+        multi_engine("c1", [0, 0], cam, 32, 16, 1)
+
+
+def test_progressive_snapshots_equal_one_shot_renders(gpu):
+    # rt_render_progressive: after each pass the snapshot equals a one-shot render of that many samples bit for bit
+    # (samples are keyed by (pixel, sample index) and summed in order), and the last one the whole frame
+    W, H, spp = 96, 54, 8
+    e = make(W=W, H=H, spp=spp)
+    img = np.zeros((H, W, 3), np.uint8)
+    acc = np.zeros((H, W, 3), np.float64)
+    snaps = []
+    e.run_progressive(img, lambda done, total: snaps.append((done, img.copy(), acc.copy())), accum=acc, samples_per_pass=3)
+    assert [s[0] for s in snaps] == [3, 6, 8]
+    for done, rgb, sums in snaps:
+        one = make(W=W, H=H, spp=done)
+        r1 = np.zeros((H, W, 3), np.uint8)
+        a1 = np.zeros((H, W, 3), np.float64)
+        one.run(r1, accum=a1)
+        assert np.array_equal(rgb, r1) and np.array_equal(sums, a1)
+    assert e.stats["primary"] == W * H * spp
+
+
+def test_progressive_callback_can_stop_early(gpu):
+    W, H, spp = 64, 40, 9
+    e = make(W=W, H=H, spp=spp)
+    img = np.zeros((H, W, 3), np.uint8)
+    seen = []
+    e.run_progressive(img, lambda done, total: seen.append(done) or done >= 4, samples_per_pass=2)
+    assert seen == [2, 4] and e.stats["primary"] == W * H * 4
+    four = make(W=W, H=H, spp=4)
+    r4 = np.zeros((H, W, 3), np.uint8)
+    four.run(r4)
+    assert np.array_equal(img, r4)

@@ -1,12 +1,13 @@
 """HIP path (through the C ABI) vs the oracle — the parity gate (SURVEY.md §8(d) tolerances).
 
-* f64 leaf/shading path vs oracle/restate.cpp ORC_PCG (same PCG streams, same f64 operation order): every scene,
-  >= 99.9 % of pixels within +-1 LSB and the exact segment count within 0.1 % (differences come only from
-  OCML-vs-glibc transcendental ulps and BVH ties flipping a branch).
-* f32 path vs the same oracle: RGB8 RMSE <= 1.0 LSB and >= 99.5 % of pixels within +-1 LSB at 64 spp.
+* The f64 path (the only arithmetic, ABI 2) vs oracle/restate.cpp ORC_PCG (same PCG streams, same f64 operation
+  order): every scene, bit-identical RGB8 frame, bit-identical f64 per-pixel radiance sums and the exact segment count.
 * Independence from the partition: band-interleaved renders reassemble to the bit-identical image.
-* Statistical parity with the reference program itself (independent RNG): RMSE vs the reference's own render of
-  configs[0] (tests/golden/render_c1_400x225x64.npz) <= 1.1x the oracle's seed-to-seed noise floor.
+* Statistical parity with the reference program itself (independent RNG, SURVEY.md §8(d) tolerance 3), f64 path:
+  - configs[0] (tests/golden/render_c1_400x225x64.npz): RMSE <= 1.1x the oracle's seed-to-seed noise floor;
+  - the headline scene (alias 1) at 384x216x16 (tests/golden/render_stat_1_384x216x16.npz: the reference's single
+    and 4-thread stripes renders): RMSE vs the single render <= 1.1x the single-vs-stripes RMSE, the same on 8x8
+    block means (x1.25: noise / 8, so a bias of ~1 LSB shows), and the per-channel mean within 0.5 LSB.
 """
 import numpy as np
 import pytest
@@ -50,34 +51,21 @@ def test_f64_matches_oracle_pcg(gpu, scene):
     g = gpu_render(scene, W, H, spp, "f64")
     o = oracle_render(scene, W, H, spp, mode="pcg")
     rmse, within1, dmax = lsb_stats(g["rgb"], o["rgb"])
-    rel = abs(g["segments"] - o["segments"]) / o["segments"]
     print(f"{scene}: rmse {rmse:.4f} within1 {within1:.5f} max {dmax} segs {g['segments']} vs {o['segments']}")
-    assert within1 >= 0.999, (rmse, within1, dmax)
-    assert rel <= 1e-3
+    assert np.array_equal(g["rgb"], o["rgb"]), (rmse, within1, dmax)
+    assert np.array_equal(g["acc"], o["acc"])
+    assert g["segments"] == o["segments"]
 
 
-@pytest.mark.xfail(reason="RT_FP32 is experimental: f32 sphere/medium tests self-intersect on the reference's "
-                          "large-radius spheres (r=1000 ground, r=5000 mist), see DESIGN.md 'Precision'", strict=False)
-@pytest.mark.parametrize("scene", ["c1", "1", "8", "cow"])
-def test_f32_within_tolerance(gpu, scene):
-    W, H, spp = 64, 36, 64
-    g = gpu_render(scene, W, H, spp, "f32", accum=False)
-    o = oracle_render(scene, W, H, spp, mode="pcg")
-    rmse, within1, dmax = lsb_stats(g["rgb"], o["rgb"])
-    print(f"{scene} f32: rmse {rmse:.4f} within1 {within1:.5f} max {dmax} segs {g['segments']} vs {o['segments']}")
-    assert rmse <= 1.0 and within1 >= 0.995, (rmse, within1, dmax)
-
-
-@pytest.mark.parametrize("precision", ["f32", "f64"])
-def test_band_partition_is_bit_identical(gpu, precision):
+def test_band_partition_is_bit_identical(gpu):
     W, H, spp = 80, 50, 4
-    full = gpu_render("1", W, H, spp, precision)
+    full = gpu_render("1", W, H, spp)
     for bands, brows in ((2, 16), (3, 8), (8, 4)):
         img = np.zeros_like(full["rgb"])
         acc = np.zeros_like(full["acc"])
         segs = 0
         for b in range(bands):
-            part = gpu_render("1", W, H, spp, precision, band=(brows, bands, b))
+            part = gpu_render("1", W, H, spp, band=(brows, bands, b))
             rows = part["engine"].local_rows(brows, bands, b)
             img[rows] = part["rgb"]
             acc[rows] = part["acc"]
@@ -138,16 +126,44 @@ def test_statistical_parity_with_reference_config0(gpu):
     ref = np.load("tests/golden/render_c1_400x225x64.npz")
     W, H, spp = int(ref["W"]), int(ref["H"]), int(ref["spp"])
     floor = np.mean([lsb_stats(oracle_render("c1", W, H, spp, mode="pcg", seed=s)["rgb"], ref["rgb"])[0] for s in (11, 12)])
-    gpu_rmse = np.mean([lsb_stats(gpu_render("c1", W, H, spp, "f32", seed=s, accum=False)["rgb"], ref["rgb"])[0]
+    gpu_rmse = np.mean([lsb_stats(gpu_render("c1", W, H, spp, "f64", seed=s, accum=False)["rgb"], ref["rgb"])[0]
                         for s in (21, 22)])
     print(f"rmse vs reference: gpu {gpu_rmse:.3f} oracle floor {floor:.3f}")
     assert gpu_rmse <= 1.1 * floor
 
 
+def _block_means(x, k=8):
+    H, W, _ = x.shape
+    return x[:H // k * k, :W // k * k].astype(np.float64).reshape(H // k, k, W // k, k, 3).mean(axis=(1, 3))
+
+
+def _rmse(a, b):
+    return float(np.sqrt(np.mean((a.astype(np.float64) - b.astype(np.float64)) ** 2)))
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_statistical_parity_headline_scene_f64(gpu, seed):
+    """The f64 GPU path vs the reference program's own render of the headline scene (independent RNG)."""
+    ref = np.load("tests/golden/render_stat_1_384x216x16.npz")
+    W, H, spp = int(ref["W"]), int(ref["H"]), int(ref["spp"])
+    single, stripes = ref["rgb_single"], ref["rgb_stripes"]
+    floor, bfloor = _rmse(single, stripes), _rmse(_block_means(single), _block_means(stripes))
+    g = gpu_render("1", W, H, spp, "f64", seed=seed, accum=False)
+    rmse, brmse = _rmse(g["rgb"], single), _rmse(_block_means(g["rgb"]), _block_means(single))
+    bias = (g["rgb"].astype(np.float64) - single).mean(axis=(0, 1))
+    print(f"seed {seed}: rmse {rmse:.3f} (floor {floor:.3f}) block rmse {brmse:.3f} (floor {bfloor:.3f}) bias {bias}")
+    assert rmse <= 1.1 * floor
+    assert brmse <= 1.25 * bfloor
+    assert np.all(np.abs(bias) <= 0.5)
+    # same light transport: segments per primary within 1 % of the reference's
+    r_ref = int(ref["segments_single"]) / (W * H * spp)
+    assert abs(g["segments"] / (W * H * spp) - r_ref) / r_ref < 0.01
+
+
 def test_segments_match_reference_rate(gpu):
     # segments per primary ray of the reference (golden, mt) vs the HIP path: same light transport
     ref = np.load("tests/golden/render_c1_400x225x64.npz")
-    g = gpu_render("c1", 400, 225, 64, "f32", accum=False)
+    g = gpu_render("c1", 400, 225, 64, "f64", accum=False)
     r_ref = int(ref["segments"]) / (400 * 225 * 64)
     r_gpu = g["segments"] / (400 * 225 * 64)
     assert abs(r_gpu - r_ref) / r_ref < 0.01, (r_gpu, r_ref)
