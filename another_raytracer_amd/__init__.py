@@ -22,7 +22,7 @@ from .engine import camera, engine, engine_mode, tracer_constants  # noqa: F401
 from .scene import (  # noqa: F401
     barycentric_image_texture, box, bvh_node, checker_texture, constant_medium, dielectric, diffuse_light, hittable_list, image_texture,
     lambertian, mesh, metal, moving_sphere, noise_texture, random_double, rotate_y, scene, scene_alias, scene_manager,
-    solid_color, sphere, translate, triangle, xy_rect, xz_rect, yz_rect, reset_scene_rng,
+    solid_color, sphere, translate, triangle, xy_rect, xz_rect, yz_rect, reset_scene_rng, save_scene,
 )
 from . import imageio  # noqa: F401
 
@@ -30,5 +30,5 @@ __all__ = [
     "RTError", "camera", "engine", "engine_mode", "tracer_constants", "scene", "scene_alias", "scene_manager",
     "hittable_list", "bvh_node", "sphere", "moving_sphere", "triangle", "xy_rect", "xz_rect", "yz_rect", "box",
     "translate", "rotate_y", "constant_medium", "lambertian", "metal", "dielectric", "diffuse_light", "solid_color",
-    "checker_texture", "noise_texture", "image_texture", "barycentric_image_texture", "mesh", "random_double", "reset_scene_rng", "imageio",
+    "checker_texture", "noise_texture", "image_texture", "barycentric_image_texture", "mesh", "random_double", "reset_scene_rng", "imageio", "save_scene",
 ]

@@ -73,9 +73,15 @@ SIGNATURES = {
     "rt_scene_info_get": (_I, [_P, ctypes.POINTER(rt_scene_info)]),
     "rt_scene_dump": (_S, [_P, ctypes.c_char_p, _S]),
     "rt_scene_destroy": (None, [_P]),
+    "rt_scene_save": (_I, [_P, ctypes.c_char_p]),
+    "rt_scene_load": (_I, [ctypes.c_char_p, _I, ctypes.POINTER(_P)]),
     "rt_render": (_I, [_P, ctypes.POINTER(rt_camera), ctypes.POINTER(rt_params), _P, _P, ctypes.POINTER(rt_stats)]),
     "rt_render_progressive": (_I, [_P, ctypes.POINTER(rt_camera), ctypes.POINTER(rt_params), _P, _P, rt_progress_fn, _P,
                                    ctypes.POINTER(rt_stats)]),
+    "rt_trace_rays": (_I, [_P, _P, ctypes.c_int64, ctypes.c_int32, _P, _P]),
+    "rt_image_load": (_I, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
+                           ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8))]),
+    "rt_image_free": (None, [ctypes.POINTER(ctypes.c_uint8)]),
     "rt_local_rows": (_I, [ctypes.POINTER(rt_params), ctypes.POINTER(ctypes.c_int32)]),
     "rt_multi_create": (_I, [ctypes.c_char_p, ctypes.c_char_p, _IP, _I, ctypes.POINTER(_P)]),
     "rt_multi_from_graph": (_I, [_P, _IP, _I, ctypes.POINTER(_P)]),

@@ -1,4 +1,5 @@
 // abi.cpp — the extern "C" boundary (include/art.h).  No exception crosses it.
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <stdexcept>
@@ -8,8 +9,10 @@
 #include <vector>
 
 #include "art.h"
+#include "imagedec.h"
 #include "multi.h"
 #include "renderer.h"
+#include "scenefile.h"
 #include "objmesh.h"
 #include "scene.h"
 
@@ -18,8 +21,10 @@ int device_count();  // kernels.hip
 }
 
 struct rt_scene {
-    art::SceneGraph graph;
+    art::SceneGraph graph;       // empty for a scene loaded from a flat-scene file (has_graph false)
+    bool has_graph = true;
     art::FlatScene flat;
+    art::SceneView view;         // scene_manager::build's lookfrom / lookat / vfov / aperture
     int device = 0;
     std::unique_ptr<art::Renderer> renderer;  // created on first render (scene build/dump works without a GPU)
 };
@@ -113,6 +118,12 @@ int scene_from_graph(art::SceneGraph graph, int device, rt_scene** out) {
     auto s = std::make_unique<rt_scene>();
     s->graph = std::move(graph);
     s->flat = art::compile_scene(s->graph);
+    for (int a = 0; a < 3; ++a) {
+        s->view.lookfrom[a] = s->graph.lookfrom[a];
+        s->view.lookat[a] = s->graph.lookat[a];
+    }
+    s->view.vfov = s->graph.vfov;
+    s->view.aperture = s->graph.aperture;
     s->device = device;
     *out = s.release();
     return RT_OK;
@@ -141,12 +152,12 @@ int rt_scene_info_get(const rt_scene* s, rt_scene_info* info) {
     if (!s || !info) return fail(RT_E_INVALID, "scene and info must be non-NULL");
     std::memset(info, 0, sizeof *info);
     for (int a = 0; a < 3; ++a) {
-        info->lookfrom[a] = s->graph.lookfrom[a];
-        info->lookat[a] = s->graph.lookat[a];
-        info->background[a] = s->graph.background[a];
+        info->lookfrom[a] = s->view.lookfrom[a];
+        info->lookat[a] = s->view.lookat[a];
+        info->background[a] = s->flat.background[a];
     }
-    info->vfov = s->graph.vfov;
-    info->aperture = s->graph.aperture;
+    info->vfov = s->view.vfov;
+    info->aperture = s->view.aperture;
     info->spheres = static_cast<int64_t>(s->flat.spheres.size());
     info->triangles = static_cast<int64_t>(s->flat.tris.size());
     info->rects = static_cast<int64_t>(s->flat.rects.size());
@@ -168,6 +179,10 @@ size_t rt_scene_dump(const rt_scene* s, char* buf, size_t cap) {
         fail(RT_E_INVALID, "scene is NULL");
         return 0;
     }
+    if (!s->has_graph) {
+        fail(RT_E_INVALID, "a scene loaded from a flat-scene file has no object graph to dump");
+        return 0;
+    }
     try {
         std::string d = art::dump_scene(s->graph);
         if (buf && cap) {
@@ -180,6 +195,27 @@ size_t rt_scene_dump(const rt_scene* s, char* buf, size_t cap) {
         fail(RT_E_INTERNAL, e.what());
         return 0;
     }
+}
+
+int rt_scene_save(const rt_scene* s, const char* path) {
+    if (!s || !path) return fail(RT_E_INVALID, "scene and path must be non-NULL");
+    return guard(RT_E_INVALID, [&] {
+        art::save_scene_file(path, s->flat, s->view);
+        return RT_OK;
+    });
+}
+
+int rt_scene_load(const char* path, int device, rt_scene** out) {
+    if (!path || !out) return fail(RT_E_INVALID, "path and out must be non-NULL");
+    *out = nullptr;
+    return guard(RT_E_SCENE, [&] {
+        auto s = std::make_unique<rt_scene>();
+        art::load_scene_file(path, s->flat, s->view);
+        s->has_graph = false;
+        s->device = device;
+        *out = s.release();
+        return RT_OK;
+    });
 }
 
 void rt_scene_destroy(rt_scene* s) {
@@ -241,6 +277,33 @@ int rt_render_progressive(rt_scene* s, const rt_camera* cam, const rt_params* p,
         return RT_OK;
     });
 }
+
+int rt_trace_rays(rt_scene* s, const double* rays, int64_t n, int32_t flags, double* t_out, double* normal_out) {
+    if (!s || n < 0 || (n > 0 && (!rays || !t_out))) return fail(RT_E_INVALID, "scene, rays and t_out must be non-NULL, n >= 0");
+    return guard(RT_E_DEVICE, [&] {
+        if (!s->renderer) s->renderer = std::make_unique<art::Renderer>(s->flat, s->device);
+        std::vector<double> nrm(normal_out ? 0 : 3 * static_cast<size_t>(n));
+        s->renderer->trace_rays(rays, static_cast<size_t>(n), (flags & RT_GLOBAL_SCENE) != 0, t_out, normal_out ? normal_out : nrm.data());
+        return RT_OK;
+    });
+}
+
+int rt_image_load(const char* path, int32_t* width, int32_t* height, int32_t* channels, uint8_t** pixels) {
+    if (!path || !width || !height || !channels || !pixels) return fail(RT_E_INVALID, "NULL argument");
+    *pixels = nullptr;
+    return guard(RT_E_INVALID, [&] {
+        art::DecodedImage d = art::load_image_file(path);
+        uint8_t* p = static_cast<uint8_t*>(std::malloc(d.data.size()));
+        if (!p) throw std::bad_alloc();
+        std::memcpy(p, d.data.data(), d.data.size());
+        *width = d.w;
+        *height = d.h;
+        *channels = d.channels;
+        *pixels = p;
+        return RT_OK;
+    });
+}
+void rt_image_free(uint8_t* pixels) { std::free(pixels); }
 
 // ---------------------------------------------------------------------------------------------- multi-GPU
 int rt_multi_create(const char* name, const char* asset_dir, const int* devices, int ngpus, rt_multi** out) {

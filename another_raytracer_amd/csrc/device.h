@@ -580,6 +580,14 @@ __device__ __forceinline__ uint32_t stack_column(uint32_t t) {
     return (t & ~63u) | ((t & 31u) << 1) | ((t >> 5) & 1u);
 }
 
+#ifndef ART_RCP_CLAMP
+#define ART_RCP_CLAMP 1
+#endif
+// f32 direction component for the slab reciprocals: magnitude at least 2^-64, sign of d (-0 stays negative).
+__device__ __forceinline__ float f32_dir(double d) {
+    const float f = static_cast<float>(d);
+    return __builtin_copysignf(fmaxf(__builtin_fabsf(f), 0x1p-64f), f);
+}
 // B: lanes per block (LDS stack stride).  L: nodes and leaf spheres come from the LDS scene image at `lds`.
 template <class R, uint32_t F, int B, bool L>
 __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* lds, int32_t root, const Ray<R>& r, R tmin, R tmax,
@@ -587,8 +595,16 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
     static_assert(!(L && (F & F_MEDIA)), "packed LDS keys need tmin > 0: no medium boundary tests in the LDS variant");
     const float ox = static_cast<float>(r.o.x), oy = static_cast<float>(r.o.y), oz = static_cast<float>(r.o.z);
     // hardware reciprocal (1 ulp): the box test is conservative by its 2e-6 relative padding, far above that
+#if ART_RCP_CLAMP
+    // A direction component that is 0 (or tiny) would give 1/d = inf, and the plane distances fma(plane, 1/d, -o/d)
+    // would mix +-inf and NaN (inf - inf): a ray parallel to an axis then missed boxes that hold it (tests/
+    // test_gpu_rays.py).  The component is raised to +-2^-64 with its sign, so 1/d, o/d and plane/d stay finite for
+    // any coordinate below 1e19 and the slab of a parallel ray holds its origin for t in (-huge, +huge) or for none.
+    const float ix = __builtin_amdgcn_rcpf(f32_dir(r.d.x)), iy = __builtin_amdgcn_rcpf(f32_dir(r.d.y)), iz = __builtin_amdgcn_rcpf(f32_dir(r.d.z));
+#else
     const float ix = __builtin_amdgcn_rcpf(static_cast<float>(r.d.x)), iy = __builtin_amdgcn_rcpf(static_cast<float>(r.d.y)),
                 iz = __builtin_amdgcn_rcpf(static_cast<float>(r.d.z));
+#endif
     const float oix = ox * ix, oiy = oy * iy, oiz = oz * iz;
     // LDS variant: the near and far plane of each axis follow from the direction's sign, so the slab test reads them
     // directly (near plane offset per axis; the far plane is always the plane above it, one kLdsPlane away -- an

@@ -933,6 +933,46 @@ __global__ __launch_bounds__(256) void k_accum(PassGeom g, Work<R> w) {
 }
 
 #if ART_SPLIT_PATHS != 2
+// Ray queries (rt_trace_rays): the world's closest hit (hittable_list::hit, hittable_list.cpp:5-19) of n caller-given
+// rays through the renderer's own traversal -- the LDS image (L) or the HBM scene -- and the surface normal
+// (hit_record::set_face_normal), so traversal edge cases (axis-parallel rays, origins on faces) can be checked one ray
+// at a time against the oracle.  Ray i's medium draws come from the PCG stream pcg_seed(0, i, 0).
+template <uint32_t F, bool L>
+__global__ __launch_bounds__(L ? kBlockL : kBlock) void k_trace_rays(DevScene<double> S, const double* rays, uint32_t n, uint32_t stack_rows,
+                                                                       double* t_out, double* n_out) {
+    using R = double;
+    constexpr int B = L ? kBlockL : kBlock;
+    extern __shared__ __align__(16) uint8_t smem[];
+    StackT<L>* stk = reinterpret_cast<StackT<L>*>(smem + (L ? kLdsImageBytes : 0u)) + B + stack_column<L>(threadIdx.x);
+    stk[-B] = static_cast<StackT<L>>(kNodeEmpty);
+    if constexpr (L) {
+        load_lds_image<B>(S.lds_image, smem);
+        __syncthreads();
+    }
+    (void)stack_rows;
+    const uint32_t i = blockIdx.x * B + threadIdx.x;
+    if (i >= n) return;
+    const double* q = rays + 7 * static_cast<size_t>(i);
+    Ray<R> r;
+    r.o = mk(q[0], q[1], q[2]);
+    r.d = mk(q[3], q[4], q[5]);
+    r.tm = q[6];
+    uint64_t rng = pcg_seed(0, i, 0);
+    R t = R(0);
+    HitOut h{0, 0, kMatUnknown};
+    if (trace_world<R, F, B, L>(S, L ? smem : nullptr, r, stk, rng, t, h)) {
+        Surf<R> s;
+        world_surface<R, F, false>(S, h, r, t, s);
+        t_out[i] = t;
+        n_out[3 * i] = s.n.x;
+        n_out[3 * i + 1] = s.n.y;
+        n_out[3 * i + 2] = s.n.z;
+    } else {
+        t_out[i] = __builtin_inf();
+        n_out[3 * i] = n_out[3 * i + 1] = n_out[3 * i + 2] = 0.0;
+    }
+}
+
 __global__ void k_finalize(const double* acc, uint8_t* rgb, uint32_t n, int spp) {  // color.h:6-22
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -1796,6 +1836,43 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
         stats.shade_launches = variant == EXT_GLOBAL || variant == EXT_LDS ? ext_launches : 0;
         for (auto e : evs) (void)hipEventDestroy(e);
     }
+}
+
+void Renderer::trace_rays(const double* rays, size_t n, bool global_scene, double* t_out, double* n_out) {
+    HIP_OK(hipSetDevice(impl_->device));
+    if (!impl_->up64) { build_device_scene(impl_->flat, impl_->s64); impl_->up64 = true; }
+    const DeviceScene<double>& ds = impl_->s64;
+    if (n == 0) return;
+    if (n > (1u << 30)) throw std::runtime_error("too many rays");
+    hipStream_t st = impl_->own_stream;
+    const size_t in_b = sizeof(double) * 7 * n, t_b = sizeof(double) * n, n_b = sizeof(double) * 3 * n;
+    char* base = static_cast<char*>(impl_->workspace(in_b + t_b + n_b));
+    double* d_rays = reinterpret_cast<double*>(base);
+    double* d_t = reinterpret_cast<double*>(base + in_b);
+    double* d_n = reinterpret_cast<double*>(base + in_b + t_b);
+    HIP_OK(hipMemcpyAsync(d_rays, rays, in_b, hipMemcpyHostToDevice, st));
+    const uint32_t stack = stack_rows(ds.max_stack), nn = static_cast<uint32_t>(n);
+    const uint32_t feat = ds.features;
+    if (ds.lds_scene && !global_scene && (feat & ~kFeatSpheres) == 0) {
+        const size_t lds = kLdsImageBytes + paths_stack_bytes(stack);
+        static const bool checked = static_lds_is_zero(reinterpret_cast<const void*>(k_trace_rays<kFeatSpheres, true>));
+        (void)checked;
+        (void)blocks_per_cu(reinterpret_cast<const void*>(k_trace_rays<kFeatSpheres, true>), kBlockL, lds);
+        hipLaunchKernelGGL((k_trace_rays<kFeatSpheres, true>), dim3((nn + kBlockL - 1) / kBlockL), dim3(kBlockL), lds, st, ds.view, d_rays, nn, stack, d_t, d_n);
+    } else {
+        const size_t lds = sizeof(int32_t) * stack * kBlock;
+        const dim3 grid((nn + kBlock - 1) / kBlock);
+        if ((feat & ~kFeatSpheres) == 0)
+            hipLaunchKernelGGL((k_trace_rays<kFeatSpheres, false>), grid, dim3(kBlock), lds, st, ds.view, d_rays, nn, stack, d_t, d_n);
+        else if ((feat & ~kFeatMesh) == 0)
+            hipLaunchKernelGGL((k_trace_rays<kFeatMesh, false>), grid, dim3(kBlock), lds, st, ds.view, d_rays, nn, stack, d_t, d_n);
+        else
+            hipLaunchKernelGGL((k_trace_rays<F_ALL, false>), grid, dim3(kBlock), lds, st, ds.view, d_rays, nn, stack, d_t, d_n);
+    }
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemcpyAsync(t_out, d_t, t_b, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(n_out, d_n, n_b, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
 }
 
 void Renderer::render(const CameraRec<double>& cam, const RenderParams& p, uint8_t* out_rgb, double* out_acc, RenderStats& stats) {

@@ -533,12 +533,8 @@ std::vector<int> build_mesh(SceneGraph& g, const ObjMesh& m) {
             if (!mm.map_kd.empty()) {
                 auto it = maps.find(mm.map_kd);
                 if (it == maps.end()) {
-                    const std::string img = m.dir + "/" + mm.map_kd;
-                    const std::string asset = texel_asset_path(img);
-                    if (asset.empty())
-                        throw std::runtime_error("texture map " + img + " has no pre-decoded texel asset (<stem>.rgb.gz or <stem>.rgb, "
-                                                 "oracle/ref_harness texture): JPEG/PNG decoding is not part of libart");
-                    it = maps.emplace(mm.map_kd, g.image_file(asset)).first;
+                    // material_map_handler (mesh.h:9-27): image_texture(dir + map_Kd), decoded from the file itself
+                    it = maps.emplace(mm.map_kd, g.image_file(m.dir + "/" + mm.map_kd)).first;
                 }
                 if (a.t < 0 || b.t < 0 || c.t < 0) throw std::runtime_error("textured mesh face without texture coordinates");
                 auto uv = [&](const ObjIndex& k, int cpt) { return static_cast<double>(m.texcoords[2 * static_cast<size_t>(k.t) + cpt]); };

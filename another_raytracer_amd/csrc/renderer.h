@@ -40,6 +40,9 @@ public:
     Renderer(const Renderer&) = delete;
     Renderer& operator=(const Renderer&) = delete;
     void render(const CameraRec<double>& cam, const RenderParams& p, uint8_t* out_rgb, double* out_acc, RenderStats& stats);
+    // Closest hit of n rays (rays: n x {ox, oy, oz, dx, dy, dz, tm}) through the renderer's traversal: t (inf on a
+    // miss) and the face normal (n x 3), host buffers; global_scene forces the HBM traversal on an LDS-image scene.
+    void trace_rays(const double* rays, size_t n, bool global_scene, double* t_out, double* n_out);
     size_t scene_bytes() const;
     const FlatScene& flat() const;
 

@@ -1,7 +1,9 @@
 // scene.cpp — scene graph builder, builtin scene recipes, canonical dump and compilation (see scene.h).
 #include "scene.h"
+#include "imagedec.h"
 
 #include <algorithm>
+#include <cctype>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -93,7 +95,21 @@ int SceneGraph::image(Image img) {
     return static_cast<int>(textures.size()) - 1;
 }
 int SceneGraph::image_file(const std::string& path) {
-    // raw texel asset (int32 w, h, bpp + bytes), optionally gzip-compressed (".gz"); gzread passes plain files through
+    // image_texture(filename) (texture.h:70-72 -> imageio::load_image = stbi_load(path, .., 0)): JPEG / PNG through
+    // imagedec.cpp, bytes as stb_image returns them
+    const size_t dot = path.find_last_of('.');
+    std::string ext = dot == std::string::npos ? std::string() : path.substr(dot);
+    for (char& ch : ext) ch = static_cast<char>(std::tolower(static_cast<unsigned char>(ch)));
+    if (ext == ".jpg" || ext == ".jpeg" || ext == ".png") {
+        DecodedImage d = load_image_file(path);
+        Image img;
+        img.w = d.w;
+        img.h = d.h;
+        img.bpp = d.channels;
+        img.data = std::move(d.data);
+        return image(std::move(img));
+    }
+    // otherwise a raw texel file (int32 w, h, bpp + bytes), optionally gzip-compressed; gzread passes plain files through
     gzFile f = gzopen(path.c_str(), "rb");
     if (!f) throw std::runtime_error("cannot open texture asset " + path);
     auto read = [&](void* dst, size_t n) {
@@ -447,7 +463,7 @@ void final_scene(SceneGraph& g, const std::string& assets) {  // scene_manager.c
     g.world.push_back(g.constant_medium(boundary, 0.2, g.solid(Vec3(0.2, 0.4, 0.9))));
     boundary = g.sphere(Vec3(0, 0, 0), 5000, g.dielectric(1.5));
     g.world.push_back(g.constant_medium(boundary, .0001, g.solid(Vec3(1, 1, 1))));
-    g.world.push_back(g.sphere(Vec3(400, 200, 400), 100, g.lambertian(g.image_file(assets + "/earthmap.rgb"))));
+    g.world.push_back(g.sphere(Vec3(400, 200, 400), 100, g.lambertian(g.image_file(assets + "/earthmap.jpg"))));
     int pertext = g.noise(0.1);
     g.world.push_back(g.sphere(Vec3(220, 280, 300), 80, g.lambertian(pertext)));
     std::vector<int> boxes2;
@@ -494,7 +510,7 @@ void build_builtin_scene(SceneGraph& g, const std::string& name, const std::stri
         g.world.push_back(g.sphere(Vec3(0, 2, 0), 2, g.lambertian(pertext)));
         cam(Vec3(13, 2, 3), Vec3(0, 0, 0), 20.0, 0.0, sky);
     } else if (name == "4" || name == "earth") {
-        g.world.push_back(g.sphere(Vec3(0, 0, 0), 2, g.lambertian(g.image_file(assets + "/earthmap.rgb"))));
+        g.world.push_back(g.sphere(Vec3(0, 0, 0), 2, g.lambertian(g.image_file(assets + "/earthmap.jpg"))));
         cam(Vec3(13, 2, 3), Vec3(0, 0, 0), 20.0, 0.0, sky);
     } else if (name == "5" || name == "simple_light") {
         int pertext = g.noise(4);

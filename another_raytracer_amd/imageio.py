@@ -1,5 +1,5 @@
 """imageio surface of the reference (src/utils/imageio.{h,cpp}): save_image writes a PNG (stdlib zlib encoder in
-place of stb_image_write), load_image reads PNGs written here and the raw texel assets (int32 w, h, bpp + bytes)."""
+place of stb_image_write); load_image decodes JPEG / PNG through libart (rt_image_load) and reads raw texel assets."""
 import struct
 import zlib
 
@@ -21,44 +21,22 @@ def save_image(path, width, height, bytes_per_pixel, data):  # imageio.cpp:17-20
     return True
 
 
-def load_image(path):  # imageio.cpp:11-15 -> (array (H, W, C) uint8)
-    with open(path, "rb") as f:
-        blob = f.read()
-    if blob[:8] != b"\x89PNG\r\n\x1a\n":
+def load_image(path):  # imageio.cpp:11-15 -> array (H, W, C) uint8
+    """stbi_load(path, .., 0): JPEG / PNG decoded by libart (rt_image_load, csrc/imagedec.cpp), native channels; a raw
+    texel asset (int32 w, h, bpp + bytes) is read as is."""
+    import ctypes
+    import os
+
+    from ._lib import check, lib
+    if os.fspath(path).endswith(".rgb"):
+        with open(path, "rb") as f:
+            blob = f.read()
         w, h, c = np.frombuffer(blob[:12], np.int32)
         return np.frombuffer(blob[12:], np.uint8)[: w * h * c].reshape(h, w, c).copy()
-    pos, idat, hdr = 8, b"", None
-    while pos < len(blob):
-        n, tag = struct.unpack(">I4s", blob[pos:pos + 8])
-        payload = blob[pos + 8:pos + 8 + n]
-        if tag == b"IHDR":
-            hdr = struct.unpack(">IIBBBBB", payload)
-        elif tag == b"IDAT":
-            idat += payload
-        pos += 12 + n
-    w, h, depth, ctype = hdr[0], hdr[1], hdr[2], hdr[3]
-    c = {0: 1, 2: 3, 4: 2, 6: 4}[ctype]
-    if depth != 8:
-        raise ValueError("only 8-bit PNGs are supported")
-    raw = np.frombuffer(zlib.decompress(idat), np.uint8).reshape(h, w * c + 1)
-    out = np.zeros((h, w * c), np.int32)
-    prev = np.zeros(w * c, np.int32)
-    for y in range(h):
-        f, line = raw[y, 0], raw[y, 1:].astype(np.int32)
-        cur = np.zeros(w * c, np.int32)
-        for x in range(w * c):
-            a = cur[x - c] if x >= c else 0
-            b = prev[x]
-            cc = prev[x - c] if x >= c else 0
-            if f == 0: v = line[x]
-            elif f == 1: v = line[x] + a
-            elif f == 2: v = line[x] + b
-            elif f == 3: v = line[x] + (a + b) // 2
-            else:
-                p = a + b - cc
-                pa, pb, pc = abs(p - a), abs(p - b), abs(p - cc)
-                v = line[x] + (a if pa <= pb and pa <= pc else b if pb <= pc else cc)
-            cur[x] = v & 0xFF
-        out[y] = cur
-        prev = cur
-    return out.astype(np.uint8).reshape(h, w, c)
+    w, h, c = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+    px = ctypes.POINTER(ctypes.c_uint8)()
+    check(lib.rt_image_load(os.fspath(path).encode(), ctypes.byref(w), ctypes.byref(h), ctypes.byref(c), ctypes.byref(px)), "load_image")
+    try:
+        return np.ctypeslib.as_array(px, shape=(h.value, w.value, c.value)).copy()
+    finally:
+        lib.rt_image_free(px)

@@ -319,7 +319,15 @@ class scene_manager:
         out = ctypes.c_void_p()
         check(lib.rt_scene_build(name.encode(), self.asset_dir.encode(), int(self.device), ctypes.byref(out)),
               f"scene_manager.build({alias})")
-        handle = _SceneHandle(out, self.device)
+        return self._wrap(_SceneHandle(out, self.device))
+
+    def load(self, path):
+        """A scene saved by save_scene (rt_scene_load: the flat-scene file, no rebuild)."""
+        out = ctypes.c_void_p()
+        check(lib.rt_scene_load(os.fspath(path).encode(), int(self.device), ctypes.byref(out)), f"scene_manager.load({path})")
+        return self._wrap(_SceneHandle(out, self.device))
+
+    def _wrap(self, handle):
         info = rt_scene_info()
         check(lib.rt_scene_info_get(handle, ctypes.byref(info)), "rt_scene_info_get")
         s = scene(tuple(info.lookfrom), tuple(info.lookat), info.vfov, info.aperture, tuple(info.background),
@@ -327,6 +335,14 @@ class scene_manager:
         s.info = {f: (tuple(getattr(info, f)) if isinstance(getattr(info, f), ctypes.Array) else getattr(info, f))
                   for f, _ in info._fields_}
         return s
+
+
+def save_scene(world, path):
+    """Writes a builtin / loaded scene (scene_manager result) as a versioned flat-scene file (rt_scene_save)."""
+    h = world.objects._native if isinstance(world, scene) else world._native
+    if h is None:
+        raise TypeError("save_scene takes a scene from scene_manager.build / load")
+    check(lib.rt_scene_save(h, os.fspath(path).encode()), "save_scene")
 
 
 def scene_dump(world):

@@ -130,6 +130,13 @@ int rt_scene_info_get(const rt_scene* scene, rt_scene_info* info);
 /* Canonical JSON of the scene graph (schema of oracle/ref_harness `dump`); returns the size needed incl. NUL. */
 size_t rt_scene_dump(const rt_scene* scene, char* buf, size_t cap);
 void rt_scene_destroy(rt_scene* scene);
+/* Versioned flat-scene files (csrc/scenefile.h): the compiled scene -- primitive records, SAH BVH4, objects, materials,
+ * textures and decoded texels, plus the scene_manager view -- written once and loaded (mmap) without re-parsing OBJ/MTL,
+ * re-decoding images or rebuilding the BVH (the reference rebuilds every run: scene_manager.cpp:260-355, mesh.h:31-145,
+ * bvh.cpp:3-42).  A loaded scene renders bit-identically to the one saved; it has no object graph (rt_scene_dump
+ * fails).  Wrong magic, version, record layout, size or checksum: RT_E_SCENE with the reason. */
+int rt_scene_save(const rt_scene* scene, const char* path);
+int rt_scene_load(const char* path, int device, rt_scene** out);
 
 /* ---- render (engine::run; the engine_mode is rt_params.flags & RT_ADAPTIVE: single, parallel_stripes and
  * parallel_images all compute every pixel and are one mode here) ----
@@ -146,8 +153,22 @@ int rt_render(rt_scene* scene, const rt_camera* cam, const rt_params* params, ui
 typedef int (*rt_progress_fn)(void* user, int32_t samples_done, int32_t spp, const uint8_t* rgb8, const double* accum);
 int rt_render_progressive(rt_scene* scene, const rt_camera* cam, const rt_params* params, uint8_t* out_rgb8, double* out_accum,
                           rt_progress_fn cb, void* user, rt_stats* stats);
+/* Ray queries: the world's closest hit (hittable_list::hit, hittable_list.cpp:5-19, t in [0.001, inf)) of n rays
+ * given as n x {ox, oy, oz, dx, dy, dz, time} doubles, through the renderer's own BVH traversal (the LDS scene image when
+ * the scene has one, unless flags has RT_GLOBAL_SCENE).  t_out: n hit distances (+inf on a miss); normal_out (may be
+ * NULL): n x 3 face normals as hit_record holds them (set_face_normal, hittable.h:18-22), 0 on a miss.  Ray i draws
+ * its constant_medium uniforms from the PCG stream keyed (seed 0, pixel i, sample 0).  Host buffers; blocking. */
+int rt_trace_rays(rt_scene* scene, const double* rays, int64_t n, int32_t flags, double* t_out, double* normal_out);
 /* Number of rows a band partition owns, and optionally their global indices (rows_out may be NULL). */
 int rt_local_rows(const rt_params* params, int32_t* rows_out);
+
+/* ---- images (imageio::load_image, imageio.cpp:11-15: stbi_load(path, &w, &h, &c, 0) of stb_image v2.27) ----
+ * Decodes a JPEG (baseline or progressive) or PNG file to 8-bit samples, native channel count, row 0 = top, the bytes
+ * stb_image returns (the JPEG inverse DCT, color transform and chroma upsampling follow its arithmetic).  *pixels is
+ * allocated by the library (h * w * channels bytes); release it with rt_image_free.  image_texture (texture.h:67-118)
+ * and map_Kd textures load their files through this decoder. */
+int rt_image_load(const char* path, int32_t* width, int32_t* height, int32_t* channels, uint8_t** pixels);
+void rt_image_free(uint8_t* pixels);
 
 /* ---- multi-GPU (one process, one host thread per GPU, RCCL) ----
  * Replaces the reference's CPU-parallel drivers (engine.h:335-376 _run_parallel_stripes: 4 threads on 4 row stripes;

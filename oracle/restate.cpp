@@ -1268,6 +1268,31 @@ int orc_render_rows(const char* scene, int W, int H, int spp, int max_depth, uin
     return -1;
 }
 
+int orc_trace_rays(const char* scene, const double* rays, long long n, double* t_out, double* normal_out) try {
+    Scene s;
+    Rng scene_rng;
+    build_scene(s, scene, scene_rng);
+    Rng rng;
+    rng.pcg = true;
+    for (long long i = 0; i < n; ++i) {
+        const double* q = rays + 7 * i;
+        Ray r{V3(q[0], q[1], q[2]), V3(q[3], q[4], q[5]), q[6]};
+        rng.state = pcg_seed(0, static_cast<uint32_t>(i), 0);
+        HitRec rec;
+        if (hit_list(s, s.world, r, 0.001, kInf, rec, rng)) {
+            t_out[i] = rec.t;
+            for (int a = 0; a < 3; ++a) normal_out[3 * i + a] = rec.normal[a];
+        } else {
+            t_out[i] = kInf;
+            for (int a = 0; a < 3; ++a) normal_out[3 * i + a] = 0.0;
+        }
+    }
+    return 0;
+} catch (const std::exception& e) {
+    g_err = e.what();
+    return -1;
+}
+
 // engine.h:96-333 (_run_adaptive), the 4 stripes one after another.  ORC_MT replays the reference's draw sequence
 // (a corner shared by two levels is traced again, from the continuing stream); ORC_PCG traces every distinct pixel
 // once (its (pixel, sample) streams would give the same value again), as the GPU does.

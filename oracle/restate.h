@@ -43,6 +43,11 @@ int orc_render(const char* scene, int W, int H, int spp, int max_depth, int mode
 int orc_render_rows(const char* scene, int W, int H, int spp, int max_depth, uint64_t seed, const int* rows, int nrows,
                     int threads, uint8_t* rgb_out, double* acc_out, long long* segments_out, double* ms_out);
 
+// hittable_list::hit (hittable_list.cpp:5-19) of the scene's world for n rays (n x {ox, oy, oz, dx, dy, dz, tm}),
+// t in [0.001, inf): t_out (+inf on a miss) and the hit_record normal (normal_out n x 3, 0 on a miss).  Ray i's
+// constant_medium draws come from the pcg stream pcg_seed(0, i, 0) -- the product's rt_trace_rays contract.
+int orc_trace_rays(const char* scene, const double* rays, long long n, double* t_out, double* normal_out);
+
 // engine_mode::adaptive (engine.h:96-333) over the whole WxH image (W, H multiples of 12).  ORC_MT: the
 // reference's draw sequence with its 4 stripes run one after another (bit-exact vs `ref_harness render .. adaptive`);
 // ORC_PCG: the product's streams, every distinct pixel traced once.  rgb_out: H*W*3 u8.  Returns -3 on a size the

@@ -16,6 +16,10 @@ fixtures pin:
                        sample sequences -- engine_mode::single, and parallel_stripes with 4 threads (its shared
                        global RNG) -- for the statistical parity test of the f64 GPU path (SURVEY.md §8(d)
                        tolerance 3: the pair's RMSE is the noise floor); `make_golden.py stat` makes only this
+  * images.npz         small JPEG / PNG files of every variant libart's decoder handles (baseline, progressive,
+                       4:4:4 / 4:2:2 / 4:2:0, grayscale, CMYK, restart intervals, extreme quantizers; PNG gray 1..16
+                       bits, palette +- tRNS, RGB(A), gray+alpha) made with PIL from a fixed pattern, each with the
+                       bytes the reference's stb_image decodes from it (`ref_harness texture`); `make_golden.py images`
   * render_adaptive_<scene>.npz  engine_mode::adaptive renders (engine.h:96-333, its 4 stripes run in order):
                        RGB8 and segment count (`python tests/golden/make_golden.py adaptive` makes only these)
 Assets written by the same harness: assets/*.tris (the reference's post-triangulation triangle lists: cow,
@@ -80,6 +84,61 @@ def stat_fixtures():
     print("stat", sc, info, info2)
 
 
+def image_fixtures():
+    import io
+
+    from PIL import Image
+    rng = np.random.default_rng(1)
+    W, H = 53, 37
+    yy, xx = np.mgrid[0:H, 0:W]
+    rgb = np.stack([(xx * 255 // W), (yy * 255 // H), ((xx + yy) * 4) % 256], -1).astype(np.int32)
+    rgb = np.clip(rgb + rng.integers(-40, 41, rgb.shape), 0, 255).astype(np.uint8)
+    gray = rgb.mean(-1).astype(np.uint8)
+    out = {}
+
+    def add(name, img, fmt, **kw):
+        buf = io.BytesIO()
+        img.save(buf, fmt, **kw)
+        data = buf.getvalue()
+        path = f"/tmp/golden_img_{name}"
+        with open(path, "wb") as f:
+            f.write(data)
+        run("texture", path, path + ".raw")
+        blob = open(path + ".raw", "rb").read()
+        w, h, c = np.frombuffer(blob[:12], np.int32)
+        dec = np.frombuffer(blob[12:], np.uint8)
+        out[f"{name}__file"] = np.frombuffer(data, np.uint8)
+        out[f"{name}__decoded"] = dec
+        out[f"{name}__whc"] = np.array([w, h, c], np.int32)
+        print("image", name, len(data), "bytes ->", w, h, c, len(dec))
+
+    im = Image.fromarray(rgb, "RGB")
+    add("jpg_444", im, "JPEG", quality=90, subsampling=0)
+    add("jpg_422", im, "JPEG", quality=85, subsampling=1)
+    add("jpg_420", im, "JPEG", quality=75, subsampling=2)
+    add("jpg_420_prog", im, "JPEG", quality=80, subsampling=2, progressive=True)
+    add("jpg_444_prog", im, "JPEG", quality=95, subsampling=0, progressive=True)
+    add("jpg_444_optimized", im, "JPEG", quality=70, subsampling=0, optimize=True)
+    add("jpg_q100", im, "JPEG", quality=100, subsampling=0)
+    add("jpg_q3", im, "JPEG", quality=3, subsampling=2)
+    add("jpg_restart", im, "JPEG", quality=85, subsampling=2, restart_marker_blocks=3)
+    add("jpg_restart_prog", im, "JPEG", quality=85, subsampling=0, progressive=True, restart_marker_rows=1)
+    add("jpg_gray", Image.fromarray(gray, "L"), "JPEG", quality=85)
+    add("jpg_gray_prog", Image.fromarray(gray, "L"), "JPEG", quality=85, progressive=True)
+    add("jpg_cmyk", im.convert("CMYK"), "JPEG", quality=90)
+    add("png_rgb", im, "PNG")
+    add("png_rgba", Image.fromarray(np.dstack([rgb, gray]), "RGBA"), "PNG")
+    add("png_gray", Image.fromarray(gray, "L"), "PNG")
+    add("png_la", Image.fromarray(np.dstack([gray, 255 - gray]), "LA"), "PNG")
+    add("png_gray1", Image.fromarray(gray > 128), "PNG")
+    add("png_pal", im.convert("P", palette=Image.ADAPTIVE, colors=16), "PNG")
+    add("png_pal_trns", im.convert("P", palette=Image.ADAPTIVE, colors=16), "PNG", transparency=3)
+    add("png_gray16", Image.fromarray((gray.astype(np.uint16) * 257 + 3).astype(np.uint16), "I;16"), "PNG")
+    pal4 = im.convert("P", palette=Image.ADAPTIVE, colors=4)
+    add("png_pal2bit", pal4, "PNG", bits=2)
+    np.savez_compressed(os.path.join(HERE, "images.npz"), **out)
+
+
 def scene_fixtures(sc):
     """probe + dump hash (scenes.json entry) and the SMALL render of one scene."""
     # the harness may log texture loads on stdout first: the values are the last 8 lines
@@ -118,6 +177,9 @@ def main():
     if sys.argv[1:] == ["stat"]:
         stat_fixtures()
         return
+    if sys.argv[1:] == ["images"]:
+        image_fixtures()
+        return
     if sys.argv[1:2] == ["scene"]:
         path = os.path.join(HERE, "scenes.json")
         scenes = json.load(open(path))
@@ -143,6 +205,7 @@ def main():
     print(sc, info)
     adaptive_fixtures()
     stat_fixtures()
+    image_fixtures()
 
 
 if __name__ == "__main__":

@@ -65,6 +65,20 @@ def oracle_render_rows(scene, W, H, spp, rows, seed=0, threads=0, max_depth=50):
     return {"rgb": rgb, "acc": acc, "segments": segs.value, "ms": ms.value}
 
 
+def oracle_trace_rays(scene, rays):
+    """Closest hits (t, normals) of rays (n x 7: o, d, tm) in the scene's world (hittable_list::hit)."""
+    lib = oracle()
+    rays = np.ascontiguousarray(rays, dtype=np.float64)
+    n = len(rays)
+    t = np.zeros(n, np.float64)
+    nrm = np.zeros((n, 3), np.float64)
+    r = lib.orc_trace_rays(str(scene).encode(), rays.ctypes.data_as(ctypes.c_void_p), ctypes.c_longlong(n),
+                           t.ctypes.data_as(ctypes.c_void_p), nrm.ctypes.data_as(ctypes.c_void_p))
+    if r != 0:
+        raise RuntimeError(lib.orc_last_error().decode())
+    return t, nrm
+
+
 def oracle_render_adaptive(scene, W, H, spp, mode="pcg", seed=0, threads=0, max_depth=50):
     lib = oracle()
     rgb = np.zeros((H, W, 3), np.uint8)

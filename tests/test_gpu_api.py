@@ -189,3 +189,21 @@ def test_progressive_callback_can_stop_early(gpu):
     r4 = np.zeros((H, W, 3), np.uint8)
     four.run(r4)
     assert np.array_equal(img, r4)
+
+
+@pytest.mark.parametrize("name", ["1", "9", "8"])
+def test_loaded_scene_renders_bit_identically(gpu, name, tmp_path):
+    # rt_scene_save -> rt_scene_load (no OBJ parse, no image decode, no BVH build): the same frame, bit for bit
+    W, H, spp = 64, 40, 4
+    built = art.scene_manager().build(name)
+    art.save_scene(built, tmp_path / "s.artscene")
+    frames = []
+    for w in (built, art.scene_manager().load(tmp_path / "s.artscene")):
+        cam = art.camera(w.lookfrom, w.lookat, (0, 1, 0), w.vfov, W / H, w.aperture, 10.0, 0.0, 1.0)
+        e = art.engine(cam, art.engine_mode.single, width=W, height=H, samples_per_pixel=spp)
+        e.set_scene(w.objects, w.background)
+        img = np.zeros((H, W, 3), np.uint8)
+        acc = np.zeros((H, W, 3), np.float64)
+        e.run(img, accum=acc)
+        frames.append((img, acc, e.stats["segments"]))
+    assert np.array_equal(frames[0][0], frames[1][0]) and np.array_equal(frames[0][1], frames[1][1]) and frames[0][2] == frames[1][2]
