@@ -10,6 +10,7 @@
 #include <cstdint>
 #include <type_traits>
 
+#include "glibc_log.h"
 #include "layout.h"
 
 namespace art {
@@ -91,7 +92,7 @@ __device__ __forceinline__ R uniform(uint64_t& s) {
     return static_cast<R>(x >> 8) * static_cast<R>(1.0 / 16777216.0);
 }
 template <class R> __device__ __forceinline__ R uniform(uint64_t& s, R lo, R hi) { return lo + (hi - lo) * uniform<R>(s); }
-// The 24-bit integer k of the next uniform (uniform<R> == k * 2^-24): indexes DevScene::log_tab.
+// The 24-bit integer k of the next uniform (uniform<R> == k * 2^-24): the argument of glibc_log in hit_medium.
 __device__ __forceinline__ uint32_t uniform_k(uint64_t& s) {
     const uint64_t old = s;
     s = old * 6364136223846793005ull + 1442695040888963407ull;
@@ -226,7 +227,6 @@ struct DevScene {
     const ImageRec* images;
     const uint8_t* texels;
     const uint8_t* lds_image;   // layout.h LDS scene image (nullptr unless the scene qualifies)
-    const double* log_tab;      // scenes with media: log_tab[k] = the C library's log(k * 2^-24), k < 2^24 (hit_medium)
     int32_t nworld;
     R bg[3];
 };
@@ -828,6 +828,9 @@ __device__ __forceinline__ bool hit_object(const DevScene<R>& S, const uint8_t* 
     return traverse<R, F, B, L>(S, lds, o.a, r, tmin, tmax, stk, t, prim, face, mt);
 }
 
+// Out of line: measured +0.2 % (cow) to +1.8 % (Next-Week final) over the inlined body, which raised the register
+// pressure of the whole path loop for a function most segments do not reach.
+static __device__ __noinline__ double glibc_log_call(double x) { return glibc_log(x); }
 // constant_medium.h:37-82.  Consumes one uniform when the clamped interval is non-empty.
 template <class R, uint32_t F, int B, bool L>
 __device__ __forceinline__ bool hit_medium(const DevScene<R>& S, const uint8_t* lds, const ObjRec<R>& m, const Ray<R>& r, R tmin, R tmax,
@@ -874,10 +877,10 @@ __device__ __forceinline__ bool hit_medium(const DevScene<R>& S, const uint8_t* 
     const R ray_length = sqrt_rn(len2(r.d));
     const R inside = (t2 - t1) * ray_length;
     // log(random_double()) of constant_medium.h:61 is the C library's log (glibc) in the reference; the device's own
-    // f64 log differs from it in the last bit for 445 762 of the 2^24 arguments a uniform can take (tools/log_check),
-    // which moves a scattering path's t and every sum after it.  The uniform's integer k indexes a table of glibc's
-    // values built on the host (build_device_scene), so every draw gives the reference's bits.
-    const R hit_distance = m.p[0] * S.log_tab[uniform_k(rng)];
+    // f64 log differs from it in the last bit for 445 762 of the 2^24 arguments a uniform can take, which moves a
+    // scattering path's t and every sum after it.  glibc_log.h restates glibc's log operation by operation (equal for
+    // every k * 2^-24); it replaced a 128 MiB table of glibc's values, whose random reads (an L2 miss per draw) cost 5-10 % on the medium scenes.
+    const R hit_distance = m.p[0] * glibc_log_call(static_cast<double>(uniform_k(rng)) * 0x1p-24);
     if (hit_distance > inside) return false;
     t = t1 + hit_distance / ray_length;
     return true;

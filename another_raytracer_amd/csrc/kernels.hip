@@ -752,13 +752,29 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S, PassGe
 __device__ long long g_trace_pixel = -1, g_trace_sample = -1;
 #define ART_DBITS(x) static_cast<unsigned long long>(__double_as_longlong(x))
 #endif
+__host__ __device__ constexpr size_t paths_g_stack_bytes(uint32_t stack) { return sizeof(StackT<false>) * stack * kBlock; }
+__host__ __device__ constexpr size_t paths_g_lds_bytes(uint32_t stack) {
+    return paths_g_stack_bytes(stack) + sizeof(CameraRec<double>) + sizeof(PassGeom);
+}
 template <uint32_t F, uint32_t TF>
 __global__ __launch_bounds__(kBlock, ART_PATHS_G_WAVES) void k_paths_g(DevScene<double> S, PassGeom g, CameraRec<double> cam, Work<double> w, uint32_t* next_slot) {
     using R = double;
     constexpr int B = kBlock;
-    extern __shared__ __align__(16) uint8_t smem[];  // traversal stack: g.stack entries x B lanes (+ sentinel row)
+    // dynamic LDS: [traversal stack: g.stack entries x B lanes (+ sentinel row)][camera][pass geometry] -- as in
+    // k_paths, the camera and pass geometry are read from LDS where a path starts (as kernel arguments held in
+    // SGPRs for the whole loop they spilled ~100 SGPRs into VGPR lanes)
+    extern __shared__ __align__(16) uint8_t smem[];
     StackT<false>* stk = reinterpret_cast<StackT<false>*>(smem) + B + threadIdx.x;
+    CameraRec<double>& s_cam = *reinterpret_cast<CameraRec<double>*>(smem + paths_g_stack_bytes(g.stack));
+    PassGeom& s_g = *reinterpret_cast<PassGeom*>(smem + paths_g_stack_bytes(g.stack) + sizeof(CameraRec<double>));
     stk[-B] = static_cast<StackT<false>>(kNodeEmpty);
+    if (threadIdx.x == 0) {
+        s_cam = cam;
+        s_g = g;
+    }
+    const uint32_t P = g.P;
+    const int max_depth = g.max_depth;
+    __syncthreads();
     const uint32_t lane = __lane_id();
     const uint64_t below = (1ull << lane) - 1ull;
     const V3<R> bg = mk(S.bg[0], S.bg[1], S.bg[2]);
@@ -790,18 +806,19 @@ __global__ __launch_bounds__(kBlock, ART_PATHS_G_WAVES) void k_paths_g(DevScene<
                 cur += n;
             }
             if (!busy && !drained) {
-                if (slot >= g.P) {
+                if (slot >= P) {
                     drained = true;
                 } else {
                     int lx, ly;
                     q = slot;
-                    if (slot_pixel(g, slot - g.fd_npix.div(slot) * g.npix_pad, lx, ly)) {
-                        gen_ray(g, cam, q, lx, ly, st);
+                    __asm__ volatile("" ::: "memory");  // keep the LDS camera/geometry loads here (see k_paths)
+                    if (slot_pixel(s_g, slot - s_g.fd_npix.div(slot) * s_g.npix_pad, lx, ly)) {
+                        gen_ray(s_g, s_cam, q, lx, ly, st);
                         busy = true;
                         depth = 0;
 #ifdef ART_TRACE
-                        tracing = static_cast<long long>(global_row(g, ly)) * g.W + lx == g_trace_pixel &&
-                                  static_cast<long long>(g.sample_base + g.fd_npix.div(slot)) == g_trace_sample;
+                        tracing = static_cast<long long>(global_row(s_g, ly)) * s_g.W + lx == g_trace_pixel &&
+                                  static_cast<long long>(s_g.sample_base + s_g.fd_npix.div(slot)) == g_trace_sample;
 #endif
                     }
                 }
@@ -834,7 +851,7 @@ __global__ __launch_bounds__(kBlock, ART_PATHS_G_WAVES) void k_paths_g(DevScene<
                 const MatRec<R>& mat = S.mats[s.mat];
                 if (mat.type == MAT_LIGHT) {  // material.h:114-116; diffuse_light never scatters
                     st.L = st.L + st.T * tex_value<R, TF>(S, mat.tex, s.u, s.v, s.p);
-                } else if (depth + 1 < g.max_depth) {
+                } else if (depth + 1 < max_depth) {
                     V3<R> att, dir;
                     bool sc = false;
                     switch (mat.type) {
@@ -1264,17 +1281,6 @@ static std::vector<uint8_t> lds_scene_image(const FlatScene& f, uint32_t& nmov, 
     return img;
 }
 
-// glibc's log of every uniform the RNG contract can produce, (k * 2^-24) for k < 2^24 (device.h hit_medium): 128 MiB,
-// computed once per process on first use by a scene with media and uploaded once per device.
-static const std::vector<double>& log_table() {
-    static const std::vector<double> tab = [] {
-        std::vector<double> t(size_t(1) << 24);
-        for (size_t k = 0; k < t.size(); ++k) t[k] = std::log(static_cast<double>(k) * (1.0 / 16777216.0));
-        return t;
-    }();
-    return tab;
-}
-
 template <class R>
 static void build_device_scene(const FlatScene& f, DeviceScene<R>& ds) {
     std::vector<SphereRec<R>> sph(f.spheres.size());
@@ -1343,7 +1349,6 @@ static void build_device_scene(const FlatScene& f, DeviceScene<R>& ds) {
             ds.lds_shade = shade_ok;
         }
     }
-    if (f.has_media) ds.view.log_tab = ds.upload(log_table());
     ds.view.nworld = static_cast<int32_t>(f.world.size());
     for (int a = 0; a < 3; ++a) ds.view.bg[a] = R(f.background[a]);
     ds.media = f.has_media;
@@ -1521,7 +1526,7 @@ static int extend_variant(const DeviceScene<R>& ds, int flags) {
 template <uint32_t F, uint32_t TF>
 static void launch_paths_g_ft(int num_cu, hipStream_t st, const DevScene<double>& S, const PassGeom& g, const CameraRec<double>& cam,
                               const Work<double>& w, uint32_t* next_slot) {
-    const size_t lds = sizeof(int32_t) * g.stack * kBlock;  // stack_rows: sentinel + entries + spare row
+    const size_t lds = paths_g_lds_bytes(g.stack);  // stack_rows: sentinel + entries + spare row
     const int blocks = blocks_per_cu(reinterpret_cast<const void*>(k_paths_g<F, TF>), kBlock, lds) * num_cu;
     hipLaunchKernelGGL((k_paths_g<F, TF>), dim3(blocks), dim3(kBlock), lds, st, S, g, cam, w, next_slot);
 }
