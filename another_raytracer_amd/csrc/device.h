@@ -227,6 +227,7 @@ struct DevScene {
     const ImageRec* images;
     const uint8_t* texels;
     const uint8_t* lds_image;   // layout.h LDS scene image (nullptr unless the scene qualifies)
+    uint32_t n_nodes, n_primrefs, n_tris;  // array lengths (k_paths_g's LDS copy of a small mesh scene)
     int32_t nworld;
     R bg[3];
 };

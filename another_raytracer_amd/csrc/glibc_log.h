@@ -17,25 +17,25 @@
 #include "glibc_log_data.h"
 
 #if defined(__HIPCC__)
-#define ART_HD __host__ __device__
+#define ART_LOG_HD __host__ __device__
 #else
-#define ART_HD
+#define ART_LOG_HD
 #endif
 
 namespace art {
 
-ART_HD inline uint64_t f64_bits(double x) {
+ART_LOG_HD inline uint64_t f64_bits(double x) {
     uint64_t u;
     std::memcpy(&u, &x, sizeof u);
     return u;
 }
-ART_HD inline double f64_from(uint64_t u) {
+ART_LOG_HD inline double f64_from(uint64_t u) {
     double x;
     std::memcpy(&x, &u, sizeof x);
     return x;
 }
 
-ART_HD inline double glibc_log(double x) {
+ART_LOG_HD inline double glibc_log(double x) {
     using namespace glibc_log_data;
     const uint64_t ix = f64_bits(x);
     if (ix - 0x3fee000000000000ull < 0x3090000000000ull) {  // 1 - 2^-4 <= x < 1 + 0x1.09p-4: the near-1 polynomial

@@ -665,6 +665,9 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S, PassGe
     int depth = 0;
     PathState<R> st;
     unsigned long long segs = 0;
+#ifdef ART_STATS
+    unsigned long long tm_load = 0, tm_trace = 0, tm_shade = 0, tm_app = 0, tm_prev = __builtin_amdgcn_s_memtime();
+#endif
     for (;;) {
         // every idle lane takes the next slot of the wave's chunk (padding slots of partial tiles stay idle a round)
         const uint64_t idle = __ballot(!busy && !drained);
@@ -701,6 +704,7 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S, PassGe
                 }
             }
         }
+        ART_TICK(tm_load);
         if (__ballot(busy) == 0) {
             if (__ballot(!drained) == 0) break;
             continue;
@@ -712,6 +716,7 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S, PassGe
             ++segs;
             hitw = trace_world<R, kFeatSpheres, B, true>(S, lds, st.ray, stk, st.rng, t, h);
         }
+        ART_TICK(tm_trace);
         // the whole wave draws random_in_unit_sphere for its lambertian and metal hits (material.h:33, :55), which
         // scatter with it first; lights and the max_depth bounce draw nothing
         const bool need = busy && hitw && (h.mt == MAT_LAMBERTIAN || h.mt == MAT_METAL) && depth + 1 < g.max_depth;
@@ -723,6 +728,7 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S, PassGe
             } else {  // engine.h:455-456: miss -> background
                 st.L = st.L + st.T * bg;
             }
+            ART_TICK(tm_shade);
             if (cont) {
                 ++depth;
             } else {
@@ -730,9 +736,18 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S, PassGe
                 busy = false;
             }
         }
+        ART_TICK(tm_app);
     }
     for (int off = 32; off > 0; off >>= 1) segs += __shfl_xor(segs, off);
     if (lane == 0) atomicAdd(w.segments, segs);
+#ifdef ART_STATS
+    if (lane == 0) {
+        atomicAdd(&g_art_stats[8], tm_load);
+        atomicAdd(&g_art_stats[9], tm_trace);
+        atomicAdd(&g_art_stats[10], tm_shade);
+        atomicAdd(&g_art_stats[11], tm_app);
+    }
+#endif
 }
 
 #endif  // ART_SPLIT_PATHS != 1
@@ -743,6 +758,9 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S, PassGe
 // the material's scatter (the k_shade arithmetic, one switch over the material type instead of one launch per type),
 // so the RNG draws and every f64 operation are those of the wavefront kernels and images are bit-identical to them.
 // F / TF: the scene's primitive and texture features (smallest instantiation that covers them).
+#ifndef ART_LDS_MESH
+#define ART_LDS_MESH 1  // k_paths_g with the mesh arrays in LDS when they fit (LM)
+#endif
 #ifndef ART_PATHS_G_WAVES
 #define ART_PATHS_G_WAVES 3  // 3 waves per SIMD (<= 168 VGPRs): measured best over 2 and 4 (cow +22 %, final +18 %, dino +21 % over 2)
 #endif
@@ -752,25 +770,57 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S, PassGe
 __device__ long long g_trace_pixel = -1, g_trace_sample = -1;
 #define ART_DBITS(x) static_cast<unsigned long long>(__double_as_longlong(x))
 #endif
-__host__ __device__ constexpr size_t paths_g_stack_bytes(uint32_t stack) { return sizeof(StackT<false>) * stack * kBlock; }
-__host__ __device__ constexpr size_t paths_g_lds_bytes(uint32_t stack) {
-    return paths_g_stack_bytes(stack) + sizeof(CameraRec<double>) + sizeof(PassGeom);
+// LM (LDS BVH): a scene whose BVH nodes and primitive references -- and triangles, for a kernel with triangles --
+// fit beside the stacks (small meshes: dino; the Next-Week final's 559 nodes) runs one 768-lane block per CU with
+// those arrays copied into LDS: node and triangle fetches at LDS latency instead of L2's.  The other arrays stay in
+// HBM.  The copies are plain LDS arrays reached through the DevScene pointers: the compiler infers their address
+// space (ds_read, no flat loads).
+constexpr int kBlockM = 768;
+constexpr size_t kPathsGLdsCap = 160 * 1024;
+__host__ __device__ constexpr size_t align16(size_t x) { return (x + 15u) & ~size_t(15); }
+__host__ __device__ constexpr size_t paths_g_stack_bytes(uint32_t stack, int block) { return sizeof(StackT<false>) * stack * block; }
+__host__ __device__ constexpr size_t paths_g_head_bytes(uint32_t stack, int block) {  // stack, camera, pass geometry
+    return align16(paths_g_stack_bytes(stack, block) + sizeof(CameraRec<double>) + sizeof(PassGeom));
 }
-template <uint32_t F, uint32_t TF>
-__global__ __launch_bounds__(kBlock, ART_PATHS_G_WAVES) void k_paths_g(DevScene<double> S, PassGeom g, CameraRec<double> cam, Work<double> w, uint32_t* next_slot) {
+__host__ __device__ constexpr size_t paths_g_mesh_bytes(uint32_t n_nodes, uint32_t n_primrefs, uint32_t n_tris) {  // n_tris: 0 unless F_TRI
+    return sizeof(BvhNode) * n_nodes + align16(sizeof(uint32_t) * n_primrefs) + sizeof(TriRec<double>) * n_tris;
+}
+template <uint32_t F, uint32_t TF, bool LM>
+__global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) void k_paths_g(DevScene<double> S0, PassGeom g, CameraRec<double> cam,
+                                                                                     Work<double> w, uint32_t* next_slot) {
     using R = double;
-    constexpr int B = kBlock;
-    // dynamic LDS: [traversal stack: g.stack entries x B lanes (+ sentinel row)][camera][pass geometry] -- as in
-    // k_paths, the camera and pass geometry are read from LDS where a path starts (as kernel arguments held in
-    // SGPRs for the whole loop they spilled ~100 SGPRs into VGPR lanes)
+    constexpr int B = LM ? kBlockM : kBlock;
+    // dynamic LDS: [traversal stack: g.stack entries x B lanes (+ sentinel row)][camera][pass geometry][LM: nodes,
+    // primrefs, triangles] -- as in k_paths, the camera and pass geometry are read from LDS where a path starts (as
+    // kernel arguments held in SGPRs for the whole loop they spilled ~100 SGPRs into VGPR lanes)
     extern __shared__ __align__(16) uint8_t smem[];
     StackT<false>* stk = reinterpret_cast<StackT<false>*>(smem) + B + threadIdx.x;
-    CameraRec<double>& s_cam = *reinterpret_cast<CameraRec<double>*>(smem + paths_g_stack_bytes(g.stack));
-    PassGeom& s_g = *reinterpret_cast<PassGeom*>(smem + paths_g_stack_bytes(g.stack) + sizeof(CameraRec<double>));
+    CameraRec<double>& s_cam = *reinterpret_cast<CameraRec<double>*>(smem + paths_g_stack_bytes(g.stack, B));
+    PassGeom& s_g = *reinterpret_cast<PassGeom*>(smem + paths_g_stack_bytes(g.stack, B) + sizeof(CameraRec<double>));
     stk[-B] = static_cast<StackT<false>>(kNodeEmpty);
     if (threadIdx.x == 0) {
         s_cam = cam;
         s_g = g;
+    }
+    DevScene<double> S = S0;
+    if constexpr (LM) {
+        uint8_t* m = smem + paths_g_head_bytes(g.stack, B);
+        const size_t nb = sizeof(BvhNode) * S0.n_nodes, pb = align16(sizeof(uint32_t) * S0.n_primrefs);
+        const size_t tb = (F & F_TRI) ? sizeof(TriRec<double>) * S0.n_tris : 0;
+        auto copy = [&](uint8_t* dst, const void* src, size_t bytes) {
+            const uint4* s4 = static_cast<const uint4*>(src);
+            uint4* d4 = reinterpret_cast<uint4*>(dst);
+            for (size_t i = threadIdx.x; i < bytes / 16; i += B) d4[i] = s4[i];
+        };
+        copy(m, S0.nodes, nb);
+        // primrefs: 4-B entries, the tail of the last 16-B word comes from past the array's end -- copy word-wise
+        for (uint32_t i = threadIdx.x; i < S0.n_primrefs; i += B) reinterpret_cast<uint32_t*>(m + nb)[i] = S0.primrefs[i];
+        S.nodes = reinterpret_cast<const BvhNode*>(m);
+        S.primrefs = reinterpret_cast<const uint32_t*>(m + nb);
+        if constexpr ((F & F_TRI) != 0) {
+            copy(m + nb + pb, S0.tris, tb);
+            S.tris = reinterpret_cast<const TriRec<double>*>(m + nb + pb);
+        }
     }
     const uint32_t P = g.P;
     const int max_depth = g.max_depth;
@@ -786,6 +836,9 @@ __global__ __launch_bounds__(kBlock, ART_PATHS_G_WAVES) void k_paths_g(DevScene<
     unsigned long long segs = 0;
 #ifdef ART_TRACE
     bool tracing = false;
+#endif
+#ifdef ART_STATS
+    unsigned long long tm_load = 0, tm_trace = 0, tm_shade = 0, tm_app = 0, tm_prev = __builtin_amdgcn_s_memtime();
 #endif
     for (;;) {
         const uint64_t idle = __ballot(!busy && !drained);
@@ -824,6 +877,7 @@ __global__ __launch_bounds__(kBlock, ART_PATHS_G_WAVES) void k_paths_g(DevScene<
                 }
             }
         }
+        ART_TICK(tm_load);
         if (__ballot(busy) == 0) {
             if (__ballot(!drained) == 0) break;
             continue;
@@ -839,7 +893,9 @@ __global__ __launch_bounds__(kBlock, ART_PATHS_G_WAVES) void k_paths_g(DevScene<
                        ART_DBITS(st.ray.o.y), ART_DBITS(st.ray.o.z), ART_DBITS(st.ray.d.x), ART_DBITS(st.ray.d.y), ART_DBITS(st.ray.d.z),
                        ART_DBITS(st.ray.tm), static_cast<unsigned long long>(st.rng));
 #endif
-            if (trace_world<R, F, B, false>(S, nullptr, st.ray, stk, st.rng, t, h)) {
+            const bool hitw = trace_world<R, F, B, false>(S, nullptr, st.ray, stk, st.rng, t, h);
+            ART_TICK(tm_trace);
+            if (hitw) {
                 Surf<R> s;
                 world_surface<R, F, (TF & TF_IMAGE) != 0>(S, h, st.ray, t, s);
 #ifdef ART_TRACE
@@ -874,6 +930,7 @@ __global__ __launch_bounds__(kBlock, ART_PATHS_G_WAVES) void k_paths_g(DevScene<
 #endif
                 st.L = st.L + st.T * bg;
             }
+            ART_TICK(tm_shade);
             if (cont) {
                 ++depth;
             } else {
@@ -881,9 +938,18 @@ __global__ __launch_bounds__(kBlock, ART_PATHS_G_WAVES) void k_paths_g(DevScene<
                 busy = false;
             }
         }
+        ART_TICK(tm_app);
     }
     for (int off = 32; off > 0; off >>= 1) segs += __shfl_xor(segs, off);
     if (lane == 0) atomicAdd(w.segments, segs);
+#ifdef ART_STATS
+    if (lane == 0) {
+        atomicAdd(&g_art_stats[8], tm_load);
+        atomicAdd(&g_art_stats[9], tm_trace);
+        atomicAdd(&g_art_stats[10], tm_shade);
+        atomicAdd(&g_art_stats[11], tm_app);
+    }
+#endif
 }
 
 // Input: the kShards shards of material queue M at depth d (the extend stage sorted hits by material type).
@@ -1349,6 +1415,9 @@ static void build_device_scene(const FlatScene& f, DeviceScene<R>& ds) {
             ds.lds_shade = shade_ok;
         }
     }
+    ds.view.n_nodes = static_cast<uint32_t>(f.nodes.size());
+    ds.view.n_primrefs = static_cast<uint32_t>(f.primrefs.size());
+    ds.view.n_tris = static_cast<uint32_t>(f.tris.size());
     ds.view.nworld = static_cast<int32_t>(f.world.size());
     for (int a = 0; a < 3; ++a) ds.view.bg[a] = R(f.background[a]);
     ds.media = f.has_media;
@@ -1526,9 +1595,20 @@ static int extend_variant(const DeviceScene<R>& ds, int flags) {
 template <uint32_t F, uint32_t TF>
 static void launch_paths_g_ft(int num_cu, hipStream_t st, const DevScene<double>& S, const PassGeom& g, const CameraRec<double>& cam,
                               const Work<double>& w, uint32_t* next_slot) {
-    const size_t lds = paths_g_lds_bytes(g.stack);  // stack_rows: sentinel + entries + spare row
-    const int blocks = blocks_per_cu(reinterpret_cast<const void*>(k_paths_g<F, TF>), kBlock, lds) * num_cu;
-    hipLaunchKernelGGL((k_paths_g<F, TF>), dim3(blocks), dim3(kBlock), lds, st, S, g, cam, w, next_slot);
+    // g.stack = stack_rows: sentinel + entries + spare row
+    const size_t lds_m = paths_g_head_bytes(g.stack, kBlockM) + paths_g_mesh_bytes(S.n_nodes, S.n_primrefs, (F & F_TRI) ? S.n_tris : 0u);
+#if ART_LDS_MESH
+    if (S.n_nodes > 0 && lds_m <= kPathsGLdsCap) {
+        const int blocks = blocks_per_cu(reinterpret_cast<const void*>(k_paths_g<F, TF, true>), kBlockM, lds_m) * num_cu;
+        hipLaunchKernelGGL((k_paths_g<F, TF, true>), dim3(blocks), dim3(kBlockM), lds_m, st, S, g, cam, w, next_slot);
+        return;
+    }
+#else
+    (void)lds_m;
+#endif
+    const size_t lds = paths_g_head_bytes(g.stack, kBlock);
+    const int blocks = blocks_per_cu(reinterpret_cast<const void*>(k_paths_g<F, TF, false>), kBlock, lds) * num_cu;
+    hipLaunchKernelGGL((k_paths_g<F, TF, false>), dim3(blocks), dim3(kBlock), lds, st, S, g, cam, w, next_slot);
 }
 static void launch_paths_g(uint32_t feat, bool tex_basic, int num_cu, hipStream_t st, const DevScene<double>& S, const PassGeom& g,
                            const CameraRec<double>& cam, const Work<double>& w, uint32_t* next_slot) {
@@ -1806,7 +1886,7 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
                      st[0], st[1], st[1] / (64.0 * st[0]), st[2], st[3], st[3] / (64.0 * st[2]), st[4], st[5], st[5] / (64.0 * st[4]), st[6],
                      double(st[1]) / st[6], double(st[3]) / st[6]);
         const double tt = double(st[8] + st[9] + st[10] + st[11]);
-        if (tt > 0) std::fprintf(stderr, "ART_STATS k_extend cycles: load %.3f trace %.3f shade %.3f append %.3f\n", st[8] / tt, st[9] / tt, st[10] / tt, st[11] / tt);
+        if (tt > 0) std::fprintf(stderr, "ART_STATS cycles: load/claim %.3f trace %.3f shade %.3f append/store %.3f\n", st[8] / tt, st[9] / tt, st[10] / tt, st[11] / tt);
         std::memset(st, 0, sizeof st);
         HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(g_art_stats), st, sizeof st));
     }

@@ -9,10 +9,13 @@ max-over-ranks wall time of the K timed steps.  A segment is one ray traced thro
 engine.h:453), counted exactly on the device from the wavefront queue sizes.
 
 Extra fields:
-  roofline      dominant kernel (k_paths / k_paths_g, or k_extend for the per-depth variants): SURVEY.md §8(d) algorithmic bytes
-                (128 B per segment + 12 B per pixel + the flat scene once per launch) / summed launch time measured live
-                with HIP events on the render stream during the timed steps; HBM peak 8 TB/s.  moved_bytes_per_segment
-                is what the variant really moves by construction.
+  roofline      dominant kernel (k_paths / k_paths_g, or k_extend for the per-depth variants), timed live with HIP events
+                on the render stream during the timed steps.  The persistent path kernels are VALU-issue / divergence
+                bound: bound "valu", achieved = VALU lane-instruction slots issued per second (the newest
+                committed PMC summary's wave-instructions per segment x 64 x this run's segments / kernel time), peak
+                78.6 T/s (2 cycles per wave-instruction per SIMD at 2.4 GHz), lane_util from the same summary; the
+                SURVEY.md §8(d) HBM figure (128 B per segment + 12 B per pixel + the flat scene once per launch, vs
+                8 TB/s) sits under `hbm`.  Without a PMC summary for the scene/variant the HBM figure is the roofline.
                 `traffic` = FETCH_SIZE*2 + WRITE_SIZE per segment from the committed rocprofv3 PMC summary
                 (profiles/, MI355X_MICROARCH.md "HBM") scaled to this run, or null.
   cpu_baseline  the reference itself (oracle/_ref/ref_harness = /root/reference/src compiled unmodified), its own
@@ -32,6 +35,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# MI355X_MICROARCH.md: a wave issues one VALU instruction per 2 cycles per SIMD (64 lanes), 256 CUs x 4 SIMDs at the
+# 2.4 GHz max clock: 78.6 T lane-instructions/s (x 2 flops per FMA = the guide's 157.3 TF f32 vector peak)
+VALU_PEAK_TLANE = 256 * 4 * 64 / 2 * 2.4e9 / 1e12
 # algorithmic bytes of the path = 128 B per segment (a 64-B fp32 path record read once and written
 # once per bounce) + 12 B per pixel (f32 RGB accumulator write) + one pass over the flat scene.  The same figure for
 # every kernel variant, so `achieved` compares variants and rounds on one scale.
@@ -137,6 +143,23 @@ def cpu_baseline(args, repeats=3):
     except Exception as e:  # the port is optional evidence: report, do not fail the bench
         res["all_cores"] = {"error": str(e)[-300:]}
     return res
+
+
+def latest_pmc(precision, scene, variant):
+    """The newest committed PMC summary (tools/pmc_summary.py format: per-segment wave-instruction counts of the
+    dominant kernel) for this scene and extend variant, or None."""
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):  # tags sort by round and letter
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        k = d.get("dominant_kernel")
+        if (d.get("precision") == precision and str(d.get("scene")) == str(scene) and d.get("extend_variant") == variant and k
+                and (d.get("kernels", {}).get(k, {}).get("per_segment_wave_instructions"))):
+            d["_file"] = os.path.relpath(path, ROOT)
+            best = d
+    return best
 
 
 def latest_traffic(precision, scene, variant):
@@ -248,18 +271,34 @@ def main():
             achieved = alg / (ext_ms * 1e-3) / 1e9
             moved = extend_moved_bytes(args.precision, variant, segs, primary_segs)
             tr = latest_traffic(args.precision, args.scene, variant)
-            line["roofline"] = {
-                "bound": "hbm", "kernel": {3: "k_paths", 4: "k_paths_g"}.get(variant, "k_extend"), "achieved": round(achieved, 2),
-                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                "traffic": (round(tr["extend_bytes_per_segment"] * segs / launches) if tr else None),
-                "algorithmic_bytes_per_launch": round(alg / launches),
-                "algorithmic_bytes": "SURVEY 8(d): 128 B/segment + 12 B/pixel + scene bytes per launch",
-                "moved_bytes_per_segment": round(moved / max(segs, 1), 2), "extend_variant": variant,
-                "avg_launch_ms": round(per_launch_ms, 4), "launches": int(ext_launches),
-                "extend_ms_total": round(ext_ms, 2), "shade_ms_total": round(shade_ms, 2),
-            }
-            if tr and tr.get("valu_busy") is not None:
-                line["roofline"]["valu_busy_pmc"] = tr["valu_busy"]
+            kernel = {3: "k_paths", 4: "k_paths_g"}.get(variant, "k_extend")
+            hbm = {"achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                   "algorithmic_bytes_per_launch": round(alg / launches),
+                   "algorithmic_bytes": "SURVEY 8(d): 128 B/segment + 12 B/pixel + scene bytes per launch",
+                   "moved_bytes_per_segment": round(moved / max(segs, 1), 2)}
+            roof = {"kernel": kernel, "traffic": (round(tr["extend_bytes_per_segment"] * segs / launches) if tr else None),
+                    "extend_variant": variant, "avg_launch_ms": round(per_launch_ms, 4), "launches": int(ext_launches),
+                    "extend_ms_total": round(ext_ms, 2), "shade_ms_total": round(shade_ms, 2)}
+            pm = latest_pmc(args.precision, args.scene, variant) if variant in (3, 4) else None
+            if pm:
+                # The persistent path kernels are bound by VALU issue and lane divergence, not HBM (the
+                # scene lives in LDS / L2, ~9-30 B of HBM per segment).  achieved = VALU lane-instruction slots issued
+                # per second: the PMC summary's wave-instructions per segment x 64 lanes x the segments of this run /
+                # the kernel time measured live; lane_util = the share of those slots doing work (SQ_THREAD_CYCLES_VALU)
+                ps = pm["kernels"][pm["dominant_kernel"]]["per_segment_wave_instructions"]
+                slots = ps["insts_valu"] * 64 * segs / (ext_ms * 1e-3) / 1e12
+                roof.update({"bound": "valu", "achieved": round(slots, 3), "peak": round(VALU_PEAK_TLANE, 2), "unit": "Tlane-inst/s",
+                             "frac": round(slots / VALU_PEAK_TLANE, 4),
+                             "valu_wave_insts_per_segment": round(ps["insts_valu"], 2),
+                             "lane_util": pm.get("valu_lane_util"), "useful_frac": round(slots / VALU_PEAK_TLANE * pm.get("valu_lane_util", 0), 4),
+                             "issue_util_calibrated_pmc": pm.get("valu_issue_util_calibrated"),
+                             "wave_frac_wait_waitcnt_pmc": pm.get("wave_frac_wait_waitcnt"),
+                             "wave_frac_wait_dependency_pmc": pm.get("wave_frac_wait_inst_dependency"),
+                             "pmc_summary": pm["_file"], "hbm": hbm})
+            else:
+                roof.update({"bound": "hbm", "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm["frac"]})
+                roof.update({k: v for k, v in hbm.items() if k not in roof})
+            line["roofline"] = roof
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(line), flush=True)
