@@ -226,6 +226,7 @@ struct DevScene {
     const PerlinRec<R>* perlins;
     const ImageRec* images;
     const uint8_t* texels;
+    const TriRec<R>* leaf_tris;  // leaf_tris[slot] = tris[index of primrefs[slot]] for triangle refs, zeros otherwise
     const uint8_t* lds_image;   // layout.h LDS scene image (nullptr unless the scene qualifies)
     uint32_t n_nodes, n_primrefs, n_tris;  // array lengths (k_paths_g's LDS copy of a small mesh scene)
     int32_t nworld;
@@ -309,8 +310,7 @@ __device__ __forceinline__ bool hit_sphere(const SphereRec<R>& s, const Ray<R>& 
 
 // triangle.h:22-88 (geometric test, unnormalised normal).
 template <class R>
-__device__ __forceinline__ bool hit_tri(const TriRec<R>& tr, const Ray<R>& r, R tmin, R tmax, R& t) {
-    const V3<R> p1 = ld3(tr.p), p2 = ld3(tr.p + 3), p3 = ld3(tr.p + 6);
+__device__ __forceinline__ bool hit_tri_v(V3<R> p1, V3<R> p2, V3<R> p3, const Ray<R>& r, R tmin, R tmax, R& t) {
     const V3<R> N = cross(p2 - p1, p3 - p1);
     const R ndd = dot(N, r.d);
     if (fabs(ndd) < R(DBL_EPSILON)) return false;
@@ -323,6 +323,10 @@ __device__ __forceinline__ bool hit_tri(const TriRec<R>& tr, const Ray<R>& r, R 
     if (dot(N, cross(p1 - p3, p - p3)) < R(0)) return false;
     t = tt;
     return true;
+}
+template <class R>
+__device__ __forceinline__ bool hit_tri(const TriRec<R>& tr, const Ray<R>& r, R tmin, R tmax, R& t) {
+    return hit_tri_v(ld3(tr.p), ld3(tr.p + 3), ld3(tr.p + 6), r, tmin, tmax, t);
 }
 
 template <class R> __device__ __forceinline__ R comp(V3<R> v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
@@ -520,6 +524,9 @@ __device__ __forceinline__ void stat_lane(int k) { atomicAdd(&g_art_stats[k], 1u
 
 #ifndef ART_SPECULATIVE
 #define ART_SPECULATIVE 1
+#endif
+#ifndef ART_LEAF_TRIS
+#define ART_LEAF_TRIS 1  // triangle leaves read the leaf-ordered copy (DevScene::leaf_tris)
 #endif
 #ifndef ART_LEAF2_G
 #define ART_LEAF2_G 1  // the HBM-scene traversal also tests a lane's two pending leaves in one leaf phase
@@ -771,11 +778,24 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                 fc = slot;  // the leaf slot travels in the face field (spheres have no face): LDS shading reads it
             } else {
 #if ART_SPECULATIVE
-                ref = S.primrefs[(k < cnt ? first : first2) + k];
+                const uint32_t slot = (k < cnt ? first : first2) + k;
 #else
-                ref = S.primrefs[first + k];
+                const uint32_t slot = first + k;
 #endif
-                h = hit_prim<R, F>(S, ref, r, tmin, tmax, tt, fc);
+                if constexpr ((F & F_TRI) != 0 && ART_LEAF_TRIS) {
+                    // the leaf-ordered triangle copy: its address depends on the slot alone, so its loads go out
+                    // beside the primref's instead of behind it (one L2 round trip per test instead of two); the
+                    // empty asm keeps the compiler from sinking them under the type test
+                    const TriRec<R>& lt = S.leaf_tris[slot];
+                    V3<R> p1 = ld3(lt.p), p2 = ld3(lt.p + 3), p3 = ld3(lt.p + 6);
+                    ref = S.primrefs[slot];
+                    __asm__ volatile("" : "+v"(p1.x), "+v"(p1.y), "+v"(p1.z), "+v"(p2.x), "+v"(p2.y), "+v"(p2.z), "+v"(p3.x), "+v"(p3.y), "+v"(p3.z));
+                    if (F == F_TRI || primref_type(ref) == PRIM_TRIANGLE) h = hit_tri_v(p1, p2, p3, r, tmin, tmax, tt);
+                    else h = hit_prim<R, F & ~F_TRI>(S, ref, r, tmin, tmax, tt, fc);
+                } else {
+                    ref = S.primrefs[slot];
+                    h = hit_prim<R, F>(S, ref, r, tmin, tmax, tt, fc);
+                }
             }
             if (h) {
                 tmax = tt;

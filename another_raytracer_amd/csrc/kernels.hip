@@ -806,7 +806,7 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
     if constexpr (LM) {
         uint8_t* m = smem + paths_g_head_bytes(g.stack, B);
         const size_t nb = sizeof(BvhNode) * S0.n_nodes, pb = align16(sizeof(uint32_t) * S0.n_primrefs);
-        const size_t tb = (F & F_TRI) ? sizeof(TriRec<double>) * S0.n_tris : 0;
+        const size_t tb = (F & F_TRI) ? sizeof(TriRec<double>) * (ART_LEAF_TRIS ? S0.n_primrefs : S0.n_tris) : 0;
         auto copy = [&](uint8_t* dst, const void* src, size_t bytes) {
             const uint4* s4 = static_cast<const uint4*>(src);
             uint4* d4 = reinterpret_cast<uint4*>(dst);
@@ -818,8 +818,13 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
         S.nodes = reinterpret_cast<const BvhNode*>(m);
         S.primrefs = reinterpret_cast<const uint32_t*>(m + nb);
         if constexpr ((F & F_TRI) != 0) {
+#if ART_LEAF_TRIS
+            copy(m + nb + pb, S0.leaf_tris, tb);
+            S.leaf_tris = reinterpret_cast<const TriRec<double>*>(m + nb + pb);
+#else
             copy(m + nb + pb, S0.tris, tb);
             S.tris = reinterpret_cast<const TriRec<double>*>(m + nb + pb);
+#endif
         }
     }
     const uint32_t P = g.P;
@@ -1397,6 +1402,12 @@ static void build_device_scene(const FlatScene& f, DeviceScene<R>& ds) {
     ds.view.rects = ds.upload(rect);
     ds.view.boxes = ds.upload(box);
     ds.view.primrefs = ds.upload(f.primrefs);
+    {  // every scene with a BVH: any kernel instantiated with triangles reads it, whatever the scene holds
+        std::vector<TriRec<R>> lt(f.primrefs.size());
+        for (size_t i = 0; i < lt.size(); ++i)
+            if (primref_type(f.primrefs[i]) == PRIM_TRIANGLE) lt[i] = tri[primref_index(f.primrefs[i])];
+        ds.view.leaf_tris = ds.upload(lt);
+    }
     ds.view.nodes = ds.upload(f.nodes);
     ds.view.objs = ds.upload(objs);
     ds.view.world = ds.upload(f.world);
@@ -1596,7 +1607,8 @@ template <uint32_t F, uint32_t TF>
 static void launch_paths_g_ft(int num_cu, hipStream_t st, const DevScene<double>& S, const PassGeom& g, const CameraRec<double>& cam,
                               const Work<double>& w, uint32_t* next_slot) {
     // g.stack = stack_rows: sentinel + entries + spare row
-    const size_t lds_m = paths_g_head_bytes(g.stack, kBlockM) + paths_g_mesh_bytes(S.n_nodes, S.n_primrefs, (F & F_TRI) ? S.n_tris : 0u);
+    const size_t lds_m = paths_g_head_bytes(g.stack, kBlockM) +
+                         paths_g_mesh_bytes(S.n_nodes, S.n_primrefs, (F & F_TRI) ? (ART_LEAF_TRIS ? S.n_primrefs : S.n_tris) : 0u);
 #if ART_LDS_MESH
     if (S.n_nodes > 0 && lds_m <= kPathsGLdsCap) {
         const int blocks = blocks_per_cu(reinterpret_cast<const void*>(k_paths_g<F, TF, true>), kBlockM, lds_m) * num_cu;
@@ -1616,8 +1628,16 @@ static void launch_paths_g(uint32_t feat, bool tex_basic, int num_cu, hipStream_
         if (tex_basic) launch_paths_g_ft<kFeatSpheres, kTexBasic>(num_cu, st, S, g, cam, w, next_slot);
         else launch_paths_g_ft<kFeatSpheres, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
     } else if ((feat & ~kFeatMesh) == 0) {
-        if (tex_basic) launch_paths_g_ft<kFeatMesh, kTexBasic>(num_cu, st, S, g, cam, w, next_slot);
-        else launch_paths_g_ft<kFeatMesh, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
+        // the F_TRI bit of an instantiation <=> the scene has triangles (leaf_tris exists)
+        if (feat & F_TRI) {
+            if (tex_basic) launch_paths_g_ft<kFeatMesh, kTexBasic>(num_cu, st, S, g, cam, w, next_slot);
+            else launch_paths_g_ft<kFeatMesh, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
+        } else {
+            if (tex_basic) launch_paths_g_ft<kFeatMesh & ~F_TRI, kTexBasic>(num_cu, st, S, g, cam, w, next_slot);
+            else launch_paths_g_ft<kFeatMesh & ~F_TRI, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
+        }
+    } else if ((feat & F_TRI) == 0) {  // e.g. the Next-Week final: no triangle code in the kernel
+        launch_paths_g_ft<F_ALL & ~F_TRI, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
     } else {
         launch_paths_g_ft<F_ALL, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
     }
