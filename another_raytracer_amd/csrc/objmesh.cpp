@@ -502,17 +502,6 @@ ObjMesh load_obj(const std::string& path) {
     return m;
 }
 
-std::string texel_asset_path(const std::string& image_path) {
-    const size_t slash = image_path.find_last_of('/');
-    const size_t dot = image_path.find_last_of('.');
-    const std::string stem = (dot != std::string::npos && (slash == std::string::npos || dot > slash)) ? image_path.substr(0, dot) : image_path;
-    for (const char* ext : {".rgb.gz", ".rgb"}) {
-        const std::string p = stem + ext;
-        if (std::ifstream(p, std::ios::binary)) return p;
-    }
-    return {};
-}
-
 std::vector<int> build_mesh(SceneGraph& g, const ObjMesh& m) {
     std::map<std::string, int> maps;  // material_map_handler (mesh.h:9-27): one image texture per map name
     auto vert = [&](const ObjIndex& k) {  // get_vertice_by_index (mesh.h:76-82): f32 -> f64

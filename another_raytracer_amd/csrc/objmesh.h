@@ -50,13 +50,9 @@ ObjMesh load_obj(const std::string& path);
 //     distinct map name, material_map_handler mesh.h:9-27),
 //   * lambertian(Ka + Kd) (f32 sums) for other materials,
 //   * lambertian(color::random()) when the OBJ has no materials (draws from g.rng).
-// Returns the triangle node ids (consecutive, in order).  A map_Kd image is read from its pre-decoded texel asset
-// (texel_asset_path); JPEG/PNG decoding itself (stb_image v2.27 in the reference) is not part of this library.
+// Returns the triangle node ids (consecutive, in order).  A map_Kd image is decoded from its file next to the MTL
+// (SceneGraph::image_file: imagedec.cpp, stb_image v2.27's bytes, as material_map_handler's image_texture loads it).
 std::vector<int> build_mesh(SceneGraph& g, const ObjMesh& m);
-
-// Texel asset of an image file: "<path minus extension>.rgb.gz" or ".rgb" (int32 w, h, bpp header + bytes, the
-// reference's stb_image output as written by oracle/ref_harness `texture`).  Empty when neither exists.
-std::string texel_asset_path(const std::string& image_path);
 
 // mapbox earcut (rapidobj.hpp:497-1166) over one ring of 2-D points (x0, y0, x1, y1, ...): vertex indices, 3 per
 // triangle, before rapidobj's swap of each triangle's first two.  Empty on failure.

@@ -2,10 +2,13 @@
 // scene_manager::build -> camera (aspect W/H, focus distance 10, shutter [0, 1]) -> engine::run -> imageio::save_image.
 //
 //   art_render SCENE W H SPP OUT.png [--mode single|stripes|images|adaptive] [--seed N] [--max-depth D] [--device I]
-//                                    [--assets DIR]
+//                                    [--assets DIR] [--gpus N] [--progressive K] [--save-scene FILE]
 //   art_render --info SCENE [--assets DIR]     scene_manager::build only (no GPU needed): prints the scene summary
 //
-// Prints one JSON line: {"scene", "W", "H", "spp", "ms", "segments", "msamples_per_s", "extend_variant"}.
+// SCENE is a scene_manager alias, or file:PATH for a flat-scene file written by --save-scene.  --gpus N renders on
+// devices 0..N-1 through multi_engine (RCCL); --progressive K traces K samples per pass and prints one JSON line per
+// pass (the headless live preview).  Prints one JSON line: {"scene", "W", "H", "spp", "ms", "segments",
+// "msamples_per_s", "extend_variant"}.
 #include <cstdlib>
 #include <cstring>
 #include <iostream>
@@ -25,7 +28,8 @@ std::string default_assets(const char* argv0) {  // <repo>/assets next to <repo>
 
 int usage() {
     std::cerr << "usage: art_render SCENE W H SPP OUT.png [--mode single|stripes|images|adaptive] [--seed N] [--max-depth D]"
-                 " [--device I] [--assets DIR]\n       art_render --info SCENE [--assets DIR]\n";
+                 " [--device I] [--assets DIR] [--gpus N] [--progressive K] [--save-scene FILE]\n"
+                 "       art_render --info SCENE [--assets DIR]\n";
     return 2;
 }
 
@@ -35,7 +39,8 @@ int main(int argc, char** argv) try {
     std::vector<std::string> pos;
     std::string assets = default_assets(argv[0]), mode = "stripes";
     uint64_t seed = 0;
-    int max_depth = 50, device = 0;
+    int max_depth = 50, device = 0, gpus = 0, progressive = -1;
+    std::string save_path;
     bool info = false;
     for (int i = 1; i < argc; ++i) {
         const std::string a = argv[i];
@@ -49,6 +54,9 @@ int main(int argc, char** argv) try {
         else if (a == "--seed") seed = std::strtoull(next().c_str(), nullptr, 10);
         else if (a == "--max-depth") max_depth = std::atoi(next().c_str());
         else if (a == "--device") device = std::atoi(next().c_str());
+        else if (a == "--gpus") gpus = std::atoi(next().c_str());
+        else if (a == "--progressive") progressive = std::atoi(next().c_str());
+        else if (a == "--save-scene") save_path = next();
         else pos.push_back(a);
     }
     art::scene_manager sm(assets, device);  // main.cpp:29-30
@@ -67,17 +75,38 @@ int main(int argc, char** argv) try {
                                : mode == "adaptive" ? art::engine_mode::adaptive
                                : mode == "images"   ? art::engine_mode::parallel_images
                                                     : art::engine_mode::parallel_stripes;
-    const art::scene world = sm.build(pos[0]);
+    const bool from_file = pos[0].rfind("file:", 0) == 0;
+    const art::scene world = from_file ? sm.load(pos[0].substr(5)) : sm.build(pos[0]);
+    if (!save_path.empty()) art::save_scene(world, save_path);
     const double dist_to_focus = 10.0;  // main.cpp:34
     art::camera cam(world.lookfrom, world.lookat, art::vec3{{0, 1, 0}}, world.vfov, double(W) / H, world.aperture, dist_to_focus, 0.0,
                     1.0);  // main.cpp:35 (aspect W/H: SURVEY Q6)
-    art::render_engine eng(W, H, cam, m, spp, max_depth, seed);
-    eng.set_scene(world, world.background);  // main.cpp:44
     std::vector<std::uint8_t> image(static_cast<size_t>(W) * H * 3);
-    const int ms = eng.run(image.data());     // main.cpp:45
-    if (ms < 0) return 1;
+    rt_stats st{};
+    if (gpus > 0) {  // engine.h:335-376's parallel drivers over GPUs
+        if (from_file) throw std::invalid_argument("--gpus builds the scene on every device: give a scene alias");
+        std::vector<int> devs;
+        for (int k = 0; k < gpus; ++k) devs.push_back(k);
+        art::multi_engine eng(pos[0], assets, devs, W, H, cam, spp, max_depth, seed);
+        eng.set_background(world.background);
+        eng.run(image.data());
+        st = eng.stats();
+    } else {
+        art::render_engine eng(W, H, cam, m, spp, max_depth, seed);
+        eng.set_scene(world, world.background);  // main.cpp:44
+        int ms;
+        if (progressive >= 0) {
+            ms = eng.run_progressive(image.data(), [&](int done, const std::uint8_t*) {
+                std::cout << "{\"pass_samples_done\":" << done << "}" << std::endl;
+                return true;
+            }, progressive);
+        } else {
+            ms = eng.run(image.data());  // main.cpp:45
+        }
+        if (ms < 0) return 1;
+        st = eng.stats();
+    }
     if (!art::imageio::save_image(pos[4], W, H, 3, image.data())) throw std::runtime_error("cannot write " + pos[4]);
-    const rt_stats& st = eng.stats();
     std::cout << "{\"scene\":\"" << pos[0] << "\",\"W\":" << W << ",\"H\":" << H << ",\"spp\":" << spp << ",\"ms\":" << st.ms
               << ",\"segments\":" << st.segments << ",\"msamples_per_s\":" << (st.ms > 0 ? st.segments / st.ms / 1e3 : 0.0)
               << ",\"extend_variant\":" << st.extend_variant << "}" << std::endl;

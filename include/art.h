@@ -20,6 +20,13 @@
  *     constant_medium.h, material.h, texture.h)
  *   bool mesh::parse(path)                    mesh.h:31-65        rt_mesh_parse(path, &triangles, &shapes)
  *   hittable_list mesh::build()               mesh.h:67-145       rt_mesh_build(graph, path, &first_id)
+ *   imageio::load_image (stbi_load)          imageio.cpp:11-15   rt_image_load(path, &w, &h, &c, &pixels)
+ *   engine::_run_parallel_stripes (threads)  engine.h:335-376    rt_multi_create + rt_render_multi (GPUs, RCCL)
+ *   dynamic_gui refresh per row / square     gui.cpp:25-58,      rt_render_progressive(..., callback, user, ...)
+ *                                            engine.h:88,307,353
+ *   hittable_list::hit(r, 0.001, inf, rec)   hittable_list.cpp:5 rt_trace_rays(scene, rays, n, flags, t, normals)
+ *   (scene construction every run)           scene_manager.cpp,  rt_scene_save / rt_scene_load (flat-scene files)
+ *                                            mesh.h, bvh.cpp
  *
  * RNG contract: the reference draws from one global std::mt19937 (tracer_utils.h:27-31).  Scene construction here
  * replays that generator exactly (seed 5489, same draw order), so scenes are bit-identical.  Rendering draws come
@@ -103,7 +110,8 @@ typedef struct rt_stats {
     int32_t passes, samples_per_pass, local_rows;
     int32_t extend_variant;     /* 0: scene read from HBM; 1: LDS-resident scene (spheres-only scene that fits);
                                    2: LDS-resident scene with shading fused into the extend kernel (one launch per
-                                   depth); 3: persistent paths (the fused bounce loop in registers, one launch per pass) */
+                                   depth); 3: persistent paths (the fused bounce loop in registers, one launch per pass);
+                                   4: persistent paths over the HBM scene (every other scene; k_paths_g) */
 } rt_stats;
 
 typedef struct rt_scene_info {  /* scene_manager.h:6-14 */
@@ -123,8 +131,9 @@ int rt_device_count(void);
 /* ---- scenes ---- */
 /* Builtin scenes = scene_manager::build(alias): "1".."8" or "random", "two_spheres", "two_perlin_spheres", "earth",
  * "simple_light", "cornell_box", "cornell_smoke", "final"; plus "c1" (SURVEY Q7 3-sphere scene), "cow", "dino"
- * (SURVEY Q8 mesh scenes) and "9"/"mesh" (the capsule, the reference's default scene).  asset_dir holds earthmap.rgb
- * and models/{cow.obj, dino.obj, capsule/capsule.obj + .mtl + capsule.rgb.gz}. */
+ * (SURVEY Q8 mesh scenes) and "9"/"mesh" (the capsule, the reference's default scene).  asset_dir holds earthmap.jpg
+ * and models/{cow.obj, dino.obj, capsule/capsule.obj + .mtl + capsule.jpg}; images are decoded by rt_image_load's
+ * decoder. */
 int rt_scene_build(const char* name, const char* asset_dir, int device, rt_scene** out);
 int rt_scene_info_get(const rt_scene* scene, rt_scene_info* info);
 /* Canonical JSON of the scene graph (schema of oracle/ref_harness `dump`); returns the size needed incl. NUL. */
@@ -220,8 +229,8 @@ int rt_graph_set_view(rt_graph* g, const double lookfrom[3], const double lookat
  * rt_mesh_parse = mesh::parse: parses and triangulates; reports the triangle and shape counts (either may be NULL).
  * rt_mesh_build = mesh::parse + mesh::build into the graph: one triangle per post-triangulation face with
  *   lambertian(color::random()) (no MTL; draws from the graph's generator), lambertian(Ka + Kd), or
- *   lambertian(barycentric_image_texture) for a map_Kd material, whose texels are read from the pre-decoded asset
- *   <map stem>.rgb.gz or .rgb next to the MTL (JPEG decoding is not part of this library).  The triangle ids are
+ *   lambertian(barycentric_image_texture) for a map_Kd material, whose image (JPEG / PNG, next to the MTL) is decoded
+ *   as rt_image_load does (stb_image's bytes; a raw texel file <stem>.rgb[.gz] is also accepted).  The triangle ids are
  *   *first_id .. *first_id + n - 1; returns n >= 0 or a negative code. */
 int rt_mesh_parse(const char* obj_path, int64_t* triangles, int64_t* shapes);
 int rt_mesh_build(rt_graph* g, const char* obj_path, int* first_id);

@@ -4,7 +4,7 @@
 // camera (camera.h:8-36) and engine<W,H,C> (engine.h:19-54).  This header restates that surface for C++ callers on
 // top of libart.so, so a reference-style main() changes its includes and nothing else:
 //
-//     art::scene_manager sm("assets");                           // asset_dir: earthmap.rgb, models/...
+//     art::scene_manager sm("assets");                           // asset_dir: earthmap.jpg, models/...
 //     art::scene world = sm.build("1");                          // scene_alias::random
 //     art::camera cam(world.lookfrom, world.lookat, {0, 1, 0}, world.vfov, double(W) / H, world.aperture, 10.0, 0, 1);
 //     art::engine<W, H, 3> eng(cam, art::engine_mode::parallel_stripes);
@@ -23,6 +23,8 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <exception>
+#include <functional>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -90,6 +92,17 @@ public:
             if (msg.find("unkwnown scene requested") != std::string::npos) throw std::logic_error(msg);
             throw std::runtime_error("scene_manager::build(" + alias + "): " + msg);
         }
+        return wrap(raw);
+    }
+    // A scene written by save_scene (rt_scene_load: the flat-scene file, no OBJ parsing, image decoding or BVH build).
+    scene load(const std::string& path) const {
+        rt_scene* raw = nullptr;
+        check(rt_scene_load(path.c_str(), device_, &raw), "scene_manager::load");
+        return wrap(raw);
+    }
+
+private:
+    static scene wrap(rt_scene* raw) {
         scene s;
         s.objects = std::shared_ptr<rt_scene>(raw, rt_scene_destroy);
         check(rt_scene_info_get(raw, &s.info), "rt_scene_info_get");
@@ -102,11 +115,12 @@ public:
         s.aperture = s.info.aperture;
         return s;
     }
-
-private:
     std::string assets_;
     int device_;
 };
+
+// Writes a built or loaded scene as a versioned flat-scene file (rt_scene_save); scene_manager::load reads it back.
+inline void save_scene(const scene& world, const std::string& path) { check(rt_scene_save(world.objects.get(), path.c_str()), "save_scene"); }
 
 // The engine with a runtime image size (the reference fixes W, H, C at compile time: engine<W,H,C> below); samples
 // per pixel and max depth are the reference's tracer_constants (tracer_constants.h:12-13) as arguments with the same
@@ -129,6 +143,46 @@ public:
             std::fprintf(stderr, "Invalid input scene!\n");
             return -1;
         }
+        const rt_params p = params();
+        const int rc = rt_render(world_.objects.get(), &cam_.raw(), &p, out, nullptr, &stats_);
+        if (rc == RT_E_INVALID && mode_ == engine_mode::adaptive) throw std::logic_error(rt_last_error());
+        check(rc, "engine::run");
+        return static_cast<int>(stats_.ms);
+    }
+    // Progressive rendering (the reference's live preview, gui.cpp:25-58, headless): passes of samples_per_pass samples
+    // per pixel (0: spp / 8 rounded up); after each, `on_pass(samples_done, rgb)` sees the frame write_color'ed with the
+    // samples so far (in `out`); returning false stops there.  The last snapshot equals run()'s image bit for bit.
+    int run_progressive(std::uint8_t* out, const std::function<bool(int samples_done, const std::uint8_t* rgb)>& on_pass,
+                        int samples_per_pass = 0) {
+        if (!world_.objects || world_.info.objects == 0) {
+            std::fprintf(stderr, "Invalid input scene!\n");
+            return -1;
+        }
+        rt_params p = params();
+        if (p.flags & RT_ADAPTIVE) throw std::logic_error("engine::run_progressive: no progressive adaptive mode");
+        p.samples_per_pass = samples_per_pass;
+        struct ctx_t {
+            const std::function<bool(int, const std::uint8_t*)>* fn;
+            std::exception_ptr err;
+        } ctx{&on_pass, nullptr};
+        auto tramp = [](void* user, int32_t done, int32_t, const std::uint8_t* rgb, const double*) -> int {
+            auto* c = static_cast<ctx_t*>(user);
+            try {
+                return (*c->fn)(done, rgb) ? 0 : 1;
+            } catch (...) {  // no exception crosses the C ABI: stop the render, rethrow after it returns
+                c->err = std::current_exception();
+                return 1;
+            }
+        };
+        const int rc = rt_render_progressive(world_.objects.get(), &cam_.raw(), &p, out, nullptr, tramp, &ctx, &stats_);
+        if (ctx.err) std::rethrow_exception(ctx.err);
+        check(rc, "engine::run_progressive");
+        return static_cast<int>(stats_.ms);
+    }
+    const rt_stats& stats() const { return stats_; }
+
+private:
+    rt_params params() const {
         rt_params p{};
         p.width = w_;
         p.height = h_;
@@ -141,14 +195,8 @@ public:
         p.band_index = 0;
         p.flags = mode_ == engine_mode::adaptive ? RT_ADAPTIVE : 0;
         for (int k = 0; k < 3; ++k) p.background[k] = background_.e[k];
-        const int rc = rt_render(world_.objects.get(), &cam_.raw(), &p, out, nullptr, &stats_);
-        if (rc == RT_E_INVALID && mode_ == engine_mode::adaptive) throw std::logic_error(rt_last_error());
-        check(rc, "engine::run");
-        return static_cast<int>(stats_.ms);
+        return p;
     }
-    const rt_stats& stats() const { return stats_; }
-
-private:
     int w_, h_;
     camera cam_;
     engine_mode mode_;
@@ -168,7 +216,62 @@ public:
         : render_engine(W, H, cam, mode, samples_per_pixel, max_depth, seed) {}
 };
 
+// The reference's CPU-parallel drivers (engine.h:335-376: row stripes on threads) over several GPUs of one process:
+// the scene on every device, one RCCL communicator per device, each device rendering its row bands and one
+// ncclGather assembling the frame on devices[0] (rt_render_multi).  Same image as engine::run for any device count.
+class multi_engine {
+public:
+    multi_engine(const std::string& alias, const std::string& asset_dir, const std::vector<int>& devices, int width, int height,
+                 const camera& cam, int samples_per_pixel = 100, int max_depth = 50, uint64_t seed = 0, int band_rows = 16)
+        : w_(width), h_(height), cam_(cam), spp_(samples_per_pixel), max_depth_(max_depth), seed_(seed), band_rows_(band_rows) {
+        rt_multi* raw = nullptr;
+        check(rt_multi_create(alias.c_str(), asset_dir.c_str(), devices.data(), static_cast<int>(devices.size()), &raw), "multi_engine");
+        m_ = std::shared_ptr<rt_multi>(raw, rt_multi_destroy);
+    }
+    void set_background(color background) { background_ = background; }
+    // W*H*3 bytes of host memory, row 0 = top; returns the wall milliseconds of the call
+    int run(std::uint8_t* out) {
+        rt_params p{};
+        p.width = w_;
+        p.height = h_;
+        p.spp = spp_;
+        p.max_depth = max_depth_;
+        p.seed = seed_;
+        p.fp_mode = RT_FP64;
+        p.band_rows = band_rows_;
+        p.band_count = 1;
+        p.band_index = 0;
+        for (int k = 0; k < 3; ++k) p.background[k] = background_.e[k];
+        check(rt_render_multi(m_.get(), &cam_.raw(), &p, out, &stats_), "multi_engine::run");
+        return static_cast<int>(stats_.ms);
+    }
+    const rt_stats& stats() const { return stats_; }
+
+private:
+    std::shared_ptr<rt_multi> m_;
+    int w_, h_;
+    camera cam_;
+    int spp_, max_depth_;
+    uint64_t seed_;
+    int band_rows_;
+    color background_;
+    rt_stats stats_{};
+};
+
 namespace imageio {  // utils/imageio.h: save_image writes a PNG (zlib deflate; stb_image_write in the reference)
+// imageio::load_image (imageio.cpp:11-15, stbi_load(path, &w, &h, &c, 0)): JPEG / PNG through libart's decoder,
+// the bytes stb_image v2.27 returns (rt_image_load); throws std::runtime_error on an unreadable file.
+inline std::vector<std::uint8_t> load_image(const std::string& path, int& width, int& height, int& channels) {
+    int32_t w = 0, h = 0, c = 0;
+    std::uint8_t* px = nullptr;
+    check(rt_image_load(path.c_str(), &w, &h, &c, &px), "imageio::load_image");
+    std::vector<std::uint8_t> out(px, px + static_cast<size_t>(w) * h * c);
+    rt_image_free(px);
+    width = w;
+    height = h;
+    channels = c;
+    return out;
+}
 inline bool save_image(const std::string& path, int width, int height, int bytes_per_pixel, const std::uint8_t* data) {
     const int color_type = bytes_per_pixel == 1 ? 0 : bytes_per_pixel == 2 ? 4 : bytes_per_pixel == 3 ? 2 : 6;
     std::vector<std::uint8_t> raw;

@@ -75,3 +75,55 @@ def test_cpp_host_renders_the_python_image(tmp_path, mode):
     eng.run(img)
     assert np.array_equal(got, img)
     assert info["segments"] == eng.stats["segments"]
+
+
+def test_header_surface_beyond_main_compiles(tmp_path):
+    """The rest of the C++ surface: multi_engine (rt_render_multi), run_progressive, save_scene / scene_manager::load,
+    imageio::load_image."""
+    src = tmp_path / "more.cpp"
+    src.write_text("""
+#include "art_engine.hpp"
+int main() {
+    art::scene_manager sm("assets");
+    art::scene world = sm.build("cow");
+    art::save_scene(world, "cow.artscn");
+    art::scene again = sm.load("cow.artscn");
+    art::camera cam(again.lookfrom, again.lookat, art::vec3{{0, 1, 0}}, again.vfov, 16.0 / 9, again.aperture, 10.0, 0.0, 1.0);
+    art::render_engine eng(320, 180, cam, art::engine_mode::parallel_stripes, 16);
+    eng.set_scene(again, again.background);
+    std::vector<std::uint8_t> image(320 * 180 * 3);
+    int passes = 0;
+    eng.run_progressive(image.data(), [&](int, const std::uint8_t*) { return ++passes < 3; }, 4);
+    art::multi_engine multi("cow", "assets", {0, 1}, 320, 180, cam, 16);
+    multi.set_background(world.background);
+    multi.run(image.data());
+    int w = 0, h = 0, c = 0;
+    std::vector<std::uint8_t> tex = art::imageio::load_image("assets/earthmap.jpg", w, h, c);
+    return tex.size() == static_cast<size_t>(w) * h * c ? 0 : 1;
+}
+""")
+    out = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-Wall", "-Wextra", "-Werror",
+                          "-I" + os.path.join(ROOT, "include"), str(src)], capture_output=True, text=True)
+    assert out.returncode == 0, out.stderr
+
+
+@pytest.mark.gpu
+def test_cpp_host_multi_progressive_and_scene_file(tmp_path):
+    """--gpus 1 (multi_engine: RCCL gather path), --progressive (last snapshot) and a saved-then-loaded scene file all
+    give the plain run's image bit for bit."""
+    W, H, spp = 96, 54, 8
+    base = tmp_path / "base.png"
+    scn = tmp_path / "cow.artscn"
+    info = json.loads(run("cow", W, H, spp, base, "--save-scene", scn).stdout)
+    ref = imageio.load_image(str(base))
+    multi = tmp_path / "multi.png"
+    run("cow", W, H, spp, multi, "--gpus", 1)
+    assert np.array_equal(imageio.load_image(str(multi)), ref)
+    prog = tmp_path / "prog.png"
+    out = run("cow", W, H, spp, prog, "--progressive", 3).stdout.strip().splitlines()
+    assert [json.loads(x)["pass_samples_done"] for x in out[:-1]] == [3, 6, 8]
+    assert np.array_equal(imageio.load_image(str(prog)), ref)
+    loaded = tmp_path / "loaded.png"
+    info2 = json.loads(run(f"file:{scn}", W, H, spp, loaded).stdout)
+    assert np.array_equal(imageio.load_image(str(loaded)), ref)
+    assert info2["segments"] == info["segments"]
