@@ -5,8 +5,9 @@
 
 
 The reference splits an image into 4 contiguous row stripes on 4 threads (engine.h:335-376).  Here rank r of N
-renders every global row y with (y // band_rows) % N == r (band_rows = 16: sky rows are cheap and object rows
-expensive, so interleaving balances the load), packs its rows contiguously, and rank 0 gathers the packed RGB8
+renders every global row y with (y // band_rows) % N == r (band_rows = 8: sky rows are cheap and object rows
+expensive, so interleaving balances the load; 8-row bands keep the kernels' 8x8 pixel tiles on 8 consecutive image
+rows, and split 1080 rows over 8 GPUs as 136/135 rows where 16-row bands gave 144/128), packs its rows contiguously, and rank 0 gathers the packed RGB8
 blocks (RCCL over xGMI; the only collective of the path) and un-interleaves them.  Every pixel's RNG stream is keyed
 by (seed, global pixel, sample), so the gathered image is bit-identical to a single-GPU render (tests/).
 """
@@ -18,7 +19,7 @@ import torch.distributed as dist
 
 from ._lib import RT_OUT_DEVICE, check, lib, rt_params, rt_stats
 
-DEFAULT_BAND_ROWS = 16
+DEFAULT_BAND_ROWS = 8
 
 
 def band_rows_of(height, band_rows, band_count, band_index):

@@ -78,7 +78,7 @@ def parse():
     ap.add_argument("--spp", type=int, default=1024)
     ap.add_argument("--max-depth", type=int, default=50)
     ap.add_argument("--precision", default="f64", choices=["f64"])  # the reference's double (ABI 2: the only mode)
-    ap.add_argument("--band-rows", type=int, default=16)
+    ap.add_argument("--band-rows", type=int, default=8)  # distributed.DEFAULT_BAND_ROWS
     ap.add_argument("--samples-per-pass", type=int, default=0)
     ap.add_argument("--no-profile", action="store_true", help="skip per-launch HIP events (no roofline)")
     ap.add_argument("--global-scene", action="store_true", help="force the global-memory extend kernel (A/B vs LDS scene)")
