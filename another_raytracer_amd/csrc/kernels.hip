@@ -775,7 +775,7 @@ __device__ long long g_trace_pixel = -1, g_trace_sample = -1;
 // those arrays copied into LDS: node and triangle fetches at LDS latency instead of L2's.  The other arrays stay in
 // HBM.  The copies are plain LDS arrays reached through the DevScene pointers: the compiler infers their address
 // space (ds_read, no flat loads).
-constexpr int kBlockM = 768;
+constexpr int kBlockM = 256 * ART_PATHS_G_WAVES;  // one LM block per CU at the kernel's occupancy
 constexpr size_t kPathsGLdsCap = 160 * 1024;
 __host__ __device__ constexpr size_t align16(size_t x) { return (x + 15u) & ~size_t(15); }
 __host__ __device__ constexpr size_t paths_g_stack_bytes(uint32_t stack, int block) { return sizeof(StackT<false>) * stack * block; }
