@@ -229,6 +229,8 @@ struct DevScene {
     const TriRec<R>* leaf_tris;  // leaf_tris[slot] = tris[index of primrefs[slot]] for triangle refs, zeros otherwise
     const uint8_t* lds_image;   // layout.h LDS scene image (nullptr unless the scene qualifies)
     uint32_t n_nodes, n_primrefs, n_tris;  // array lengths (k_paths_g's LDS copy of a small mesh scene)
+    uint32_t nodes_lds;         // k_paths_g LM 2: LDS byte address of the copy of nodes [0, n_lds_nodes) (top levels)
+    uint32_t n_lds_nodes;
     int32_t nworld;
     R bg[3];
 };
@@ -597,7 +599,7 @@ __device__ __forceinline__ float f32_dir(double d) {
     return __builtin_copysignf(fmaxf(__builtin_fabsf(f), 0x1p-64f), f);
 }
 // B: lanes per block (LDS stack stride).  L: nodes and leaf spheres come from the LDS scene image at `lds`.
-template <class R, uint32_t F, int B, bool L>
+template <class R, uint32_t F, int B, bool L, bool PL = false>
 __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* lds, int32_t root, const Ray<R>& r, R tmin, R tmax,
                                          StackT<L>* stk, R& t, uint32_t& prim, uint32_t& face, uint32_t& mt) {
     static_assert(!(L && (F & F_MEDIA)), "packed LDS keys need tmin > 0: no medium boundary tests in the LDS variant");
@@ -657,6 +659,12 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                 lz = lds_f4(az);
                 hz = lds_f4(az + kLdsPlane);
                 ch = lds_i4(kLdsOffNodes + 9 * kLdsPlane + n16);
+            } else if (PL && static_cast<uint32_t>(node) < S.n_lds_nodes) {
+                // the top levels, copied into LDS: explicit LDS loads (a generic pointer here would be merged with
+                // the global branch's into flat loads)
+                const uint32_t a = S.nodes_lds + static_cast<uint32_t>(node) * static_cast<uint32_t>(sizeof(BvhNode));
+                lx = lds_f4(a); hx = lds_f4(a + 16); ly = lds_f4(a + 32); hy = lds_f4(a + 48); lz = lds_f4(a + 64); hz = lds_f4(a + 80);
+                ch = lds_i4(a + 96);
             } else {
                 const float4* np = reinterpret_cast<const float4*>(S.nodes + node);
                 lx = np[0]; hx = np[1]; ly = np[2]; hy = np[3]; lz = np[4]; hz = np[5];
@@ -828,7 +836,7 @@ __device__ __forceinline__ Ray<R> xform_in(const ObjRec<R>& o, const Ray<R>& r) 
 }
 
 // Any non-medium object: prim, BVH, or a translate/rotate_y chain (<= kMaxXformChain) over one of them.
-template <class R, uint32_t F, int B, bool L>
+template <class R, uint32_t F, int B, bool L, bool PL = false>
 __device__ __forceinline__ bool hit_object(const DevScene<R>& S, const uint8_t* lds, int32_t oi, Ray<R> r, R tmin, R tmax, StackT<L>* stk,
                                            R& t, uint32_t& prim, uint32_t& face, uint32_t& mt) {
     if (F & F_XFORM) {
@@ -846,14 +854,14 @@ __device__ __forceinline__ bool hit_object(const DevScene<R>& S, const uint8_t* 
         mt = kMatUnknown;
         return hit_prim<R, F>(S, prim, r, tmin, tmax, t, face);
     }
-    return traverse<R, F, B, L>(S, lds, o.a, r, tmin, tmax, stk, t, prim, face, mt);
+    return traverse<R, F, B, L, PL>(S, lds, o.a, r, tmin, tmax, stk, t, prim, face, mt);
 }
 
 // Out of line: measured +0.2 % (cow) to +1.8 % (Next-Week final) over the inlined body, which raised the register
 // pressure of the whole path loop for a function most segments do not reach.
 static __device__ __noinline__ double glibc_log_call(double x) { return glibc_log(x); }
 // constant_medium.h:37-82.  Consumes one uniform when the clamped interval is non-empty.
-template <class R, uint32_t F, int B, bool L>
+template <class R, uint32_t F, int B, bool L, bool PL = false>
 __device__ __forceinline__ bool hit_medium(const DevScene<R>& S, const uint8_t* lds, const ObjRec<R>& m, const Ray<R>& r, R tmin, R tmax,
                                            StackT<L>* stk, uint64_t& rng, R& t) {
     const R inf = R(__builtin_inf());
@@ -888,8 +896,8 @@ __device__ __forceinline__ bool hit_medium(const DevScene<R>& S, const uint8_t* 
         }
     } else {
         uint32_t p, f, mt;
-        if (!hit_object<R, F, B, L>(S, lds, m.a, r, -inf, inf, stk, t1, p, f, mt)) return false;
-        if (!hit_object<R, F, B, L>(S, lds, m.a, r, t1 + R(0.0001), inf, stk, t2, p, f, mt)) return false;
+        if (!hit_object<R, F, B, L, PL>(S, lds, m.a, r, -inf, inf, stk, t1, p, f, mt)) return false;
+        if (!hit_object<R, F, B, L, PL>(S, lds, m.a, r, t1 + R(0.0001), inf, stk, t2, p, f, mt)) return false;
     }
     if (t1 < tmin) t1 = tmin;
     if (t2 > tmax) t2 = tmax;
@@ -912,7 +920,7 @@ struct HitOut {
     uint32_t prim, obj;  // obj: world slot | box face << 16
     uint32_t mt;         // material type when the hit came from the LDS scene image, else kMatUnknown
 };
-template <class R, uint32_t F, int B, bool L>
+template <class R, uint32_t F, int B, bool L, bool PL = false>
 __device__ __forceinline__ bool trace_world(const DevScene<R>& S, const uint8_t* lds, const Ray<R>& r, StackT<L>* stk, uint64_t& rng, R& t,
                                             HitOut& h) {
     R closest = R(__builtin_inf());
@@ -922,7 +930,7 @@ __device__ __forceinline__ bool trace_world(const DevScene<R>& S, const uint8_t*
         const ObjRec<R>& o = S.objs[oi];
         R tt;
         if ((F & F_MEDIA) && o.kind == OBJ_MEDIUM) {
-            if (hit_medium<R, F, B, L>(S, lds, o, r, R(0.001), closest, stk, rng, tt)) {
+            if (hit_medium<R, F, B, L, PL>(S, lds, o, r, R(0.001), closest, stk, rng, tt)) {
                 closest = tt;
                 any = true;
                 h.prim = kMediumHit;
@@ -931,7 +939,7 @@ __device__ __forceinline__ bool trace_world(const DevScene<R>& S, const uint8_t*
             }
         } else {
             uint32_t prim = 0, face = 0, mt = kMatUnknown;
-            if (hit_object<R, F, B, L>(S, lds, oi, r, R(0.001), closest, stk, tt, prim, face, mt)) {
+            if (hit_object<R, F, B, L, PL>(S, lds, oi, r, R(0.001), closest, stk, tt, prim, face, mt)) {
                 closest = tt;
                 any = true;
                 h.prim = prim;

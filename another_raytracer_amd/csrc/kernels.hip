@@ -761,6 +761,10 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S, PassGe
 #ifndef ART_LDS_MESH
 #define ART_LDS_MESH 1  // k_paths_g with the mesh arrays in LDS when they fit (LM)
 #endif
+#ifndef ART_LDS_PARTIAL
+#define ART_LDS_PARTIAL 1  // k_paths_g LM 2: the top BVH levels in LDS when the whole BVH does not fit
+#endif
+constexpr uint32_t kLdsPartialMinNodes = 64;
 #ifndef ART_PATHS_G_WAVES
 #define ART_PATHS_G_WAVES 3  // 3 waves per SIMD (<= 168 VGPRs): measured best over 2 and 4 (cow +22 %, final +18 %, dino +21 % over 2)
 #endif
@@ -785,7 +789,7 @@ __host__ __device__ constexpr size_t paths_g_head_bytes(uint32_t stack, int bloc
 __host__ __device__ constexpr size_t paths_g_mesh_bytes(uint32_t n_nodes, uint32_t n_primrefs, uint32_t n_tris) {  // n_tris: 0 unless F_TRI
     return sizeof(BvhNode) * n_nodes + align16(sizeof(uint32_t) * n_primrefs) + sizeof(TriRec<double>) * n_tris;
 }
-template <uint32_t F, uint32_t TF, bool LM>
+template <uint32_t F, uint32_t TF, int LM>
 __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) void k_paths_g(DevScene<double> S0, PassGeom g, CameraRec<double> cam,
                                                                                      Work<double> w, uint32_t* next_slot) {
     using R = double;
@@ -803,7 +807,14 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
         s_g = g;
     }
     DevScene<double> S = S0;
-    if constexpr (LM) {
+    if constexpr (LM == 2) {  // the first n_lds_nodes nodes (the top levels of every BVH) into LDS
+        BvhNode* m = reinterpret_cast<BvhNode*>(smem + paths_g_head_bytes(g.stack, B));
+        const uint4* s4 = reinterpret_cast<const uint4*>(S0.nodes);
+        uint4* d4 = reinterpret_cast<uint4*>(m);
+        for (uint32_t i = threadIdx.x; i < S0.n_lds_nodes * (sizeof(BvhNode) / 16); i += B) d4[i] = s4[i];
+        S.nodes_lds = static_cast<uint32_t>(reinterpret_cast<size_t>((__attribute__((address_space(3))) BvhNode*)m));
+    }
+    if constexpr (LM == 1) {
         uint8_t* m = smem + paths_g_head_bytes(g.stack, B);
         const size_t nb = sizeof(BvhNode) * S0.n_nodes, pb = align16(sizeof(uint32_t) * S0.n_primrefs);
         const size_t tb = (F & F_TRI) ? sizeof(TriRec<double>) * (ART_LEAF_TRIS ? S0.n_primrefs : S0.n_tris) : 0;
@@ -898,7 +909,7 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
                        ART_DBITS(st.ray.o.y), ART_DBITS(st.ray.o.z), ART_DBITS(st.ray.d.x), ART_DBITS(st.ray.d.y), ART_DBITS(st.ray.d.z),
                        ART_DBITS(st.ray.tm), static_cast<unsigned long long>(st.rng));
 #endif
-            const bool hitw = trace_world<R, F, B, false>(S, nullptr, st.ray, stk, st.rng, t, h);
+            const bool hitw = trace_world<R, F, B, false, LM == 2>(S, nullptr, st.ray, stk, st.rng, t, h);
             ART_TICK(tm_trace);
             if (hitw) {
                 Surf<R> s;
@@ -1611,16 +1622,29 @@ static void launch_paths_g_ft(int num_cu, hipStream_t st, const DevScene<double>
                          paths_g_mesh_bytes(S.n_nodes, S.n_primrefs, (F & F_TRI) ? (ART_LEAF_TRIS ? S.n_primrefs : S.n_tris) : 0u);
 #if ART_LDS_MESH
     if (S.n_nodes > 0 && lds_m <= kPathsGLdsCap) {
-        const int blocks = blocks_per_cu(reinterpret_cast<const void*>(k_paths_g<F, TF, true>), kBlockM, lds_m) * num_cu;
-        hipLaunchKernelGGL((k_paths_g<F, TF, true>), dim3(blocks), dim3(kBlockM), lds_m, st, S, g, cam, w, next_slot);
+        const int blocks = blocks_per_cu(reinterpret_cast<const void*>(k_paths_g<F, TF, 1>), kBlockM, lds_m) * num_cu;
+        hipLaunchKernelGGL((k_paths_g<F, TF, 1>), dim3(blocks), dim3(kBlockM), lds_m, st, S, g, cam, w, next_slot);
         return;
     }
 #else
     (void)lds_m;
 #endif
+#if ART_LDS_PARTIAL
+    // too large for LM 1: as many of the first (top-level) nodes as fit beside the stacks
+    const size_t head = paths_g_head_bytes(g.stack, kBlockM);
+    const uint32_t fit = head < kPathsGLdsCap ? static_cast<uint32_t>((kPathsGLdsCap - head) / sizeof(BvhNode)) : 0u;
+    if (S.n_nodes > 0 && fit >= kLdsPartialMinNodes) {
+        DevScene<double> SP = S;
+        SP.n_lds_nodes = std::min<uint32_t>(fit, S.n_nodes);
+        const size_t lds_p = head + sizeof(BvhNode) * SP.n_lds_nodes;
+        const int blocks = blocks_per_cu(reinterpret_cast<const void*>(k_paths_g<F, TF, 2>), kBlockM, lds_p) * num_cu;
+        hipLaunchKernelGGL((k_paths_g<F, TF, 2>), dim3(blocks), dim3(kBlockM), lds_p, st, SP, g, cam, w, next_slot);
+        return;
+    }
+#endif
     const size_t lds = paths_g_head_bytes(g.stack, kBlock);
-    const int blocks = blocks_per_cu(reinterpret_cast<const void*>(k_paths_g<F, TF, false>), kBlock, lds) * num_cu;
-    hipLaunchKernelGGL((k_paths_g<F, TF, false>), dim3(blocks), dim3(kBlock), lds, st, S, g, cam, w, next_slot);
+    const int blocks = blocks_per_cu(reinterpret_cast<const void*>(k_paths_g<F, TF, 0>), kBlock, lds) * num_cu;
+    hipLaunchKernelGGL((k_paths_g<F, TF, 0>), dim3(blocks), dim3(kBlock), lds, st, S, g, cam, w, next_slot);
 }
 static void launch_paths_g(uint32_t feat, bool tex_basic, int num_cu, hipStream_t st, const DevScene<double>& S, const PassGeom& g,
                            const CameraRec<double>& cam, const Work<double>& w, uint32_t* next_slot) {
