@@ -20,7 +20,7 @@ LIB_PATH = os.environ.get("ART_LIB") or os.path.join(_HERE, "libart.so")  # ART_
 RT_OK = 0
 RT_FP64 = 0  # the only fp_mode since ABI 2 (include/art.h)
 RT_ABI_VERSION = 2
-RT_OUT_DEVICE, RT_PROFILE, RT_GLOBAL_SCENE, RT_SPLIT_SHADE, RT_ADAPTIVE, RT_WAVEFRONT = 1, 2, 4, 8, 16, 32
+RT_OUT_DEVICE, RT_PROFILE, RT_GLOBAL_SCENE, RT_SPLIT_SHADE, RT_ADAPTIVE, RT_WAVEFRONT, RT_PARALLEL_IMAGES = 1, 2, 4, 8, 16, 32, 64
 ERRORS = {-1: "RT_E_INVALID", -2: "RT_E_SCENE", -3: "RT_E_DEVICE", -4: "RT_E_INTERNAL"}
 
 

@@ -243,6 +243,7 @@ int rt_render(rt_scene* s, const rt_camera* cam, const rt_params* p, uint8_t* ou
     std::string why;
     if (!s || !cam) return fail(RT_E_INVALID, "scene and camera must be non-NULL");
     if (!valid_params(p, why)) return fail(RT_E_INVALID, why);
+    if ((p->flags & RT_ADAPTIVE) && (p->flags & RT_PARALLEL_IMAGES)) return fail(RT_E_INVALID, "RT_ADAPTIVE and RT_PARALLEL_IMAGES are two engine modes");
     if (p->flags & RT_ADAPTIVE) {
         const int rows = rt_local_rows(p, nullptr);
         if (p->width % 12 != 0 || rows % 12 != 0 || (p->band_count > 1 && p->band_rows % 12 != 0))
@@ -264,7 +265,8 @@ int rt_render_progressive(rt_scene* s, const rt_camera* cam, const rt_params* p,
     std::string why;
     if (!s || !cam || !cb || !out_rgb8) return fail(RT_E_INVALID, "scene, camera, callback and out_rgb8 must be non-NULL");
     if (!valid_params(p, why)) return fail(RT_E_INVALID, why);
-    if (p->flags & RT_ADAPTIVE) return fail(RT_E_INVALID, "progressive rendering traces whole frames (no RT_ADAPTIVE)");
+    if (p->flags & (RT_ADAPTIVE | RT_PARALLEL_IMAGES))
+        return fail(RT_E_INVALID, "progressive rendering traces whole frames of consecutive samples (no RT_ADAPTIVE or RT_PARALLEL_IMAGES)");
     return guard(RT_E_DEVICE, [&] {
         if (!s->renderer) s->renderer = std::make_unique<art::Renderer>(s->flat, s->device);
         art::RenderParams rp = render_params(p);

@@ -1031,6 +1031,41 @@ __global__ __launch_bounds__(256) void k_accum(PassGeom g, Work<R> w) {
     a[2] = b;
 }
 
+// engine_mode::parallel_images (engine.h:378-445): sample s of a pixel belongs to partial image s / m (m = spp / 4).
+// Its samples are summed in order into the quarter sum q (f64, as the reference's pixel_color); when the quarter's
+// last sample is in, write_color_raw<float> rounds q to float and the running image sum takes it:
+// acc = ((c1 + c2) + c3) + c4 in double, the reference's `pixel_color1 + ... + pixel_color4`.  q persists across passes.
+template <class R>
+__global__ __launch_bounds__(256) void k_accum_images(PassGeom g, Work<R> w, double* qsum, uint32_t m) {
+    const uint32_t qi = blockIdx.x * blockDim.x + threadIdx.x;
+    if (qi >= g.npix_pad) return;
+    int lx, ly;
+    if (!slot_pixel(g, qi, lx, ly)) return;
+    const size_t pix = static_cast<size_t>(ly) * g.W + lx;
+    double* a = w.acc + 3 * pix;
+    double* q = qsum + 3 * pix;
+    double ar = a[0], ag = a[1], ab = a[2], qr = q[0], qg = q[1], qb = q[2];
+    for (uint32_t j = 0; j < g.k; ++j) {
+        double x, y, z;
+        load_res(w.res, j * g.npix_pad + qi, x, y, z);
+        qr += x;
+        qg += y;
+        qb += z;
+        if ((g.sample_base + j + 1) % m == 0) {
+            ar += static_cast<double>(static_cast<float>(qr));
+            ag += static_cast<double>(static_cast<float>(qg));
+            ab += static_cast<double>(static_cast<float>(qb));
+            qr = qg = qb = 0.0;
+        }
+    }
+    a[0] = ar;
+    a[1] = ag;
+    a[2] = ab;
+    q[0] = qr;
+    q[1] = qg;
+    q[2] = qb;
+}
+
 #if ART_SPLIT_PATHS != 2
 // Ray queries (rt_trace_rays): the world's closest hit (hittable_list::hit, hittable_list.cpp:5-19) of n caller-given
 // rays through the renderer's own traversal -- the LDS image (L) or the HBM scene -- and the surface normal
@@ -1746,12 +1781,15 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     // Slot ids, FastDiv operands and shard capacities are u32 and exact below 2^31: a pass never holds more than
     // kMaxPassSlots slots, whether k comes from free memory or from the caller's samples_per_pass.
     if (g.npix_pad > kMaxPassSlots) throw std::runtime_error("image too large for one pass (more than 2^31 padded pixels)");
+    // samples traced per pixel: spp, or parallel_images' 4 * (spp / 4) (engine.h:411-414)
+    const bool images = (p.flags & RT_PARALLEL_IMAGES) != 0;
+    const int spp_t = images ? 4 * (p.spp / 4) : p.spp;
     const uint64_t k_cap = std::max<uint64_t>(1, kMaxPassSlots / g.npix_pad);
     uint64_t k64 = p.samples_per_pass > 0 ? static_cast<uint64_t>(p.samples_per_pass) : std::max<uint64_t>(1, target / g.npix_pad);
-    k64 = std::min<uint64_t>(std::min<uint64_t>(k64, k_cap), static_cast<uint64_t>(p.spp));
+    k64 = std::min<uint64_t>(std::min<uint64_t>(k64, k_cap), static_cast<uint64_t>(std::max(1, spp_t)));
     uint32_t k = static_cast<uint32_t>(k64);
-    const int npasses = static_cast<int>((p.spp + k - 1) / k);
-    k = static_cast<uint32_t>((p.spp + npasses - 1) / npasses);
+    const int npasses = static_cast<int>((std::max(1, spp_t) + k - 1) / k);
+    k = static_cast<uint32_t>((std::max(1, spp_t) + npasses - 1) / npasses);
     const uint64_t Pmax64 = static_cast<uint64_t>(k) * g.npix_pad;
     if (Pmax64 > kMaxPassSlots) throw std::runtime_error("internal: pass larger than 2^31 slots");
     const uint32_t Pmax = static_cast<uint32_t>(Pmax64);
@@ -1773,6 +1811,7 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     const size_t o_seg = off; off += al(sizeof(unsigned long long));
     const size_t o_acc = off; off += al(sizeof(double) * 3 * local_pix);
     const size_t o_rgb = off; off += al(3 * local_pix);
+    const size_t o_qsum = off; off += images ? al(sizeof(double) * 3 * local_pix) : 0;  // parallel_images quarter sums
     // adaptive mode: int work frame, pixel list (<= 80 of every 144 pixels per level), square flags, list counter
     const bool adapt_ws = (p.flags & RT_ADAPTIVE) != 0;
     const size_t nsq_ws = adapt_ws ? local_pix / (kBig * kBig) : 0;
@@ -1799,6 +1838,7 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     w.segments = reinterpret_cast<unsigned long long*>(base + o_seg);
     w.acc = reinterpret_cast<double*>(base + o_acc);
     uint8_t* drgb = reinterpret_cast<uint8_t*>(base + o_rgb);
+    double* qsum = reinterpret_cast<double*>(base + o_qsum);
 
     CameraRec<R> cam{};
     for (int a = 0; a < 3; ++a) {
@@ -1838,9 +1878,10 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
             kk = std::max<uint32_t>(1, std::min<uint32_t>(static_cast<uint32_t>(p.spp), Pmax / std::max<uint32_t>(g.npix_pad, 64u)));
         }
         HIP_OK(hipMemsetAsync(w.acc, 0, sizeof(double) * 3 * npix, stream));
-        for (uint32_t sb = 0; sb < static_cast<uint32_t>(p.spp); sb += kk) {
+        if (images) HIP_OK(hipMemsetAsync(qsum, 0, sizeof(double) * 3 * npix, stream));
+        for (uint32_t sb = 0; sb < static_cast<uint32_t>(spp_t); sb += kk) {
             g.sample_base = sb;
-            g.k = std::min<uint32_t>(kk, static_cast<uint32_t>(p.spp) - sb);
+            g.k = std::min<uint32_t>(kk, static_cast<uint32_t>(spp_t) - sb);
             g.P = g.k * g.npix_pad;
             g.live = g.k * npix;
             HIP_OK(hipMemsetAsync(w.counters, 0, 4ull * cnt_words, stream));
@@ -1862,7 +1903,12 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
                     bounce<R>(ds, variant, I.num_cu, stream, g, cam, w, d, prof ? std::function<void()>(mark) : std::function<void()>());
                 ext_launches += static_cast<uint64_t>(p.max_depth);
             }
-            hipLaunchKernelGGL(k_accum<R>, dim3((g.npix_pad + 255) / 256), dim3(256), 0, stream, g, w);
+            if (images) {
+                hipLaunchKernelGGL(k_accum_images<R>, dim3((g.npix_pad + 255) / 256), dim3(256), 0, stream, g, w, qsum,
+                                   static_cast<uint32_t>(spp_t / 4));
+            } else {
+                hipLaunchKernelGGL(k_accum<R>, dim3((g.npix_pad + 255) / 256), dim3(256), 0, stream, g, w);
+            }
             ++passes_run;
             spp_done = static_cast<int>(sb + g.k);
             // progressive snapshot (whole-image traces only): write_color of the sums so far, with the samples so far
@@ -1949,7 +1995,7 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     stats.samples_per_pass = static_cast<int>(k);
     stats.segments = segs;
     stats.extend_variant = variant;
-    stats.primary = traced * static_cast<uint64_t>(stopped ? spp_done : p.spp);
+    stats.primary = traced * static_cast<uint64_t>(stopped ? spp_done : spp_t);
     if (prof) {
         double ext_ms = 0, sh_ms = 0;
         for (size_t e = 0; e + 2 < ev_next; e += 3) {

@@ -10,7 +10,7 @@ import enum
 
 import numpy as np
 
-from ._lib import RT_ADAPTIVE, RT_FP64, rt_progress_fn, RT_GLOBAL_SCENE, RT_OUT_DEVICE, RT_PROFILE, RT_SPLIT_SHADE, RT_WAVEFRONT, check, dvec, lib, rt_camera, rt_params, rt_stats
+from ._lib import RT_ADAPTIVE, RT_FP64, RT_PARALLEL_IMAGES, rt_progress_fn, RT_GLOBAL_SCENE, RT_OUT_DEVICE, RT_PROFILE, RT_SPLIT_SHADE, RT_WAVEFRONT, check, dvec, lib, rt_camera, rt_params, rt_stats
 from .scene import compile_world
 
 
@@ -95,8 +95,9 @@ class engine:
     def run(self, output_image, accum=None, band_rows=None, band_count=1, band_index=0, profile=False, stream=None):
         """Renders into output_image (uint8, local_rows x W x 3).  Returns elapsed ms, or -1 on an empty world
         (engine.h:32-36).  `accum` (optional, float64 local_rows x W x 3) receives the per-pixel radiance sums.
-        engine_mode.adaptive runs _run_adaptive (engine.h:151-333) on the GPU; single / parallel_stripes /
-        parallel_images all trace every pixel (their only differences are the reference's CPU threading)."""
+        engine_mode.adaptive runs _run_adaptive (engine.h:151-333) on the GPU; engine_mode.parallel_images runs
+        _run_parallel_images (engine.h:378-445: four float partial images of spp/4 samples, summed); single and
+        parallel_stripes compute the same image (their only difference is the reference's CPU threading)."""
         if self._scene is None:
             print("Invalid input scene!")
             return -1
@@ -108,6 +109,7 @@ class engine:
             raise ValueError("engine_mode.adaptive interpolates most pixels: there are no radiance sums to return")
         flags = ((RT_PROFILE if profile else 0) | (RT_GLOBAL_SCENE if self.global_scene else 0)
                  | (RT_SPLIT_SHADE if self.split_shade else 0) | (RT_ADAPTIVE if adaptive else 0)
+                 | (RT_PARALLEL_IMAGES if self.m == engine_mode.parallel_images else 0)
                  | (RT_WAVEFRONT if self.wavefront else 0))
         p = self.params(band_rows, band_count, band_index, flags, stream)
         rows = check(lib.rt_local_rows(ctypes.byref(p), None), "rt_local_rows")
@@ -133,8 +135,9 @@ class engine:
         if self._scene is None:
             print("Invalid input scene!")
             return -1
-        if self.m == engine_mode.adaptive:
-            raise ValueError("progressive rendering traces whole frames (engine_mode.adaptive is not progressive)")
+        if self.m in (engine_mode.adaptive, engine_mode.parallel_images):
+            raise ValueError("progressive rendering traces whole frames of consecutive samples "
+                             "(engine_mode.adaptive / parallel_images are not progressive)")
         p = self.params(None, 1, 0, 0, None)
         p.samples_per_pass = int(samples_per_pass)
         nbytes = self.height * self.width * 3

@@ -71,6 +71,11 @@ extern "C" {
                                band_count > 1, and out_accum NULL (interpolated pixels have no radiance sums). */
 #define RT_WAVEFRONT 32     /* LDS-scene renders: one fused extend launch per bounce depth (paths stored in HBM between
                                bounces) instead of the persistent-path kernel (A/B and parity tests) */
+#define RT_PARALLEL_IMAGES 64 /* engine_mode::parallel_images (engine.h:378-445): four partial images of spp/4 samples
+                               each (samples [q*spp/4, (q+1)*spp/4) of every pixel's streams), every pixel's partial
+                               sum rounded to float (write_color_raw<float>), the four summed in double and written
+                               with the full spp -- the reference's float rounding and its spp/4 truncation included.
+                               out_accum receives that sum.  Not with RT_ADAPTIVE or progressive rendering. */
 
 typedef struct rt_scene rt_scene;
 typedef struct rt_graph rt_graph;
@@ -147,8 +152,8 @@ void rt_scene_destroy(rt_scene* scene);
 int rt_scene_save(const rt_scene* scene, const char* path);
 int rt_scene_load(const char* path, int device, rt_scene** out);
 
-/* ---- render (engine::run; the engine_mode is rt_params.flags & RT_ADAPTIVE: single, parallel_stripes and
- * parallel_images all compute every pixel and are one mode here) ----
+/* ---- render (engine::run; the engine_mode is in rt_params.flags: RT_ADAPTIVE, RT_PARALLEL_IMAGES, or neither for
+ * single and parallel_stripes, which compute the same image) ----
  * out_rgb8: local_rows * width * 3 bytes (row-major, local row 0 = the first row this band set owns, top-most first);
  * out_accum (optional): local_rows * width * 3 f64 radiance sums (pixel_color before write_color).  Host pointers
  * unless RT_OUT_DEVICE.  Blocking. */

@@ -137,7 +137,8 @@ public:
     }
 
     // engine.h:30-54: blocking, fills W*H*3 bytes (row 0 = top); returns the elapsed milliseconds, or -1 for an empty
-    // world.  Every engine_mode computes every pixel; adaptive traces corners and interpolates (engine.h:96-333).
+    // world.  single and parallel_stripes compute the same image; adaptive traces corners and interpolates
+    // (engine.h:96-333); parallel_images sums four float images of spp/4 samples (engine.h:378-445).
     int run(std::uint8_t* out) {
         if (!world_.objects || world_.info.objects == 0) {
             std::fprintf(stderr, "Invalid input scene!\n");
@@ -159,7 +160,7 @@ public:
             return -1;
         }
         rt_params p = params();
-        if (p.flags & RT_ADAPTIVE) throw std::logic_error("engine::run_progressive: no progressive adaptive mode");
+        if (p.flags & (RT_ADAPTIVE | RT_PARALLEL_IMAGES)) throw std::logic_error("engine::run_progressive: adaptive and parallel_images are not progressive");
         p.samples_per_pass = samples_per_pass;
         struct ctx_t {
             const std::function<bool(int, const std::uint8_t*)>* fn;
@@ -193,7 +194,7 @@ private:
         p.band_rows = h_;
         p.band_count = 1;
         p.band_index = 0;
-        p.flags = mode_ == engine_mode::adaptive ? RT_ADAPTIVE : 0;
+        p.flags = mode_ == engine_mode::adaptive ? RT_ADAPTIVE : mode_ == engine_mode::parallel_images ? RT_PARALLEL_IMAGES : 0;
         for (int k = 0; k < 3; ++k) p.background[k] = background_.e[k];
         return p;
     }

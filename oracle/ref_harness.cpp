@@ -15,10 +15,13 @@
 //
 // Commands:
 //   ref_harness kat N                               first N random_double() of a fresh generator
-//   ref_harness render SCENE W H SPP OUT [single|stripes T|adaptive]
+//   ref_harness render SCENE W H SPP OUT [single|stripes T|adaptive|images]
 //                                                   writes OUT.rgb (u8) and OUT.acc (f64 sums; zero in adaptive
 //                                                   mode), prints JSON.  "adaptive" = `_run_adaptive` (engine.h:96-333)
-//                                                   with its 4 stripes run one after another (deterministic)
+//                                                   with its 4 stripes run one after another (deterministic);
+//                                                   "images" = `_run_parallel_images` (engine.h:378-445) with its 4
+//                                                   partial images traced one after another (OUT.acc: the pixel_acc
+//                                                   sum of the four float images)
 //   ref_harness probe SCENE K                       next K random_double() after the scene build (RNG pin)
 //   ref_harness dump SCENE OUT.json                 canonical dump of the scene graph (scene pin)
 //   ref_harness mesh SCENE|PATH.obj OUT.bin                 post-triangulation triangle list: u32 n, f32 xyz*3*n, f64 rgb*n (solid albedo,
@@ -351,8 +354,46 @@ int cmd_render(const std::string& name, int W, int H, int spp, const std::string
         std::transform(work.begin(), work.end(), rgb.begin(), [](int v) { return static_cast<std::uint8_t>(v); });
     };
 
+    // engine.h:378-445 (_run_parallel_images) on reference types: four partial images of spp/4 samples each, stored
+    // as float by write_color_raw<float> (no gamma), summed as colors and written with the full spp.  The reference
+    // runs the four on 4 threads sharing the global RNG; here they run one after another.
+    auto run_images = [&](long long& segs) {
+        const int m = spp / 4;
+        std::vector<float> part(static_cast<size_t>(W) * H * 3 * 4, 0.f);
+        for (int q = 0; q < 4; ++q)
+            for (int j = 0; j < H; ++j)
+                for (int i = 0; i < W; ++i) {
+                    color pixel_color(0, 0, 0);
+                    for (int s = 0; s < m; ++s) {
+                        auto u = (i + random_double()) / (W - 1);
+                        auto v = ((H - 1 - j) + random_double()) / (H - 1);
+                        ray r = cam.get_ray(u, v);
+                        pixel_color += ray_color(r, world.background, objs, 50, segs);
+                    }
+                    write_color_raw<float>(part.data() + (static_cast<size_t>(q) * H * W + static_cast<size_t>(j) * W + i) * 3, pixel_color);
+                }
+        for (int j = 0; j < H; ++j)
+            for (int i = 0; i < W; ++i) {
+                color c[4];
+                for (int q = 0; q < 4; ++q) {
+                    const float* f = part.data() + (static_cast<size_t>(q) * H * W + static_cast<size_t>(j) * W + i) * 3;
+                    c[q] = color(f[0], f[1], f[2]);
+                }
+                const color pixel_acc = c[0] + c[1] + c[2] + c[3];
+                const size_t o = 3 * (static_cast<size_t>(j) * W + i);
+                acc[o + 0] = pixel_acc[0];
+                acc[o + 1] = pixel_acc[1];
+                acc[o + 2] = pixel_acc[2];
+                write_color(rgb.data() + o, pixel_acc, spp);
+            }
+    };
+
     const auto start = std::chrono::steady_clock::now();
-    if (mode == "adaptive") {
+    if (mode == "images") {
+        long long segs = 0;
+        run_images(segs);
+        g_segments += segs;
+    } else if (mode == "adaptive") {
         if (W % 12 != 0 || H % 12 != 0) throw std::logic_error("for adaptive strategy image size should perfectly fit big square size for now!!");
         long long segs = 0;
         run_adaptive(segs);

@@ -1209,6 +1209,79 @@ int orc_render(const char* scene, int W, int H, int spp, int max_depth, int mode
     return -1;
 }
 
+// engine.h:378-445 (_run_parallel_images), see restate.h.
+int orc_render_images(const char* scene, int W, int H, int spp, int max_depth, int mode, uint64_t seed, int threads,
+                      uint8_t* rgb_out, double* acc_out, long long* segments_out, double* ms_out) try {
+    if (W < 2 || H < 2 || spp < 1 || max_depth < 0) {
+        g_err = "invalid render arguments";
+        return -2;
+    }
+    Scene s;
+    Rng scene_rng;
+    build_scene(s, scene, scene_rng);
+    Camera cam(s.lookfrom, s.lookat, V3(0, 1, 0), s.vfov, static_cast<double>(W) / static_cast<double>(H), s.aperture, 10.0, 0.0, 1.0);
+    const int m = spp / 4;  // tracer_constants::samples_per_pixel / 4 per partial image
+    std::vector<float> part(static_cast<size_t>(W) * H * 3 * 4, 0.f);
+    auto t0 = std::chrono::steady_clock::now();
+    std::atomic<long long> segs_total{0};
+    // partial image q of pixel (i, j): run_image's _stochastic_sample (engine.h:395-405) + write_color_raw<float>
+    auto partial = [&](int q, int i, int j, Rng& rng, long long& segs) {
+        V3 pc(0, 0, 0);
+        for (int k = 0; k < m; ++k) {
+            if (mode == ORC_PCG)
+                rng.state = pcg_seed(seed, static_cast<uint32_t>(j) * static_cast<uint32_t>(W) + static_cast<uint32_t>(i), static_cast<uint32_t>(q * m + k));
+            double ru = rng.d();
+            double rv = rng.d();
+            Ray r = cam.get_ray((i + ru) / (W - 1), ((H - 1 - j) + rv) / (H - 1), rng);
+            pc += mode == ORC_PCG ? ray_color_iter(s, r, max_depth, rng, segs) : ray_color_rec(s, r, max_depth, rng, segs);
+        }
+        float* f = part.data() + (static_cast<size_t>(q) * H * W + static_cast<size_t>(j) * W + i) * 3;
+        f[0] = static_cast<float>(pc[0]);
+        f[1] = static_cast<float>(pc[1]);
+        f[2] = static_cast<float>(pc[2]);
+    };
+    if (mode == ORC_MT) {
+        long long segs = 0;
+        for (int q = 0; q < 4; ++q)
+            for (int j = 0; j < H; ++j)
+                for (int i = 0; i < W; ++i) partial(q, i, j, scene_rng, segs);
+        segs_total = segs;
+    } else {
+        const int nt = threads > 0 ? threads : static_cast<int>(std::max(1u, std::thread::hardware_concurrency()));
+        std::atomic<int> next{0};
+        std::vector<std::thread> pool;
+        for (int t = 0; t < nt; ++t)
+            pool.emplace_back([&]() {
+                Rng rng;
+                rng.pcg = true;
+                long long segs = 0;
+                for (int it = next++; it < 4 * H; it = next++)
+                    for (int i = 0; i < W; ++i) partial(it / H, i, it % H, rng, segs);
+                segs_total += segs;
+            });
+        for (auto& th : pool) th.join();
+    }
+    for (int j = 0; j < H; ++j)  // engine.h:424-440
+        for (int i = 0; i < W; ++i) {
+            V3 c[4];
+            for (int q = 0; q < 4; ++q) {
+                const float* f = part.data() + (static_cast<size_t>(q) * H * W + static_cast<size_t>(j) * W + i) * 3;
+                c[q] = V3(f[0], f[1], f[2]);
+            }
+            const V3 acc = c[0] + c[1] + c[2] + c[3];
+            const size_t o = 3 * (static_cast<size_t>(j) * W + i);
+            if (acc_out) { acc_out[o] = acc[0]; acc_out[o + 1] = acc[1]; acc_out[o + 2] = acc[2]; }
+            if (rgb_out) write_color(rgb_out + o, acc, spp);
+        }
+    auto t1 = std::chrono::steady_clock::now();
+    if (segments_out) *segments_out = segs_total.load();
+    if (ms_out) *ms_out = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    return 0;
+} catch (const std::exception& e) {
+    g_err = e.what();
+    return -1;
+}
+
 int orc_render_rows(const char* scene, int W, int H, int spp, int max_depth, uint64_t seed, const int* rows, int nrows, int threads,
                     uint8_t* rgb_out, double* acc_out, long long* segments_out, double* ms_out) try {
     if (W < 2 || H < 2 || spp < 1 || max_depth < 0 || nrows < 0 || (nrows > 0 && !rows)) {

@@ -55,6 +55,14 @@ int orc_trace_rays(const char* scene, const double* rays, long long n, double* t
 int orc_render_adaptive(const char* scene, int W, int H, int spp, int max_depth, int mode, uint64_t seed, int threads,
                         uint8_t* rgb_out, long long* segments_out, double* ms_out);
 
+// engine_mode::parallel_images (engine.h:378-445) over the whole WxH image: four partial images of spp/4 samples each,
+// each pixel's sum rounded to float (write_color_raw<float>), pixel_acc = ((c1 + c2) + c3) + c4 in double, written
+// with the full spp.  ORC_MT: the reference's draw sequence with the four images traced one after another
+// (bit-exact vs `ref_harness render .. images`); ORC_PCG: partial image q takes samples [q*spp/4, (q+1)*spp/4) of
+// the product's (pixel, sample) streams.  acc_out: the pixel_acc sums (H*W*3 f64, may be NULL).
+int orc_render_images(const char* scene, int W, int H, int spp, int max_depth, int mode, uint64_t seed, int threads,
+                      uint8_t* rgb_out, double* acc_out, long long* segments_out, double* ms_out);
+
 const char* orc_last_error(void);
 
 #ifdef __cplusplus

@@ -22,6 +22,8 @@ fixtures pin:
                        bytes the reference's stb_image decodes from it (`ref_harness texture`); `make_golden.py images`
   * render_adaptive_<scene>.npz  engine_mode::adaptive renders (engine.h:96-333, its 4 stripes run in order):
                        RGB8 and segment count (`python tests/golden/make_golden.py adaptive` makes only these)
+  * render_images_<scene>.npz  engine_mode::parallel_images renders (engine.h:378-445, its 4 partial images traced
+                       in order): RGB8, the pixel_acc sums and the segment count (`make_golden.py images_mode`)
 Assets written by the same harness: assets/*.tris (the reference's post-triangulation triangle lists: cow,
 dino, capsule incl. its texture coordinates; the oracle's mesh input and the pin of the product's OBJ loader),
 assets/earthmap.rgb and assets/models/capsule/capsule.rgb.gz (stb_image-decoded texels, the latter gzipped).
@@ -67,6 +69,22 @@ def adaptive_fixtures():
         np.savez_compressed(os.path.join(HERE, f"render_adaptive_{sc}_{W}x{H}x{spp}.npz"), rgb=rgb,
                             segments=np.int64(info["segments"]), W=W, H=H, spp=spp)
         print("adaptive", sc, info)
+
+
+# engine_mode::parallel_images (engine.h:378-445; the four partial images traced in order): spp not a multiple of 4,
+# so 4 * (spp / 4) samples are traced and write_color divides by spp, as the reference does
+IMAGES = [("c1", 48, 27, 10), ("4", 40, 24, 6)]
+
+
+def images_mode_fixtures():
+    for sc, W, H, spp in IMAGES:
+        tmp = "/tmp/golden_images"
+        info = json.loads(run("render", sc, W, H, spp, tmp, "images").strip().splitlines()[-1])
+        rgb = np.fromfile(tmp + ".rgb", np.uint8).reshape(H, W, 3)
+        acc = np.fromfile(tmp + ".acc", np.float64).reshape(H, W, 3)
+        np.savez_compressed(os.path.join(HERE, f"render_images_{sc}_{W}x{H}x{spp}.npz"), rgb=rgb, acc=acc,
+                            segments=np.int64(info["segments"]), W=W, H=H, spp=spp)
+        print("images", sc, info)
 
 
 STAT = ("1", 384, 216, 16)
@@ -180,6 +198,9 @@ def main():
     if sys.argv[1:] == ["images"]:
         image_fixtures()
         return
+    if sys.argv[1:] == ["images_mode"]:
+        images_mode_fixtures()
+        return
     if sys.argv[1:2] == ["scene"]:
         path = os.path.join(HERE, "scenes.json")
         scenes = json.load(open(path))
@@ -206,6 +227,7 @@ def main():
     adaptive_fixtures()
     stat_fixtures()
     image_fixtures()
+    images_mode_fixtures()
 
 
 if __name__ == "__main__":

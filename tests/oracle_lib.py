@@ -32,6 +32,9 @@ def oracle():
         lib.orc_render_adaptive.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                             ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p,
                                             ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double)]
+        lib.orc_render_images.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double)]
         lib.orc_set_asset_dir(ASSETS.encode())
         _lib = lib
     return _lib
@@ -88,6 +91,19 @@ def oracle_render_adaptive(scene, W, H, spp, mode="pcg", seed=0, threads=0, max_
     if r != 0:
         raise RuntimeError(lib.orc_last_error().decode())
     return {"rgb": rgb, "segments": segs.value, "ms": ms.value}
+
+
+def oracle_render_images(scene, W, H, spp, mode="pcg", seed=0, threads=0, max_depth=50):
+    """engine_mode::parallel_images (engine.h:378-445): four float partial images of spp/4 samples summed."""
+    lib = oracle()
+    rgb = np.zeros((H, W, 3), np.uint8)
+    acc = np.zeros((H, W, 3), np.float64)
+    segs, ms = ctypes.c_longlong(), ctypes.c_double()
+    r = lib.orc_render_images(str(scene).encode(), W, H, spp, max_depth, MODES[mode], seed, threads, rgb.ctypes.data,
+                              acc.ctypes.data, ctypes.byref(segs), ctypes.byref(ms))
+    if r != 0:
+        raise RuntimeError(lib.orc_last_error().decode())
+    return {"rgb": rgb, "acc": acc, "segments": segs.value, "ms": ms.value}
 
 
 def oracle_dump(scene):

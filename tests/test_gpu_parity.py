@@ -206,3 +206,35 @@ def test_adaptive_band_partition_is_bit_identical(gpu):
         segs += eng.stats["segments"]
     assert np.array_equal(img, full)
     assert segs == e.stats["segments"]
+
+
+@pytest.mark.parametrize("scene,spp,per_pass", [("1", 10, 3), ("cow", 9, 0), ("4", 6, 5), ("8", 8, 2)])
+def test_parallel_images_matches_oracle_pcg(gpu, scene, spp, per_pass):
+    """engine_mode::parallel_images (engine.h:378-445): four float partial images of spp/4 samples, summed and written
+    with the full spp.  RGB8, the f64 sums and the segment count equal the oracle's, with passes that split the
+    quarters (samples_per_pass 3 of m = 2, 5 of m = 1, 2 of m = 2)."""
+    from tests.oracle_lib import oracle_render_images
+    W, H = 64, 36
+    world = art.scene_manager().build(scene)
+    cam = art.camera(world.lookfrom, world.lookat, (0, 1, 0), world.vfov, W / H, world.aperture, 10.0, 0.0, 1.0)
+    eng = art.engine(cam, art.engine_mode.parallel_images, width=W, height=H, samples_per_pixel=spp, samples_per_pass=per_pass)
+    eng.set_scene(world.objects, world.background)
+    img = np.zeros((H, W, 3), np.uint8)
+    acc = np.zeros((H, W, 3), np.float64)
+    eng.run(img, accum=acc)
+    o = oracle_render_images(scene, W, H, spp, mode="pcg")
+    assert np.array_equal(img, o["rgb"])
+    assert np.array_equal(acc, o["acc"])
+    assert eng.stats["segments"] == o["segments"]
+    assert eng.stats["primary"] == W * H * 4 * (spp // 4)
+
+
+def test_parallel_images_below_four_spp_is_black(gpu):
+    """spp < 4: the reference's four partial images get spp/4 = 0 samples each, so every pixel is write_color(0, spp)."""
+    world = art.scene_manager().build("1")
+    cam = art.camera(world.lookfrom, world.lookat, (0, 1, 0), world.vfov, 2.0, world.aperture, 10.0, 0.0, 1.0)
+    eng = art.engine(cam, art.engine_mode.parallel_images, width=32, height=16, samples_per_pixel=3)
+    eng.set_scene(world.objects, world.background)
+    img = np.full((16, 32, 3), 7, np.uint8)
+    eng.run(img)
+    assert not img.any() and eng.stats["segments"] == 0

@@ -7,7 +7,8 @@ import os
 import numpy as np
 import pytest
 
-from tests.oracle_lib import REF_HARNESS, oracle_dump, oracle_kat, oracle_probe, oracle_render, oracle_render_adaptive
+from tests.oracle_lib import (REF_HARNESS, oracle_dump, oracle_kat, oracle_probe, oracle_render, oracle_render_adaptive,
+                              oracle_render_images)
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 SCENES = ["c1", "1", "2", "3", "4", "5", "6", "7", "8", "cow", "dino", "9"]
@@ -119,3 +120,29 @@ def test_adaptive_pcg_traces_corners_like_the_full_render():
 def test_adaptive_rejects_sizes_off_the_12px_grid():
     with pytest.raises(RuntimeError, match="big square"):
         oracle_render_adaptive("c1", 50, 36, 2)
+
+
+IMAGES = [("c1", 48, 27, 10), ("4", 40, 24, 6)]
+
+
+@pytest.mark.parametrize("scene,W,H,spp", IMAGES)
+def test_parallel_images_mt_bit_exact(scene, W, H, spp):
+    """engine_mode::parallel_images (engine.h:378-445) restated: bit-exact (RGB8, the float-image sums, segments) vs
+    the reference's own render with its four partial images traced in order; spp not a multiple of 4."""
+    g = np.load(os.path.join(GOLD, f"render_images_{scene}_{W}x{H}x{spp}.npz"))
+    o = oracle_render_images(scene, W, H, spp, mode="mt")
+    assert o["segments"] == int(g["segments"])
+    assert np.array_equal(o["rgb"], g["rgb"])
+    assert np.array_equal(o["acc"], g["acc"])
+
+
+def test_parallel_images_pcg_is_the_quartered_sum():
+    """pcg mode: partial image q holds samples [q*m, (q+1)*m) of the full render's streams, each sum rounded to float;
+    thread count does not matter."""
+    W, H, spp = 32, 18, 9
+    a = oracle_render_images("1", W, H, spp, mode="pcg", threads=1)
+    b = oracle_render_images("1", W, H, spp, mode="pcg", threads=3)
+    assert np.array_equal(a["acc"], b["acc"]) and a["segments"] == b["segments"]
+    full = oracle_render("1", W, H, 8, mode="pcg")  # the same 8 samples, summed in one f64 run
+    assert a["segments"] == full["segments"]
+    assert np.allclose(a["acc"], full["acc"], rtol=1e-6, atol=1e-9)
