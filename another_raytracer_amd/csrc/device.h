@@ -894,10 +894,12 @@ __device__ __forceinline__ bool hit_medium(const DevScene<R>& S, const uint8_t* 
             t2 = r_far;
             if (t2 < tmin2 || inf < t2) return false;
         }
-    } else {
+    } else if constexpr ((F & F_MEDIA_G) != 0) {
         uint32_t p, f, mt;
         if (!hit_object<R, F, B, L, PL>(S, lds, m.a, r, -inf, inf, stk, t1, p, f, mt)) return false;
         if (!hit_object<R, F, B, L, PL>(S, lds, m.a, r, t1 + R(0.0001), inf, stk, t2, p, f, mt)) return false;
+    } else {
+        return false;  // unreachable: a scene with a non-sphere medium boundary has F_MEDIA_G
     }
     if (t1 < tmin) t1 = tmin;
     if (t2 > tmax) t2 = tmax;
@@ -965,14 +967,19 @@ __device__ __forceinline__ void set_face_normal(Surf<R>& s, const Ray<R>& r, V3<
     s.ff = dot(r.d, outward) < R(0);
     s.n = s.ff ? outward : -outward;
 }
-template <class R>
+template <class R, bool UV = true>
 __device__ __forceinline__ void rect_surface(Surf<R>& s, int axis, R a0, R a1, R b0, R b1, R k, const Ray<R>& r, R t) {
-    const int ia = axis == 2 ? 1 : 0;
-    const int ib = axis == 0 ? 1 : 2;
-    const R x = comp(r.o, ia) + t * comp(r.d, ia);
-    const R y = comp(r.o, ib) + t * comp(r.d, ib);
-    s.u = (x - a0) / (a1 - a0);
-    s.v = (y - b0) / (b1 - b0);
+    if (UV) {  // u, v feed image textures only
+        const int ia = axis == 2 ? 1 : 0;
+        const int ib = axis == 0 ? 1 : 2;
+        const R x = comp(r.o, ia) + t * comp(r.d, ia);
+        const R y = comp(r.o, ib) + t * comp(r.d, ib);
+        s.u = (x - a0) / (a1 - a0);
+        s.v = (y - b0) / (b1 - b0);
+    } else {
+        s.u = R(0);
+        s.v = R(0);
+    }
     const V3<R> n = axis == 0 ? mk(R(0), R(0), R(1)) : (axis == 1 ? mk(R(0), R(1), R(0)) : mk(R(1), R(0), R(0)));
     set_face_normal(s, r, n);
     s.p = r.at(t);
@@ -1010,19 +1017,24 @@ __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref,
             const V3<R> p1 = ld3(tr.p), p2 = ld3(tr.p + 3), p3 = ld3(tr.p + 6);
             const V3<R> N = cross(p2 - p1, p3 - p1);
             const V3<R> p = r.o + t * r.d;
-            const R u = dot(N, cross(p3 - p2, p - p2));
-            const R v = dot(N, cross(p1 - p3, p - p3));
             s.p = p;
             set_face_normal(s, r, N);
-            s.u = u / len2(N);
-            s.v = v / len2(N);
+            if (UV) {  // barycentric u, v feed image textures only (texture.h:135-154)
+                const R u = dot(N, cross(p3 - p2, p - p2));
+                const R v = dot(N, cross(p1 - p3, p - p3));
+                s.u = u / len2(N);
+                s.v = v / len2(N);
+            } else {
+                s.u = R(0);
+                s.v = R(0);
+            }
             s.mat = tr.mat;
             break;
         }
         case PRIM_RECT: {
             if (!(F & F_RECT)) break;
             const RectRec<R>& q = S.rects[idx];
-            rect_surface(s, static_cast<int>(q.axis), q.a0, q.a1, q.b0, q.b1, q.k, r, t);
+            rect_surface<R, UV>(s, static_cast<int>(q.axis), q.a0, q.a1, q.b0, q.b1, q.k, r, t);
             s.mat = q.mat;
             break;
         }
@@ -1032,7 +1044,7 @@ __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref,
             int axis;
             R a0, a1, b0, b1, k;
             box_face(b, static_cast<int>(face), axis, a0, a1, b0, b1, k);
-            rect_surface(s, axis, a0, a1, b0, b1, k, r, t);
+            rect_surface<R, UV>(s, axis, a0, a1, b0, b1, k, r, t);
             s.mat = b.mat;
             break;
         }

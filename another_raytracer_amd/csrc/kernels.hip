@@ -1696,7 +1696,8 @@ static void launch_paths_g(uint32_t feat, bool tex_basic, int num_cu, hipStream_
             else launch_paths_g_ft<kFeatMesh & ~F_TRI, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
         }
     } else if ((feat & F_TRI) == 0) {  // e.g. the Next-Week final: no triangle code in the kernel
-        launch_paths_g_ft<F_ALL & ~F_TRI, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
+        if (feat & F_MEDIA_G) launch_paths_g_ft<F_ALL & ~F_TRI, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
+        else launch_paths_g_ft<F_ALL & ~F_TRI & ~F_MEDIA_G, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
     } else {
         launch_paths_g_ft<F_ALL, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
     }

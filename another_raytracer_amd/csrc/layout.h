@@ -135,7 +135,9 @@ struct ObjRec {
 };
 constexpr int kMaxXformChain = 2;  // translate(rotate_y(X)) is the deepest chain in the reference scenes
 // Scene features: kernels are instantiated for feature subsets (spheres only / meshes / everything).
-enum Feature : uint32_t { F_SPHERE = 1u, F_TRI = 2u, F_RECT = 4u, F_BOX = 8u, F_XFORM = 16u, F_MEDIA = 32u, F_ALL = 63u };
+// F_MEDIA: constant_medium objects; F_MEDIA_G: one of them has a boundary that is not a sphere primitive (its two
+// boundary hits are whole object traversals; a sphere boundary is one quadratic, device.h hit_medium)
+enum Feature : uint32_t { F_SPHERE = 1u, F_TRI = 2u, F_RECT = 4u, F_BOX = 8u, F_XFORM = 16u, F_MEDIA = 32u, F_MEDIA_G = 64u, F_ALL = 127u };
 constexpr uint32_t kFeatSpheres = F_SPHERE;
 constexpr uint32_t kFeatMesh = F_SPHERE | F_TRI | F_RECT | F_MEDIA;
 

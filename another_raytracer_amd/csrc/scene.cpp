@@ -896,8 +896,13 @@ FlatScene compile_scene(const SceneGraph& g) {
     if (f.max_stack > kMaxStackDepth) throw std::runtime_error("bvh needs a deeper traversal stack than kMaxStackDepth");
     f.features = (f.spheres.empty() ? 0u : F_SPHERE) | (f.tris.empty() ? 0u : F_TRI) | (f.rects.empty() ? 0u : F_RECT) |
                  (f.boxes.empty() ? 0u : F_BOX) | (f.has_media ? F_MEDIA : 0u);
-    for (const auto& o : f.objs)
+    for (const auto& o : f.objs) {
         if (o.kind == OBJ_TRANSLATE || o.kind == OBJ_ROTATE_Y) f.features |= F_XFORM;
+        if (o.kind == OBJ_MEDIUM) {
+            const ObjRec<double>& b = f.objs[o.a];
+            if (!(b.kind == OBJ_PRIM && primref_type(static_cast<uint32_t>(b.a)) == PRIM_SPHERE)) f.features |= F_MEDIA_G;
+        }
+    }
     relabel_level_major(f);
     return f;
 }
