@@ -228,7 +228,7 @@ struct DevScene {
     const uint8_t* texels;
     const TriRec<R>* leaf_tris;  // leaf_tris[slot] = tris[index of primrefs[slot]] for triangle refs, zeros otherwise
     const uint8_t* lds_image;   // layout.h LDS scene image (nullptr unless the scene qualifies)
-    uint32_t n_nodes, n_primrefs, n_tris;  // array lengths (k_paths_g's LDS copy of a small mesh scene)
+    uint32_t n_nodes, n_primrefs, n_tris, n_objs;  // array lengths (k_paths_g's LDS copies)
     uint32_t nodes_lds;         // k_paths_g LM 2: LDS byte address of the copy of nodes [0, n_lds_nodes) (top levels)
     uint32_t n_lds_nodes;
     int32_t nworld;

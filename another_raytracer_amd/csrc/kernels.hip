@@ -786,6 +786,11 @@ __host__ __device__ constexpr size_t paths_g_stack_bytes(uint32_t stack, int blo
 __host__ __device__ constexpr size_t paths_g_head_bytes(uint32_t stack, int block) {  // stack, camera, pass geometry
     return align16(paths_g_stack_bytes(stack, block) + sizeof(CameraRec<double>) + sizeof(PassGeom));
 }
+// LM kernels also hold the world list and the object records (a few KiB): every segment walks them, and a prim
+// object's test otherwise waits on three dependent L1 loads (world slot -> object -> primitive)
+__host__ __device__ constexpr size_t paths_g_world_bytes(int32_t nworld, uint32_t n_objs) {
+    return align16(sizeof(int32_t) * static_cast<uint32_t>(nworld)) + sizeof(ObjRec<double>) * n_objs;
+}
 __host__ __device__ constexpr size_t paths_g_mesh_bytes(uint32_t n_nodes, uint32_t n_primrefs, uint32_t n_tris) {  // n_tris: 0 unless F_TRI
     return sizeof(BvhNode) * n_nodes + align16(sizeof(uint32_t) * n_primrefs) + sizeof(TriRec<double>) * n_tris;
 }
@@ -807,15 +812,26 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
         s_g = g;
     }
     DevScene<double> S = S0;
+    size_t lm_off = paths_g_head_bytes(g.stack, B);  // LM: world list and objects, then the BVH arrays
+    if constexpr (LM != 0) {
+        uint8_t* wb = smem + lm_off;
+        for (int32_t i = static_cast<int32_t>(threadIdx.x); i < S0.nworld; i += B) reinterpret_cast<int32_t*>(wb)[i] = S0.world[i];
+        uint8_t* ob = wb + align16(sizeof(int32_t) * static_cast<uint32_t>(S0.nworld));
+        const uint4* os = reinterpret_cast<const uint4*>(S0.objs);
+        for (uint32_t i = threadIdx.x; i < S0.n_objs * (sizeof(ObjRec<double>) / 16); i += B) reinterpret_cast<uint4*>(ob)[i] = os[i];
+        S.world = reinterpret_cast<const int32_t*>(wb);
+        S.objs = reinterpret_cast<const ObjRec<double>*>(ob);
+        lm_off += paths_g_world_bytes(S0.nworld, S0.n_objs);
+    }
     if constexpr (LM == 2) {  // the first n_lds_nodes nodes (the top levels of every BVH) into LDS
-        BvhNode* m = reinterpret_cast<BvhNode*>(smem + paths_g_head_bytes(g.stack, B));
+        BvhNode* m = reinterpret_cast<BvhNode*>(smem + lm_off);
         const uint4* s4 = reinterpret_cast<const uint4*>(S0.nodes);
         uint4* d4 = reinterpret_cast<uint4*>(m);
         for (uint32_t i = threadIdx.x; i < S0.n_lds_nodes * (sizeof(BvhNode) / 16); i += B) d4[i] = s4[i];
         S.nodes_lds = static_cast<uint32_t>(reinterpret_cast<size_t>((__attribute__((address_space(3))) BvhNode*)m));
     }
     if constexpr (LM == 1) {
-        uint8_t* m = smem + paths_g_head_bytes(g.stack, B);
+        uint8_t* m = smem + lm_off;
         const size_t nb = sizeof(BvhNode) * S0.n_nodes, pb = align16(sizeof(uint32_t) * S0.n_primrefs);
         const size_t tb = (F & F_TRI) ? sizeof(TriRec<double>) * (ART_LEAF_TRIS ? S0.n_primrefs : S0.n_tris) : 0;
         auto copy = [&](uint8_t* dst, const void* src, size_t bytes) {
@@ -1473,6 +1489,7 @@ static void build_device_scene(const FlatScene& f, DeviceScene<R>& ds) {
         }
     }
     ds.view.n_nodes = static_cast<uint32_t>(f.nodes.size());
+    ds.view.n_objs = static_cast<uint32_t>(f.objs.size());
     ds.view.n_primrefs = static_cast<uint32_t>(f.primrefs.size());
     ds.view.n_tris = static_cast<uint32_t>(f.tris.size());
     ds.view.nworld = static_cast<int32_t>(f.world.size());
@@ -1653,8 +1670,8 @@ template <uint32_t F, uint32_t TF>
 static void launch_paths_g_ft(int num_cu, hipStream_t st, const DevScene<double>& S, const PassGeom& g, const CameraRec<double>& cam,
                               const Work<double>& w, uint32_t* next_slot) {
     // g.stack = stack_rows: sentinel + entries + spare row
-    const size_t lds_m = paths_g_head_bytes(g.stack, kBlockM) +
-                         paths_g_mesh_bytes(S.n_nodes, S.n_primrefs, (F & F_TRI) ? (ART_LEAF_TRIS ? S.n_primrefs : S.n_tris) : 0u);
+    const size_t lm_head = paths_g_head_bytes(g.stack, kBlockM) + paths_g_world_bytes(S.nworld, S.n_objs);
+    const size_t lds_m = lm_head + paths_g_mesh_bytes(S.n_nodes, S.n_primrefs, (F & F_TRI) ? (ART_LEAF_TRIS ? S.n_primrefs : S.n_tris) : 0u);
 #if ART_LDS_MESH
     if (S.n_nodes > 0 && lds_m <= kPathsGLdsCap) {
         const int blocks = blocks_per_cu(reinterpret_cast<const void*>(k_paths_g<F, TF, 1>), kBlockM, lds_m) * num_cu;
@@ -1666,7 +1683,7 @@ static void launch_paths_g_ft(int num_cu, hipStream_t st, const DevScene<double>
 #endif
 #if ART_LDS_PARTIAL
     // too large for LM 1: as many of the first (top-level) nodes as fit beside the stacks
-    const size_t head = paths_g_head_bytes(g.stack, kBlockM);
+    const size_t head = lm_head;
     const uint32_t fit = head < kPathsGLdsCap ? static_cast<uint32_t>((kPathsGLdsCap - head) / sizeof(BvhNode)) : 0u;
     if (S.n_nodes > 0 && fit >= kLdsPartialMinNodes) {
         DevScene<double> SP = S;
