@@ -227,6 +227,7 @@ struct DevScene {
     const ImageRec* images;
     const uint8_t* texels;
     const TriRec<R>* leaf_tris;  // leaf_tris[slot] = tris[index of primrefs[slot]] for triangle refs, zeros otherwise
+    const PrimRec80* obj_prims;  // obj_prims[o] = the record of prim object o's primitive (indexed like objs)
     const uint8_t* lds_image;   // layout.h LDS scene image (nullptr unless the scene qualifies)
     uint32_t n_nodes, n_primrefs, n_tris, n_objs;  // array lengths (k_paths_g's LDS copies)
     uint32_t nodes_lds;         // k_paths_g LM 2: LDS byte address of the copy of nodes [0, n_lds_nodes) (top levels)
@@ -376,6 +377,18 @@ __device__ __forceinline__ bool hit_box(const BoxRec<R>& b, const Ray<R>& r, R t
     return any;
 }
 
+// The test of a primitive given its record (a prim object's copy, DevScene::obj_prims): the same arithmetic as hit_prim.
+template <class R, uint32_t F>
+__device__ __forceinline__ bool hit_prim_rec(uint32_t type, const PrimRec80& rec, const Ray<R>& r, R tmin, R tmax, R& t, uint32_t& face) {
+    if ((F & F_SPHERE) && (F == F_SPHERE || type == PRIM_SPHERE)) return hit_sphere(reinterpret_cast<const SphereRec<R>&>(rec), r, tmin, tmax, t);
+    if ((F & F_TRI) && (F == F_TRI || type == PRIM_TRIANGLE)) return hit_tri(reinterpret_cast<const TriRec<R>&>(rec), r, tmin, tmax, t);
+    if ((F & F_RECT) && type == PRIM_RECT) {
+        const RectRec<R>& q = reinterpret_cast<const RectRec<R>&>(rec);
+        return hit_rect(static_cast<int>(q.axis), q.a0, q.a1, q.b0, q.b1, q.k, r, tmin, tmax, t);
+    }
+    if ((F & F_BOX) && type == PRIM_BOX) return hit_box(reinterpret_cast<const BoxRec<R>&>(rec), r, tmin, tmax, t, face);
+    return false;
+}
 // F (layout.h Feature bits) prunes the primitive kinds a scene cannot contain, so a kernel instantiated for a
 // spheres-only scene carries no triangle/box/transform/medium code and needs far fewer registers.
 template <class R, uint32_t F>
@@ -526,6 +539,9 @@ __device__ __forceinline__ void stat_lane(int k) { atomicAdd(&g_art_stats[k], 1u
 
 #ifndef ART_SPECULATIVE
 #define ART_SPECULATIVE 1
+#endif
+#ifndef ART_OBJ_PRIMS
+#define ART_OBJ_PRIMS 1  // prim objects test the per-object primitive copy (DevScene::obj_prims)
 #endif
 #ifndef ART_LEAF_TRIS
 #define ART_LEAF_TRIS 1  // triangle leaves read the leaf-ordered copy (DevScene::leaf_tris)
@@ -852,7 +868,9 @@ __device__ __forceinline__ bool hit_object(const DevScene<R>& S, const uint8_t* 
     if (o.kind == OBJ_PRIM) {
         prim = static_cast<uint32_t>(o.a);
         mt = kMatUnknown;
-        return hit_prim<R, F>(S, prim, r, tmin, tmax, t, face);
+        // HBM-scene kernels: the primitive's record from obj_prims[oi], whose address does not wait on the object
+        if constexpr (!L && ART_OBJ_PRIMS) return hit_prim_rec<R, F>(primref_type(prim), S.obj_prims[oi], r, tmin, tmax, t, face);
+        else return hit_prim<R, F>(S, prim, r, tmin, tmax, t, face);
     }
     return traverse<R, F, B, L, PL>(S, lds, o.a, r, tmin, tmax, stk, t, prim, face, mt);
 }
@@ -872,7 +890,10 @@ __device__ __forceinline__ bool hit_medium(const DevScene<R>& S, const uint8_t* 
         // calls (constant_medium.h:43, :46) compute the same oc, half_b, c, discriminant and sqrt (sphere.h:39-47)
         // from the same ray and sphere, so both root selections (sphere.h:49-55) run on one quadratic: the same
         // values, half the arithmetic.
-        const SphereRec<R>& sp = S.spheres[primref_index(static_cast<uint32_t>(bo.a))];
+        const SphereRec<R>& sp = [&]() -> const SphereRec<R>& {
+            if constexpr (!L && ART_OBJ_PRIMS) return reinterpret_cast<const SphereRec<R>&>(S.obj_prims[m.a]);
+            else return S.spheres[primref_index(static_cast<uint32_t>(bo.a))];
+        }();
         V3<R> center = ld3(sp.c);
         if (sp.flags & SPH_MOVING) center = moving_center(center, ld3(sp.d), sp.t0, sp.dt, r.tm);
         const V3<R> oc = r.o - center;

@@ -789,7 +789,7 @@ __host__ __device__ constexpr size_t paths_g_head_bytes(uint32_t stack, int bloc
 // LM kernels also hold the world list and the object records (a few KiB): every segment walks them, and a prim
 // object's test otherwise waits on three dependent L1 loads (world slot -> object -> primitive)
 __host__ __device__ constexpr size_t paths_g_world_bytes(int32_t nworld, uint32_t n_objs) {
-    return align16(sizeof(int32_t) * static_cast<uint32_t>(nworld)) + sizeof(ObjRec<double>) * n_objs;
+    return align16(sizeof(int32_t) * static_cast<uint32_t>(nworld)) + (sizeof(ObjRec<double>) + sizeof(PrimRec80)) * n_objs;
 }
 __host__ __device__ constexpr size_t paths_g_mesh_bytes(uint32_t n_nodes, uint32_t n_primrefs, uint32_t n_tris) {  // n_tris: 0 unless F_TRI
     return sizeof(BvhNode) * n_nodes + align16(sizeof(uint32_t) * n_primrefs) + sizeof(TriRec<double>) * n_tris;
@@ -819,8 +819,12 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
         uint8_t* ob = wb + align16(sizeof(int32_t) * static_cast<uint32_t>(S0.nworld));
         const uint4* os = reinterpret_cast<const uint4*>(S0.objs);
         for (uint32_t i = threadIdx.x; i < S0.n_objs * (sizeof(ObjRec<double>) / 16); i += B) reinterpret_cast<uint4*>(ob)[i] = os[i];
+        uint8_t* pb = ob + sizeof(ObjRec<double>) * S0.n_objs;
+        const uint4* ps = reinterpret_cast<const uint4*>(S0.obj_prims);
+        for (uint32_t i = threadIdx.x; i < S0.n_objs * (sizeof(PrimRec80) / 16); i += B) reinterpret_cast<uint4*>(pb)[i] = ps[i];
         S.world = reinterpret_cast<const int32_t*>(wb);
         S.objs = reinterpret_cast<const ObjRec<double>*>(ob);
+        S.obj_prims = reinterpret_cast<const PrimRec80*>(pb);
         lm_off += paths_g_world_bytes(S0.nworld, S0.n_objs);
     }
     if constexpr (LM == 2) {  // the first n_lds_nodes nodes (the top levels of every BVH) into LDS
@@ -1472,6 +1476,22 @@ static void build_device_scene(const FlatScene& f, DeviceScene<R>& ds) {
     }
     ds.view.nodes = ds.upload(f.nodes);
     ds.view.objs = ds.upload(objs);
+    {  // obj_prims[o]: prim object o's primitive record (device.h hit_object)
+        std::vector<PrimRec80> op(objs.size());
+        for (size_t i = 0; i < objs.size(); ++i) {
+            if (objs[i].kind != OBJ_PRIM) continue;
+            const uint32_t ref = static_cast<uint32_t>(objs[i].a), idx = primref_index(ref);
+            switch (primref_type(ref)) {
+                case PRIM_SPHERE: std::memcpy(op[i].b, &sph[idx], sizeof(sph[idx])); break;
+                case PRIM_TRIANGLE: std::memcpy(op[i].b, &tri[idx], sizeof(tri[idx])); break;
+                case PRIM_RECT: std::memcpy(op[i].b, &rect[idx], sizeof(rect[idx])); break;
+                default: std::memcpy(op[i].b, &box[idx], sizeof(box[idx])); break;
+            }
+        }
+        static_assert(sizeof(SphereRec<R>) <= sizeof(PrimRec80) && sizeof(TriRec<R>) <= sizeof(PrimRec80) &&
+                      sizeof(RectRec<R>) <= sizeof(PrimRec80) && sizeof(BoxRec<R>) <= sizeof(PrimRec80), "PrimRec80 holds every record");
+        ds.view.obj_prims = ds.upload(op);
+    }
     ds.view.world = ds.upload(f.world);
     ds.view.mats = ds.upload(mats);
     ds.view.texs = ds.upload(texs);

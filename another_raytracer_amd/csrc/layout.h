@@ -44,6 +44,11 @@ struct TriRec {         // triangle.h: pt1, pt2, pt3
     uint32_t mat;
     uint32_t pad;
 };
+// One primitive record of any type (SphereRec, TriRec, RectRec, BoxRec are all <= 80 B): the device copy of a prim
+// object's primitive, indexed by object (DevScene::obj_prims)
+struct alignas(16) PrimRec80 {
+    uint8_t b[80];
+};
 template <class R>
 struct RectRec {        // aarect.h: axis 0 = xy_rect (k on z), 1 = xz_rect (k on y), 2 = yz_rect (k on x)
     R a0, a1, b0, b1, k;
