@@ -215,6 +215,7 @@ struct Work {
     uint32_t* counters;         // [(depth * kQueueKinds + kind) * kShards + shard] * kCounterStride
     unsigned long long* segments;
     double* acc;                // local pixels * 3
+    void* pool;                 // k_paths camera-ray rings (ART_RAY_POOL): kPoolRing PoolRays per wave
 };
 template <class R>
 __host__ __device__ __forceinline__ uint32_t* counter(const Work<R>& w, int d, int kind, int s) {
@@ -315,7 +316,7 @@ __device__ __forceinline__ int find_segment(const uint32_t* pre, int n, uint32_t
 // engine.h:58-68 + camera.h:38-47 for slot q (sample j = q / npix_pad of the pass, pixel from the 8x8 tile order).
 // Runs inside the depth-0 extend: the camera ray never round-trips through HBM.
 template <class R>
-__device__ __forceinline__ void gen_ray(const PassGeom& g, const CameraRec<R>& cam, uint32_t q, int lx, int ly, PathState<R>& st) {
+__device__ __forceinline__ void cam_ray(const PassGeom& g, const CameraRec<R>& cam, uint32_t q, int lx, int ly, Ray<R>& ray, uint64_t& rng_out) {
     const uint32_t j = g.fd_npix.div(q);
     const int gy = global_row(g, ly);
     const uint32_t pixel = static_cast<uint32_t>(gy) * static_cast<uint32_t>(g.W) + static_cast<uint32_t>(lx);
@@ -334,12 +335,16 @@ __device__ __forceinline__ void gen_ray(const PassGeom& g, const CameraRec<R>& c
     }
     const V3<R> rd = cam.lens_radius * p;
     const V3<R> offset = rd.x * ld3(cam.u) + rd.y * ld3(cam.v);
-    st.ray.o = ld3(cam.origin) + offset;
-    st.ray.d = ld3(cam.llc) + s * ld3(cam.horizontal) + t * ld3(cam.vertical) - ld3(cam.origin) - offset;
-    st.ray.tm = uniform<R>(rng, cam.time0, cam.time1);
+    ray.o = ld3(cam.origin) + offset;
+    ray.d = ld3(cam.llc) + s * ld3(cam.horizontal) + t * ld3(cam.vertical) - ld3(cam.origin) - offset;
+    ray.tm = uniform<R>(rng, cam.time0, cam.time1);
+    rng_out = rng;
+}
+template <class R>
+__device__ __forceinline__ void gen_ray(const PassGeom& g, const CameraRec<R>& cam, uint32_t q, int lx, int ly, PathState<R>& st) {
+    cam_ray(g, cam, q, lx, ly, st.ray, st.rng);
     st.T = mk(R(1), R(1), R(1));
     st.L = mk(R(0), R(0), R(0));
-    st.rng = rng;
 }
 
 // material.h scatter() for one hit of material type M (compile time: one shade kernel per material type, so a wave
@@ -629,6 +634,19 @@ __global__ __launch_bounds__(L ? kBlockL : kBlock, L ? 1 : ART_EXTEND_MIN_WAVES)
 // below the ~88 M/s a single word sustains).  The bounce arithmetic and the RNG draws are those of the fused
 // k_extend, so images are bit-identical to the wavefront variants.
 constexpr uint32_t kPathChunk = 256;
+// Camera-ray pool (ART_RAY_POOL): a path start is run by the whole wave for however few lanes start a path (~a third
+// of them per round), so the camera rays are generated 64 at a time -- one per lane, converged -- into a per-wave ring
+// in global memory (L2-resident: 8 KiB per wave), and a starting lane loads the next ring entry instead.  Entry pos
+// holds the ray of slot base[(pos / 64) & 1] + pos % 64; tm = NaN marks a padding slot of a partial tile.
+#ifndef ART_RAY_POOL
+#define ART_RAY_POOL 1
+#endif
+constexpr uint32_t kPoolRing = 128;  // two batches of 64
+struct PoolRay {
+    double ox, oy, oz, dx;
+    double dy, dz, tm;
+    uint64_t rng;
+};
 __host__ __device__ constexpr size_t paths_stack_bytes(uint32_t stack) { return (sizeof(int16_t) * stack * kBlockL + 15u) & ~size_t(15); }
 constexpr size_t kJumpBytes = sizeof(JumpEntry) * kJumpEntries;
 __host__ __device__ constexpr size_t paths_lds_bytes(uint32_t stack) {
@@ -668,7 +686,76 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S, PassGe
 #ifdef ART_STATS
     unsigned long long tm_load = 0, tm_trace = 0, tm_shade = 0, tm_app = 0, tm_prev = __builtin_amdgcn_s_memtime();
 #endif
+#if ART_RAY_POOL
+    PoolRay* ring = static_cast<PoolRay*>(w.pool) + static_cast<size_t>(blockIdx.x * (B / 64) + threadIdx.x / 64) * kPoolRing;
+    uint32_t head = 0, tail = 0;    // ring positions consumed / produced (wave-uniform)
+    uint32_t base0 = 0, base1 = 0;  // first slot of the batch in ring half 0 / 1
+    bool exhausted = false;         // every slot of the pass is in a batch
+    // one batch: the next 64 slots of the wave's chunk, a camera ray per lane
+    auto refill = [&]() {
+        if (cur == end) {
+            uint32_t nb = 0;
+            if (lane == 0) nb = atomicAdd(next_slot, kPathChunk);
+            nb = __shfl(nb, 0);
+            cur = nb;
+            end = nb + kPathChunk;
+        }
+        const uint32_t b = cur;
+        cur += 64;
+        const uint32_t slot = b + lane;
+        __asm__ volatile("" ::: "memory");  // the LDS camera loads stay here
+        PoolRay e;
+        e.tm = __builtin_nan("");
+        int lx, ly;
+        if (slot < s_g.P && slot_pixel(s_g, slot - s_g.fd_npix.div(slot) * s_g.npix_pad, lx, ly)) {
+            Ray<R> r;
+            uint64_t rng;
+            cam_ray(s_g, s_cam, slot, lx, ly, r, rng);
+            e.ox = r.o.x; e.oy = r.o.y; e.oz = r.o.z; e.dx = r.d.x;
+            e.dy = r.d.y; e.dz = r.d.z; e.tm = r.tm; e.rng = rng;
+        }
+        ring[(tail + lane) % kPoolRing] = e;
+        if ((tail / 64u) & 1u) base1 = b;
+        else base0 = b;
+        tail += 64;
+        if (b + 64u >= s_g.P) exhausted = true;
+    };
+    refill();
+    if (!exhausted) refill();
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
     for (;;) {
+#if ART_RAY_POOL
+        // every idle lane takes the next ring entry (a padding slot of a partial tile leaves it idle a round)
+        const uint64_t idle = __ballot(!busy && !drained);
+        if (idle) {
+            const uint32_t n = static_cast<uint32_t>(__popcll(idle));
+            const uint32_t rank = static_cast<uint32_t>(__popcll(idle & below));
+            if (!busy && !drained) {
+                const uint32_t pos = head + rank;
+                const uint32_t slot = (((pos / 64u) & 1u) ? base1 : base0) + pos % 64u;
+                if (pos >= tail || slot >= g.P) {
+                    drained = true;
+                } else {
+                    const PoolRay& e = ring[pos % kPoolRing];
+                    const double tm = e.tm;
+                    if (tm == tm) {
+                        st.ray.o = mk(e.ox, e.oy, e.oz);
+                        st.ray.d = mk(e.dx, e.dy, e.dz);
+                        st.ray.tm = tm;
+                        st.rng = e.rng;
+                        st.T = mk(R(1), R(1), R(1));
+                        st.L = mk(R(0), R(0), R(0));
+                        q = slot;
+                        busy = true;
+                        depth = 0;
+                    }
+                }
+            }
+            head = min(head + n, tail);
+            if (!exhausted && tail - head <= 64u) refill();
+        }
+#else
         // every idle lane takes the next slot of the wave's chunk (padding slots of partial tiles stay idle a round)
         const uint64_t idle = __ballot(!busy && !drained);
         if (idle) {
@@ -704,6 +791,7 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S, PassGe
                 }
             }
         }
+#endif
         ART_TICK(tm_load);
         if (__ballot(busy) == 0) {
             if (__ballot(!drained) == 0) break;
@@ -716,6 +804,10 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S, PassGe
             ++segs;
             hitw = trace_world<R, kFeatSpheres, B, true>(S, lds, st.ray, stk, st.rng, t, h);
         }
+#if ART_RAY_POOL
+        // the ring stores of this round's refill (issued before the trace) are complete before the next round's loads
+        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
         ART_TICK(tm_trace);
         // the whole wave draws random_in_unit_sphere for its lambertian and metal hits (material.h:33, :55), which
         // scatter with it first; lights and the max_depth bounce draw nothing
@@ -1850,6 +1942,7 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     const size_t o_acc = off; off += al(sizeof(double) * 3 * local_pix);
     const size_t o_rgb = off; off += al(3 * local_pix);
     const size_t o_qsum = off; off += images ? al(sizeof(double) * 3 * local_pix) : 0;  // parallel_images quarter sums
+    const size_t o_pool = off; off += variant == EXT_MEGA ? al(sizeof(PoolRay) * kPoolRing * (kBlockL / 64) * static_cast<size_t>(I.num_cu)) : 0;
     // adaptive mode: int work frame, pixel list (<= 80 of every 144 pixels per level), square flags, list counter
     const bool adapt_ws = (p.flags & RT_ADAPTIVE) != 0;
     const size_t nsq_ws = adapt_ws ? local_pix / (kBig * kBig) : 0;
@@ -1875,6 +1968,7 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     w.counters = reinterpret_cast<uint32_t*>(base + o_cnt);
     w.segments = reinterpret_cast<unsigned long long*>(base + o_seg);
     w.acc = reinterpret_cast<double*>(base + o_acc);
+    w.pool = base + o_pool;
     uint8_t* drgb = reinterpret_cast<uint8_t*>(base + o_rgb);
     double* qsum = reinterpret_cast<double*>(base + o_qsum);
 
