@@ -102,6 +102,19 @@ def test_persistent_paths_pass_split_is_bit_identical(gpu):
     assert np.array_equal(one["acc"], many["acc"]) and one["segments"] == many["segments"]
 
 
+@pytest.mark.parametrize("W,H,spp", [(2, 2, 1), (9, 3, 3), (13, 70, 2), (130, 2, 5)])
+def test_persistent_paths_small_and_ragged_frames(gpu, W, H, spp):
+    # k_paths takes its camera rays from a per-wave ring filled 64 slots at a time: a pass shorter than one batch
+    # (2x2x1: 64 slots, 60 of them padding), batches made mostly of padding slots of partial 8x8 tiles, and passes
+    # that end inside a batch must all trace exactly the oracle's paths
+    g = gpu_render("1", W, H, spp)
+    o = oracle_render("1", W, H, spp, mode="pcg")
+    assert g["stats"]["extend_variant"] == 3
+    assert np.array_equal(g["rgb"], o["rgb"])
+    assert np.array_equal(g["acc"], o["acc"])
+    assert g["segments"] == o["segments"]
+
+
 def test_general_scenes_use_the_hbm_kernels(gpu):
     # triangles/rects/media (or no BVH) never take the LDS variants: persistent paths over the HBM scene (4), or the
     # per-depth HBM kernels (0) with RT_WAVEFRONT
