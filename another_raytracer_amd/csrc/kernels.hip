@@ -641,11 +641,86 @@ constexpr uint32_t kPathChunk = 256;
 #ifndef ART_RAY_POOL
 #define ART_RAY_POOL 1
 #endif
+#ifndef ART_RAY_POOL_G
+#define ART_RAY_POOL_G 0  // the same ring in k_paths_g: measured -1 % to -4 % (cow, final, dino, capsule, scene 7)
+#endif
 constexpr uint32_t kPoolRing = 128;  // two batches of 64
+constexpr uint32_t kPoolWavesPerCu = 32;  // rings allocated per CU: the most waves a CU holds
 struct PoolRay {
     double ox, oy, oz, dx;
     double dy, dz, tm;
     uint64_t rng;
+};
+// A wave's ring.  Fields other than the pointer are wave-uniform.  refill() is called by the whole wave; take() by
+// the idle lanes of a round, before the round's refill (whose stores then go to entries already read).
+struct RayRing {
+    PoolRay* ring;
+    uint32_t head, tail;    // positions consumed / produced
+    uint32_t base0, base1;  // first slot of the batch in ring half 0 / 1
+    uint32_t cur, end;      // the wave's claimed slot chunk [cur, end)
+    bool exhausted;         // every slot of the pass is in a batch
+    __device__ __forceinline__ void init(void* pool, uint32_t wave) {
+        ring = static_cast<PoolRay*>(pool) + static_cast<size_t>(wave) * kPoolRing;
+        head = tail = base0 = base1 = cur = end = 0;
+        exhausted = false;
+    }
+    __device__ __forceinline__ void refill(const PassGeom& sg, const CameraRec<double>& sc, uint32_t* next_slot, uint32_t lane) {
+        if (cur == end) {
+            uint32_t nb = 0;
+            if (lane == 0) nb = atomicAdd(next_slot, kPathChunk);
+            nb = __shfl(nb, 0);
+            cur = nb;
+            end = nb + kPathChunk;
+        }
+        const uint32_t b = cur;
+        cur += 64;
+        const uint32_t slot = b + lane;
+        __asm__ volatile("" ::: "memory");  // the LDS camera loads stay here
+        PoolRay e;
+        e.tm = __builtin_nan("");
+        int lx, ly;
+        if (slot < sg.P && slot_pixel(sg, slot - sg.fd_npix.div(slot) * sg.npix_pad, lx, ly)) {
+            Ray<double> r;
+            uint64_t rng;
+            cam_ray(sg, sc, slot, lx, ly, r, rng);
+            e.ox = r.o.x; e.oy = r.o.y; e.oz = r.o.z; e.dx = r.d.x;
+            e.dy = r.d.y; e.dz = r.d.z; e.tm = r.tm; e.rng = rng;
+        }
+        ring[(tail + lane) % kPoolRing] = e;
+        if ((tail / 64u) & 1u) base1 = b;
+        else base0 = b;
+        tail += 64;
+        if (b + 64u >= sg.P) exhausted = true;
+    }
+    // The idle lane of rank `rank`: 1 = a path starts (st, q), 0 = a padding slot (the lane idles a round),
+    // 2 = the pass is drained.
+    __device__ __forceinline__ int take(uint32_t rank, uint32_t P, PathState<double>& st, uint32_t& q) const {
+        const uint32_t pos = head + rank;
+        const uint32_t slot = (((pos / 64u) & 1u) ? base1 : base0) + pos % 64u;
+        if (pos >= tail || slot >= P) return 2;
+        const PoolRay& e = ring[pos % kPoolRing];
+        const double tm = e.tm;
+        if (tm != tm) return 0;
+        st.ray.o = mk(e.ox, e.oy, e.oz);
+        st.ray.d = mk(e.dx, e.dy, e.dz);
+        st.ray.tm = tm;
+        st.rng = e.rng;
+        st.T = mk(1.0, 1.0, 1.0);
+        st.L = mk(0.0, 0.0, 0.0);
+        q = slot;
+        return 1;
+    }
+    // after the round's take(): n entries consumed; refill when a batch's worth is free, so an entry is read at
+    // least one round after its stores (ordered by the s_waitcnt vmcnt(0) the path loops place after the trace)
+    __device__ __forceinline__ void advance(uint32_t n, const PassGeom& sg, const CameraRec<double>& sc, uint32_t* next_slot, uint32_t lane) {
+        head = min(head + n, tail);
+        if (!exhausted && tail - head <= 64u) refill(sg, sc, next_slot, lane);
+    }
+    __device__ __forceinline__ void start(const PassGeom& sg, const CameraRec<double>& sc, uint32_t* next_slot, uint32_t lane) {
+        refill(sg, sc, next_slot, lane);
+        if (!exhausted) refill(sg, sc, next_slot, lane);
+        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
 };
 __host__ __device__ constexpr size_t paths_stack_bytes(uint32_t stack) { return (sizeof(int16_t) * stack * kBlockL + 15u) & ~size_t(15); }
 constexpr size_t kJumpBytes = sizeof(JumpEntry) * kJumpEntries;
@@ -687,42 +762,9 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S, PassGe
     unsigned long long tm_load = 0, tm_trace = 0, tm_shade = 0, tm_app = 0, tm_prev = __builtin_amdgcn_s_memtime();
 #endif
 #if ART_RAY_POOL
-    PoolRay* ring = static_cast<PoolRay*>(w.pool) + static_cast<size_t>(blockIdx.x * (B / 64) + threadIdx.x / 64) * kPoolRing;
-    uint32_t head = 0, tail = 0;    // ring positions consumed / produced (wave-uniform)
-    uint32_t base0 = 0, base1 = 0;  // first slot of the batch in ring half 0 / 1
-    bool exhausted = false;         // every slot of the pass is in a batch
-    // one batch: the next 64 slots of the wave's chunk, a camera ray per lane
-    auto refill = [&]() {
-        if (cur == end) {
-            uint32_t nb = 0;
-            if (lane == 0) nb = atomicAdd(next_slot, kPathChunk);
-            nb = __shfl(nb, 0);
-            cur = nb;
-            end = nb + kPathChunk;
-        }
-        const uint32_t b = cur;
-        cur += 64;
-        const uint32_t slot = b + lane;
-        __asm__ volatile("" ::: "memory");  // the LDS camera loads stay here
-        PoolRay e;
-        e.tm = __builtin_nan("");
-        int lx, ly;
-        if (slot < s_g.P && slot_pixel(s_g, slot - s_g.fd_npix.div(slot) * s_g.npix_pad, lx, ly)) {
-            Ray<R> r;
-            uint64_t rng;
-            cam_ray(s_g, s_cam, slot, lx, ly, r, rng);
-            e.ox = r.o.x; e.oy = r.o.y; e.oz = r.o.z; e.dx = r.d.x;
-            e.dy = r.d.y; e.dz = r.d.z; e.tm = r.tm; e.rng = rng;
-        }
-        ring[(tail + lane) % kPoolRing] = e;
-        if ((tail / 64u) & 1u) base1 = b;
-        else base0 = b;
-        tail += 64;
-        if (b + 64u >= s_g.P) exhausted = true;
-    };
-    refill();
-    if (!exhausted) refill();
-    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    RayRing rr;
+    rr.init(w.pool, blockIdx.x * (B / 64) + threadIdx.x / 64);
+    rr.start(s_g, s_cam, next_slot, lane);
 #endif
     for (;;) {
 #if ART_RAY_POOL
@@ -732,28 +774,12 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S, PassGe
             const uint32_t n = static_cast<uint32_t>(__popcll(idle));
             const uint32_t rank = static_cast<uint32_t>(__popcll(idle & below));
             if (!busy && !drained) {
-                const uint32_t pos = head + rank;
-                const uint32_t slot = (((pos / 64u) & 1u) ? base1 : base0) + pos % 64u;
-                if (pos >= tail || slot >= g.P) {
-                    drained = true;
-                } else {
-                    const PoolRay& e = ring[pos % kPoolRing];
-                    const double tm = e.tm;
-                    if (tm == tm) {
-                        st.ray.o = mk(e.ox, e.oy, e.oz);
-                        st.ray.d = mk(e.dx, e.dy, e.dz);
-                        st.ray.tm = tm;
-                        st.rng = e.rng;
-                        st.T = mk(R(1), R(1), R(1));
-                        st.L = mk(R(0), R(0), R(0));
-                        q = slot;
-                        busy = true;
-                        depth = 0;
-                    }
-                }
+                const int got = rr.take(rank, g.P, st, q);
+                drained = got == 2;
+                busy = got == 1;
+                depth = 0;
             }
-            head = min(head + n, tail);
-            if (!exhausted && tail - head <= 64u) refill();
+            rr.advance(n, s_g, s_cam, next_slot, lane);
         }
 #else
         // every idle lane takes the next slot of the wave's chunk (padding slots of partial tiles stay idle a round)
@@ -968,8 +994,32 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
 #ifdef ART_STATS
     unsigned long long tm_load = 0, tm_trace = 0, tm_shade = 0, tm_app = 0, tm_prev = __builtin_amdgcn_s_memtime();
 #endif
+#if ART_RAY_POOL_G
+    RayRing rr;
+    rr.init(w.pool, blockIdx.x * (B / 64) + threadIdx.x / 64);
+    rr.start(s_g, s_cam, next_slot, lane);
+#endif
     for (;;) {
         const uint64_t idle = __ballot(!busy && !drained);
+#if ART_RAY_POOL_G
+        if (idle) {  // the camera-ray ring, as in k_paths
+            const uint32_t n = static_cast<uint32_t>(__popcll(idle));
+            const uint32_t rank = static_cast<uint32_t>(__popcll(idle & below));
+            if (!busy && !drained) {
+                const int got = rr.take(rank, P, st, q);
+                drained = got == 2;
+                busy = got == 1;
+                depth = 0;
+#ifdef ART_TRACE
+                int lx = 0, ly = 0;
+                if (busy) slot_pixel(s_g, q - s_g.fd_npix.div(q) * s_g.npix_pad, lx, ly);
+                tracing = busy && static_cast<long long>(global_row(s_g, ly)) * s_g.W + lx == g_trace_pixel &&
+                          static_cast<long long>(s_g.sample_base + s_g.fd_npix.div(q)) == g_trace_sample;
+#endif
+            }
+            rr.advance(n, s_g, s_cam, next_slot, lane);
+        }
+#else
         if (idle) {
             const uint32_t n = static_cast<uint32_t>(__popcll(idle));
             const uint32_t rank = static_cast<uint32_t>(__popcll(idle & below));
@@ -1005,6 +1055,7 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
                 }
             }
         }
+#endif
         ART_TICK(tm_load);
         if (__ballot(busy) == 0) {
             if (__ballot(!drained) == 0) break;
@@ -1022,6 +1073,9 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
                        ART_DBITS(st.ray.tm), static_cast<unsigned long long>(st.rng));
 #endif
             const bool hitw = trace_world<R, F, B, false, LM == 2>(S, nullptr, st.ray, stk, st.rng, t, h);
+#if ART_RAY_POOL_G
+            __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring stores before the next round's loads
+#endif
             ART_TICK(tm_trace);
             if (hitw) {
                 Surf<R> s;
@@ -1778,6 +1832,11 @@ static int extend_variant(const DeviceScene<R>& ds, int flags) {
     if (!ds.lds_shade || (flags & RT_SPLIT_SHADE)) return EXT_LDS;
     return (flags & RT_WAVEFRONT) ? EXT_FUSED : EXT_MEGA;
 }
+// The persistent kernels' waves index the camera-ray rings (kPoolWavesPerCu per CU allocated)
+static void check_ring_waves(int blocks, int block, int num_cu) {
+    if (static_cast<size_t>(blocks) * static_cast<size_t>(block / 64) > static_cast<size_t>(num_cu) * kPoolWavesPerCu)
+        throw std::runtime_error("internal: persistent grid larger than the camera-ray rings");
+}
 template <uint32_t F, uint32_t TF>
 static void launch_paths_g_ft(int num_cu, hipStream_t st, const DevScene<double>& S, const PassGeom& g, const CameraRec<double>& cam,
                               const Work<double>& w, uint32_t* next_slot) {
@@ -1787,6 +1846,7 @@ static void launch_paths_g_ft(int num_cu, hipStream_t st, const DevScene<double>
 #if ART_LDS_MESH
     if (S.n_nodes > 0 && lds_m <= kPathsGLdsCap) {
         const int blocks = blocks_per_cu(reinterpret_cast<const void*>(k_paths_g<F, TF, 1>), kBlockM, lds_m) * num_cu;
+        check_ring_waves(blocks, kBlockM, num_cu);
         hipLaunchKernelGGL((k_paths_g<F, TF, 1>), dim3(blocks), dim3(kBlockM), lds_m, st, S, g, cam, w, next_slot);
         return;
     }
@@ -1802,12 +1862,14 @@ static void launch_paths_g_ft(int num_cu, hipStream_t st, const DevScene<double>
         SP.n_lds_nodes = std::min<uint32_t>(fit, S.n_nodes);
         const size_t lds_p = head + sizeof(BvhNode) * SP.n_lds_nodes;
         const int blocks = blocks_per_cu(reinterpret_cast<const void*>(k_paths_g<F, TF, 2>), kBlockM, lds_p) * num_cu;
+        check_ring_waves(blocks, kBlockM, num_cu);
         hipLaunchKernelGGL((k_paths_g<F, TF, 2>), dim3(blocks), dim3(kBlockM), lds_p, st, SP, g, cam, w, next_slot);
         return;
     }
 #endif
     const size_t lds = paths_g_head_bytes(g.stack, kBlock);
     const int blocks = blocks_per_cu(reinterpret_cast<const void*>(k_paths_g<F, TF, 0>), kBlock, lds) * num_cu;
+    check_ring_waves(blocks, kBlock, num_cu);
     hipLaunchKernelGGL((k_paths_g<F, TF, 0>), dim3(blocks), dim3(kBlock), lds, st, S, g, cam, w, next_slot);
 }
 static void launch_paths_g(uint32_t feat, bool tex_basic, int num_cu, hipStream_t st, const DevScene<double>& S, const PassGeom& g,
@@ -1942,7 +2004,7 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     const size_t o_acc = off; off += al(sizeof(double) * 3 * local_pix);
     const size_t o_rgb = off; off += al(3 * local_pix);
     const size_t o_qsum = off; off += images ? al(sizeof(double) * 3 * local_pix) : 0;  // parallel_images quarter sums
-    const size_t o_pool = off; off += variant == EXT_MEGA ? al(sizeof(PoolRay) * kPoolRing * (kBlockL / 64) * static_cast<size_t>(I.num_cu)) : 0;
+    const size_t o_pool = off; off += (variant == EXT_MEGA || (ART_RAY_POOL_G && variant == EXT_MEGA_G)) ? al(sizeof(PoolRay) * kPoolRing * kPoolWavesPerCu * static_cast<size_t>(I.num_cu)) : 0;
     // adaptive mode: int work frame, pixel list (<= 80 of every 144 pixels per level), square flags, list counter
     const bool adapt_ws = (p.flags & RT_ADAPTIVE) != 0;
     const size_t nsq_ws = adapt_ws ? local_pix / (kBig * kBig) : 0;
