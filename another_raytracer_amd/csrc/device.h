@@ -614,11 +614,26 @@ __device__ __forceinline__ float f32_dir(double d) {
     const float f = static_cast<float>(d);
     return __builtin_copysignf(fmaxf(__builtin_fabsf(f), 0x1p-64f), f);
 }
+// Suspendable traversal (k_paths_g, ART_SUSPEND_LANES): a world-level BVH traversal may stop at a phase boundary when
+// fewer than ART_SUSPEND_LANES lanes of the wave are still traversing, keeping its node, parked leaf and stack depth
+// (the stack stays in LDS) so the wave can shade and restart the lanes that finished and resume it next round with
+// them: the lane runs the same sequence of node visits and leaf tests, only spread over rounds.
+#ifndef ART_SUSPEND_LANES
+#define ART_SUSPEND_LANES 24  // measured over 8-40 on cow and the capsule (24: +8 %; 8: +4 %; 40: +7 %)
+#endif
+struct TravResume {
+    int32_t node, parked, sp;
+    bool fresh;  // no traversal in progress: start at the root
+    bool allow;  // wave-uniform: suspending is allowed in this round (paths remain to be started)
+    bool suspended;
+};
 // B: lanes per block (LDS stack stride).  L: nodes and leaf spheres come from the LDS scene image at `lds`.
-template <class R, uint32_t F, int B, bool L, bool PL = false>
+// RES: resumable (rs non-null), HBM-scene variant only.
+template <class R, uint32_t F, int B, bool L, bool PL = false, bool RES = false>
 __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* lds, int32_t root, const Ray<R>& r, R tmin, R tmax,
-                                         StackT<L>* stk, R& t, uint32_t& prim, uint32_t& face, uint32_t& mt) {
+                                         StackT<L>* stk, R& t, uint32_t& prim, uint32_t& face, uint32_t& mt, TravResume* rs = nullptr) {
     static_assert(!(L && (F & F_MEDIA)), "packed LDS keys need tmin > 0: no medium boundary tests in the LDS variant");
+    static_assert(!RES || (!L && ART_SPECULATIVE), "resumable traversal: HBM-scene speculative variant only");
     const float ox = static_cast<float>(r.o.x), oy = static_cast<float>(r.o.y), oz = static_cast<float>(r.o.z);
     // hardware reciprocal (1 ulp): the box test is conservative by its 2e-6 relative padding, far above that
 #if ART_RCP_CLAMP
@@ -656,8 +671,27 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
     // tested together.  Nodes visited past a parked leaf used the older (larger) tmax: extra visits, same closest hit.
     int32_t parked = kNodeEmpty;
 #endif
+    if constexpr (RES) {
+        if (!rs->fresh) {
+            node = rs->node;
+            parked = rs->parked;
+            st.sp = rs->sp;
+        }
+    }
+    [[maybe_unused]] bool progressed = false;
     ART_STAT_LANE(6);
     for (;;) {
+        if constexpr (RES) {
+            if (rs->allow && progressed && __popcll(__ballot(true)) < ART_SUSPEND_LANES) {
+                rs->node = node;
+                rs->parked = parked;
+                rs->sp = st.sp;
+                rs->fresh = false;
+                rs->suspended = true;
+                return hit;
+            }
+            progressed = true;
+        }
         ART_STAT_WAVE(4);
         ART_STAT_LANE(5);
         while (node >= 0) {
@@ -852,9 +886,9 @@ __device__ __forceinline__ Ray<R> xform_in(const ObjRec<R>& o, const Ray<R>& r) 
 }
 
 // Any non-medium object: prim, BVH, or a translate/rotate_y chain (<= kMaxXformChain) over one of them.
-template <class R, uint32_t F, int B, bool L, bool PL = false>
+template <class R, uint32_t F, int B, bool L, bool PL = false, bool RES = false>
 __device__ __forceinline__ bool hit_object(const DevScene<R>& S, const uint8_t* lds, int32_t oi, Ray<R> r, R tmin, R tmax, StackT<L>* stk,
-                                           R& t, uint32_t& prim, uint32_t& face, uint32_t& mt) {
+                                           R& t, uint32_t& prim, uint32_t& face, uint32_t& mt, TravResume* rs = nullptr) {
     if (F & F_XFORM) {
 #pragma unroll
         for (int c = 0; c < kMaxXformChain; ++c) {
@@ -872,7 +906,7 @@ __device__ __forceinline__ bool hit_object(const DevScene<R>& S, const uint8_t* 
         if constexpr (!L && ART_OBJ_PRIMS) return hit_prim_rec<R, F>(primref_type(prim), S.obj_prims[oi], r, tmin, tmax, t, face);
         else return hit_prim<R, F>(S, prim, r, tmin, tmax, t, face);
     }
-    return traverse<R, F, B, L, PL>(S, lds, o.a, r, tmin, tmax, stk, t, prim, face, mt);
+    return traverse<R, F, B, L, PL, RES>(S, lds, o.a, r, tmin, tmax, stk, t, prim, face, mt, rs);
 }
 
 // Out of line: measured +0.2 % (cow) to +1.8 % (Next-Week final) over the inlined body, which raised the register
@@ -973,6 +1007,57 @@ __device__ __forceinline__ bool trace_world(const DevScene<R>& S, const uint8_t*
     }
     t = closest;
     return any;
+}
+
+// trace_world with suspendable BVH traversals (ART_SUSPEND_LANES): the world list walk of one segment, resumed at
+// world slot w with the closest hit so far.  Returns true when the segment's trace is complete.  Medium boundaries
+// and prim objects never suspend.
+template <class R>
+struct TraceState {
+    R closest;
+    HitOut h;
+    int32_t w;
+    bool any;
+    TravResume tr;
+    __device__ __forceinline__ void start() {
+        closest = R(__builtin_inf());
+        any = false;
+        w = 0;
+        tr.fresh = true;
+    }
+};
+template <class R, uint32_t F, int B, bool PL>
+__device__ __forceinline__ bool trace_world_res(const DevScene<R>& S, const Ray<R>& r, StackT<false>* stk, uint64_t& rng, TraceState<R>& ts) {
+    ts.tr.suspended = false;
+    for (int32_t w = ts.w; w < S.nworld; ++w) {
+        const int32_t oi = S.world[w];
+        const ObjRec<R>& o = S.objs[oi];
+        R tt;
+        if ((F & F_MEDIA) && o.kind == OBJ_MEDIUM) {
+            if (hit_medium<R, F, B, false, PL>(S, nullptr, o, r, R(0.001), ts.closest, stk, rng, tt)) {
+                ts.closest = tt;
+                ts.any = true;
+                ts.h.prim = kMediumHit;
+                ts.h.obj = static_cast<uint32_t>(w);
+                ts.h.mt = kMatUnknown;
+            }
+        } else {
+            uint32_t prim = 0, face = 0, mt = kMatUnknown;
+            if (hit_object<R, F, B, false, PL, true>(S, nullptr, oi, r, R(0.001), ts.closest, stk, tt, prim, face, mt, &ts.tr)) {
+                ts.closest = tt;
+                ts.any = true;
+                ts.h.prim = prim;
+                ts.h.obj = static_cast<uint32_t>(w) | (face << 16);
+                ts.h.mt = mt;
+            }
+            if (ts.tr.suspended) {
+                ts.w = w;
+                return false;
+            }
+            ts.tr.fresh = true;
+        }
+    }
+    return true;
 }
 
 // ------------------------------------------------------------------------------------------------ surfaces

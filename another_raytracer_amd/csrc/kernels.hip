@@ -988,6 +988,11 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
     int depth = 0;
     PathState<R> st;
     unsigned long long segs = 0;
+    // suspendable BVH traversals (ART_SUSPEND_LANES) where node fetches go to L2 (LM 0, 2); with the whole BVH in LDS
+    // (LM 1) a traversal is short and suspending only adds rounds
+    constexpr bool SUSP = ART_SUSPEND_LANES > 0 && LM != 1;
+    TraceState<R> ts;  // the lane's segment trace, possibly suspended in a BVH
+    bool in_trace = false;
 #ifdef ART_TRACE
     bool tracing = false;
 #endif
@@ -1061,23 +1066,39 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
             if (__ballot(!drained) == 0) break;
             continue;
         }
+        const bool allow = SUSP && __ballot(drained) == 0;  // suspend only while there are paths to start
         if (busy) {
             R t;
             HitOut h{0, 0, kMatUnknown};
-            ++segs;
             bool cont = false;
+            const bool fresh = !in_trace;
+            if (fresh) {
+                ++segs;
+                if constexpr (SUSP) ts.start();
+            }
 #ifdef ART_TRACE
-            if (tracing)
+            if (tracing && fresh)
                 printf("TRACE d=%d o=%016llx,%016llx,%016llx dir=%016llx,%016llx,%016llx tm=%016llx rng=%016llx\n", depth, ART_DBITS(st.ray.o.x),
                        ART_DBITS(st.ray.o.y), ART_DBITS(st.ray.o.z), ART_DBITS(st.ray.d.x), ART_DBITS(st.ray.d.y), ART_DBITS(st.ray.d.z),
                        ART_DBITS(st.ray.tm), static_cast<unsigned long long>(st.rng));
 #endif
-            const bool hitw = trace_world<R, F, B, false, LM == 2>(S, nullptr, st.ray, stk, st.rng, t, h);
+            bool hitw;
+            if constexpr (SUSP) {
+                ts.tr.allow = allow;
+                in_trace = !trace_world_res<R, F, B, LM == 2>(S, st.ray, stk, st.rng, ts);
+                hitw = ts.any;
+                t = ts.closest;
+                h = ts.h;
+            } else {
+                hitw = trace_world<R, F, B, false, LM == 2>(S, nullptr, st.ray, stk, st.rng, t, h);
+            }
+            const bool susp = in_trace;  // suspended: nothing to shade this round
 #if ART_RAY_POOL_G
             __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring stores before the next round's loads
 #endif
             ART_TICK(tm_trace);
-            if (hitw) {
+            if (susp) {
+            } else if (hitw) {
                 Surf<R> s;
                 world_surface<R, F, (TF & TF_IMAGE) != 0>(S, h, st.ray, t, s);
 #ifdef ART_TRACE
@@ -1113,7 +1134,8 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
                 st.L = st.L + st.T * bg;
             }
             ART_TICK(tm_shade);
-            if (cont) {
+            if (susp) {
+            } else if (cont) {
                 ++depth;
             } else {
                 store_res(w.res, q, st.L);
