@@ -623,8 +623,9 @@ __device__ __forceinline__ float f32_dir(double d) {
 #endif
 struct TravResume {
     int32_t node, parked, sp;
-    bool fresh;  // no traversal in progress: start at the root
-    bool allow;  // wave-uniform: suspending is allowed in this round (paths remain to be started)
+    int32_t lanes;  // suspend when fewer lanes of the wave are traversing
+    bool fresh;     // no traversal in progress: start at the root
+    bool allow;     // wave-uniform: suspending is allowed in this round (paths remain to be started)
     bool suspended;
 };
 // B: lanes per block (LDS stack stride).  L: nodes and leaf spheres come from the LDS scene image at `lds`.
@@ -682,7 +683,7 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
     ART_STAT_LANE(6);
     for (;;) {
         if constexpr (RES) {
-            if (rs->allow && progressed && __popcll(__ballot(true)) < ART_SUSPEND_LANES) {
+            if (rs->allow && progressed && __popcll(__ballot(true)) < rs->lanes) {
                 rs->node = node;
                 rs->parked = parked;
                 rs->sp = st.sp;

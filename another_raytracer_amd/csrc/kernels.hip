@@ -990,7 +990,11 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
     unsigned long long segs = 0;
     // suspendable BVH traversals (ART_SUSPEND_LANES) where node fetches go to L2 (LM 0, 2); with the whole BVH in LDS
     // (LM 1) a traversal is short and suspending only adds rounds
-    constexpr bool SUSP = ART_SUSPEND_LANES > 0 && LM != 1;
+#ifndef ART_SUSPEND_LANES_LM1
+#define ART_SUSPEND_LANES_LM1 0  // LM 1 (BVH in LDS): thresholds 4-40 measured -5 % to -22 % on dino and the final scene
+#endif
+    constexpr int kSuspLanes = LM == 1 ? ART_SUSPEND_LANES_LM1 : ART_SUSPEND_LANES;
+    constexpr bool SUSP = kSuspLanes > 0;
     TraceState<R> ts;  // the lane's segment trace, possibly suspended in a BVH
     bool in_trace = false;
 #ifdef ART_TRACE
@@ -1085,6 +1089,7 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
             bool hitw;
             if constexpr (SUSP) {
                 ts.tr.allow = allow;
+                ts.tr.lanes = kSuspLanes;
                 in_trace = !trace_world_res<R, F, B, LM == 2>(S, st.ray, stk, st.rng, ts);
                 hitw = ts.any;
                 t = ts.closest;
