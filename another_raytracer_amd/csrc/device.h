@@ -462,15 +462,25 @@ __device__ __forceinline__ uint32_t slab_key_packed(float x0, float x1, float y0
     const uint32_t key = (__float_as_uint(lo) & 0xFFFF0000u) | (static_cast<uint32_t>(child) & 0xFFFFu);
     return lo <= hi ? key : kKeyMiss;  // empty slots carry a box no ray enters (layout.h kLdsEmptyChild)
 }
+// dly / dhy: the y motion planes (near, far), tiy = tm * iy: the y plane distances are those of the boxes at the ray's
+// time, (plane0 + tm * dplane) * iy - oy * iy, as two single-rounding FMAs (the box padding covers the extra rounding)
+template <bool MOT>
 __device__ __forceinline__ void slab4_packed(const float4& lx, const float4& hx, const float4& ly, const float4& hy, const float4& lz,
-                                             const float4& hz, const int4& ch, float ix, float iy, float iz, float oix, float oiy,
-                                             float oiz, float tminf, float tmaxf, uint32_t& q0, uint32_t& q1, uint32_t& q2, uint32_t& q3) {
-    const f2v vx = {ix, ix}, vy = {iy, iy}, vz = {iz, iz};
+                                             const float4& hz, const float4& dly, const float4& dhy, const int4& ch, float ix, float iy,
+                                             float iz, float tiy, float oix, float oiy, float oiz, float tminf, float tmaxf, uint32_t& q0,
+                                             uint32_t& q1, uint32_t& q2, uint32_t& q3) {
+    const f2v vx = {ix, ix}, vy = {iy, iy}, vz = {iz, iz}, vty = {tiy, tiy};
     const f2v nx = {-oix, -oix}, ny = {-oiy, -oiy}, nz = {-oiz, -oiz};
     const f2v x0a = __builtin_elementwise_fma(f2v{lx.x, lx.y}, vx, nx), x0b = __builtin_elementwise_fma(f2v{lx.z, lx.w}, vx, nx);
     const f2v x1a = __builtin_elementwise_fma(f2v{hx.x, hx.y}, vx, nx), x1b = __builtin_elementwise_fma(f2v{hx.z, hx.w}, vx, nx);
-    const f2v y0a = __builtin_elementwise_fma(f2v{ly.x, ly.y}, vy, ny), y0b = __builtin_elementwise_fma(f2v{ly.z, ly.w}, vy, ny);
-    const f2v y1a = __builtin_elementwise_fma(f2v{hy.x, hy.y}, vy, ny), y1b = __builtin_elementwise_fma(f2v{hy.z, hy.w}, vy, ny);
+    f2v y0a = __builtin_elementwise_fma(f2v{ly.x, ly.y}, vy, ny), y0b = __builtin_elementwise_fma(f2v{ly.z, ly.w}, vy, ny);
+    f2v y1a = __builtin_elementwise_fma(f2v{hy.x, hy.y}, vy, ny), y1b = __builtin_elementwise_fma(f2v{hy.z, hy.w}, vy, ny);
+    if constexpr (MOT) {
+        y0a = __builtin_elementwise_fma(f2v{dly.x, dly.y}, vty, y0a);
+        y0b = __builtin_elementwise_fma(f2v{dly.z, dly.w}, vty, y0b);
+        y1a = __builtin_elementwise_fma(f2v{dhy.x, dhy.y}, vty, y1a);
+        y1b = __builtin_elementwise_fma(f2v{dhy.z, dhy.w}, vty, y1b);
+    }
     const f2v z0a = __builtin_elementwise_fma(f2v{lz.x, lz.y}, vz, nz), z0b = __builtin_elementwise_fma(f2v{lz.z, lz.w}, vz, nz);
     const f2v z1a = __builtin_elementwise_fma(f2v{hz.x, hz.y}, vz, nz), z1b = __builtin_elementwise_fma(f2v{hz.z, hz.w}, vz, nz);
     q0 = slab_key_packed(x0a.x, x1a.x, y0a.x, y1a.x, z0a.x, z1a.x, ch.x, tminf, tmaxf);
@@ -510,10 +520,8 @@ __device__ __forceinline__ bool hit_lds_slot(const uint8_t* lds, uint32_t slot, 
     const uint32_t code = lds_u1(kLdsOffRef + slot * 4u);
     V3<double> center{a.x, a.y, b.x};
     const uint32_t mv = (code >> kLdsRefMovShift) & ((1u << (kLdsRefMatShift - kLdsRefMovShift)) - 1);
-    if (mv) {
-        const double2 m0 = lds_d2(kLdsOffMov + (mv - 1u) * 16u);
-        const double dz = lds_d1(kLdsOffMov + (kLdsMovCap + mv - 1u) * 16u);
-        center = center + r.tm * V3<double>{m0.x, m0.y, dz};
+    if (mv) {  // y motion only (lds_scene_image): c + tm * (+0, dy, +0) leaves x and z exactly as they are
+        center.y = center.y + r.tm * lds_d1(kLdsOffMov + (mv - 1u) * 8u);
     }
     prim = make_primref(PRIM_SPHERE, code & kLdsRefIndexMask);
     mt = code >> kLdsRefMatShift;
@@ -632,7 +640,8 @@ struct TravResume {
 // RES: resumable (rs non-null), HBM-scene variant only.
 template <class R, uint32_t F, int B, bool L, bool PL = false, bool RES = false>
 __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* lds, int32_t root, const Ray<R>& r, R tmin, R tmax,
-                                         StackT<L>* stk, R& t, uint32_t& prim, uint32_t& face, uint32_t& mt, TravResume* rs = nullptr) {
+                                         StackT<L>* stk, R& t, uint32_t& prim, uint32_t& face, uint32_t& mt, TravResume* rs = nullptr,
+                                         int32_t hoisted = kNodeEmpty) {
     static_assert(!(L && (F & F_MEDIA)), "packed LDS keys need tmin > 0: no medium boundary tests in the LDS variant");
     static_assert(!RES || (!L && ART_SPECULATIVE), "resumable traversal: HBM-scene speculative variant only");
     const float ox = static_cast<float>(r.o.x), oy = static_cast<float>(r.o.y), oz = static_cast<float>(r.o.z);
@@ -648,11 +657,13 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                 iz = __builtin_amdgcn_rcpf(static_cast<float>(r.d.z));
 #endif
     const float oix = ox * ix, oiy = oy * iy, oiz = oz * iz;
+    // L: the y slabs move with the ray time (layout.h motion planes): plane(tm) * iy = plane0 * iy + dplane * (tm * iy)
+    const float tiy = (L && ART_LDS_MOTION) ? static_cast<float>(r.tm) * iy : 0.0f;
     // LDS variant: the near and far plane of each axis follow from the direction's sign, so the slab test reads them
     // directly (near plane offset per axis; the far plane is always the plane above it, one kLdsPlane away -- an
     // immediate DS offset -- since each axis stores lo, hi, lo) and needs no per-axis min/max
     constexpr uint32_t kLdsPlane = kLdsNodeCap * 16;
-    static_assert((kLdsPlane & (kLdsPlane - 1)) == 0 && kLdsOffNodes % kLdsPlane == 0, "node offsets OR into plane offsets");
+    static_assert(kLdsPlane % 256 == 0, "every node plane starts on bank 0");
     const uint32_t off_nx = kLdsOffNodes + (0u + (__float_as_uint(ix) >> 31)) * kLdsPlane;
     const uint32_t off_ny = kLdsOffNodes + (3u + (__float_as_uint(iy) >> 31)) * kLdsPlane;
     const uint32_t off_nz = kLdsOffNodes + (6u + (__float_as_uint(iz) >> 31)) * kLdsPlane;
@@ -672,6 +683,22 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
     // tested together.  Nodes visited past a parked leaf used the older (larger) tmax: extra visits, same closest hit.
     int32_t parked = kNodeEmpty;
 #endif
+    // hoisted (wave-uniform: the BVH object's leaf of hoisted primitives, ObjRec::b): every lane tests it in the first
+    // leaf phase, at once and before any node visit, so the tree walk starts with its closest hit as tmax.  Speculative
+    // walk: it is the parked leaf and the first node loop is skipped (a wave-uniform flag; pushing the root under it
+    // instead measured 10 more VGPR spills in k_paths); otherwise the walk starts at it with the root pushed under it
+    // (popped before any other push: no extra stack depth).
+    [[maybe_unused]] bool skip_nodes = false;
+    if (hoisted != kNodeEmpty && (!RES || rs->fresh)) {
+        const int32_t h = L ? lds_leaf(leaf_first(hoisted), leaf_count(hoisted)) : hoisted;
+#if ART_SPECULATIVE
+        parked = h;
+        skip_nodes = true;
+#else
+        st.push(root, true);
+        node = h;
+#endif
+    }
     if constexpr (RES) {
         if (!rs->fresh) {
             node = rs->node;
@@ -695,21 +722,26 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
         }
         ART_STAT_WAVE(4);
         ART_STAT_LANE(5);
-        while (node >= 0) {
+        while (node >= 0 && !skip_nodes) {  // skip_nodes: ART_SPECULATIVE only
             ART_STAT_WAVE(0);
             ART_STAT_LANE(1);
             float4 lx, hx, ly, hy, lz, hz;  // L: near (lx, ly, lz) and far (hx, hy, hz) planes
             int4 ch;
+            [[maybe_unused]] float4 dly, dhy;  // L: near / far y motion planes
             if constexpr (L) {
                 const uint32_t n16 = static_cast<uint32_t>(node) * 16u;
-                const uint32_t ax = n16 | off_nx, ay = n16 | off_ny, az = n16 | off_nz;
+                const uint32_t ax = n16 + off_nx, ay = n16 + off_ny, az = n16 + off_nz;
                 lx = lds_f4(ax);
                 hx = lds_f4(ax + kLdsPlane);
                 ly = lds_f4(ay);
                 hy = lds_f4(ay + kLdsPlane);
                 lz = lds_f4(az);
                 hz = lds_f4(az + kLdsPlane);
-                ch = lds_i4(kLdsOffNodes + 9 * kLdsPlane + n16);
+#if ART_LDS_MOTION
+                dly = lds_f4(ay + (kLdsNodePlaneMotion - 3) * kLdsPlane);
+                dhy = lds_f4(ay + (kLdsNodePlaneMotion - 2) * kLdsPlane);
+#endif
+                ch = lds_i4(kLdsOffNodes + kLdsNodePlaneChild * kLdsPlane + n16);
             } else if (PL && static_cast<uint32_t>(node) < S.n_lds_nodes) {
                 // the top levels, copied into LDS: explicit LDS loads (a generic pointer here would be merged with
                 // the global branch's into flat loads)
@@ -730,7 +762,7 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                 // 16-bit child codes ride in the low half of the entry-distance keys: the network is 5 integer
                 // min/max pairs and each code comes back with one bit-field extract
                 uint32_t q0, q1, q2, q3;
-                slab4_packed(lx, hx, ly, hy, lz, hz, ch, ix, iy, iz, oix, oiy, oiz, tminf, tmaxf, q0, q1, q2, q3);
+                slab4_packed<ART_LDS_MOTION != 0>(lx, hx, ly, hy, lz, hz, dly, dhy, ch, ix, iy, iz, tiy, oix, oiy, oiz, tminf, tmaxf, q0, q1, q2, q3);
                 ucas(q0, q1);
                 ucas(q2, q3);
                 ucas(q0, q2);
@@ -774,6 +806,7 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
         // wave-wide break still has an inner node to return to)
         // L: a lane that left the node loop holding a second leaf (parked + current) tests both in this phase, one
         // leaf phase instead of two (the wave's leaf loop runs over the longer sum, once)
+        skip_nodes = false;
         int32_t leaf = parked;
         int32_t leaf2 = kNodeEmpty;
         if (leaf != kNodeEmpty) {
@@ -907,7 +940,7 @@ __device__ __forceinline__ bool hit_object(const DevScene<R>& S, const uint8_t* 
         if constexpr (!L && ART_OBJ_PRIMS) return hit_prim_rec<R, F>(primref_type(prim), S.obj_prims[oi], r, tmin, tmax, t, face);
         else return hit_prim<R, F>(S, prim, r, tmin, tmax, t, face);
     }
-    return traverse<R, F, B, L, PL, RES>(S, lds, o.a, r, tmin, tmax, stk, t, prim, face, mt, rs);
+    return traverse<R, F, B, L, PL, RES>(S, lds, o.a, r, tmin, tmax, stk, t, prim, face, mt, rs, o.b);
 }
 
 // Out of line: measured +0.2 % (cow) to +1.8 % (Next-Week final) over the inlined body, which raised the register

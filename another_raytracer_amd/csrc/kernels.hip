@@ -22,7 +22,11 @@
 #include <map>
 #include <mutex>
 #include <tuple>
+#include <algorithm>
+#include <array>
 #include <cmath>
+#include <functional>
+#include <limits>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -406,10 +410,9 @@ __device__ __forceinline__ bool shade_hit_lds(const uint8_t* lds, uint32_t slot,
     const uint32_t mi = reinterpret_cast<const uint16_t*>(lds + kLdsOffMatIdx)[slot];
     V3<R> center{a.x, a.y, b.x};
     const uint32_t mv = (code >> kLdsRefMovShift) & ((1u << (kLdsRefMatShift - kLdsRefMovShift)) - 1);
-    if (mv) {  // moving_sphere.h:72-74, as prim_surface
-        const double2* mp = reinterpret_cast<const double2*>(lds + kLdsOffMov) + (mv - 1);
-        const double2 m0 = mp[0], m1 = mp[kLdsMovCap];
-        center = center + st.ray.tm * V3<R>{m0.x, m0.y, m1.x};  // unit shutter (lds_scene_image): (tm - 0) / 1 == tm
+    if (mv) {  // moving_sphere.h:72-74, as prim_surface; unit shutter, y motion (lds_scene_image): (tm - 0) / 1 == tm,
+               // and x + tm * (+0) == x, z + tm * (+0) == z
+        center.y = center.y + st.ray.tm * reinterpret_cast<const double*>(lds + kLdsOffMov)[mv - 1];
     }
     Surf<R> s;
     s.p = st.ray.at(t);
@@ -1506,8 +1509,9 @@ static std::vector<uint8_t> lds_scene_image(const FlatScene& f, uint32_t& nmov, 
         const SphereRec<double>& sp = f.spheres[primref_index(ref)];
         if (sp.flags & SPH_MOVING) {
             // the image's moving spheres span the unit shutter (every moving_sphere of the reference scenes,
-            // scene_manager.cpp:34-35, :201): their centre fraction is the ray time itself (hit_lds_slot)
-            if (sp.t0 != 0.0 || sp.dt != 1.0) return img;
+            // scene_manager.cpp:34-35, :201): their centre fraction is the ray time itself (hit_lds_slot); and they
+            // move along y only (scene_manager.cpp:33), so the node boxes carry y motion planes (layout.h)
+            if (sp.t0 != 0.0 || sp.dt != 1.0 || sp.d[0] != 0.0 || sp.d[2] != 0.0) return img;
             ++nmov;
         }
     }
@@ -1515,11 +1519,61 @@ static std::vector<uint8_t> lds_scene_image(const FlatScene& f, uint32_t& nmov, 
     for (const BvhNode& b : f.nodes)
         for (int c = 0; c < 4; ++c)
             if (b.child[c] < 0 && b.child[c] != kNodeEmpty && leaf_count(b.child[c]) > kLdsLeafMaxCount) return img;
+    // y extent of every child at t = 0 and t = 1 (f64, exact sphere bounds; the centre at ray time tm is
+    // c.y + tm * dy, so the lerp of the two extents bounds it, and the lerp of a union bounds the union of lerps)
+    struct YSpan {
+        double lo0, hi0, lo1, hi1;
+        void grow(const YSpan& o) {
+            lo0 = std::min(lo0, o.lo0); hi0 = std::max(hi0, o.hi0);
+            lo1 = std::min(lo1, o.lo1); hi1 = std::max(hi1, o.hi1);
+        }
+    };
+    const double dinf = std::numeric_limits<double>::infinity();
+    const YSpan kNone{dinf, -dinf, dinf, -dinf};
+    std::vector<std::array<YSpan, 4>> cspan(f.nodes.size());
+    std::vector<uint8_t> state(f.nodes.size(), 0);
+    std::function<YSpan(int32_t)> node_span = [&](int32_t n) -> YSpan {
+        if (state[n] == 1) throw std::runtime_error("bvh node cycle");
+        YSpan all = kNone;
+        if (state[n] == 2) {
+            for (const YSpan& s : cspan[n]) all.grow(s);
+            return all;
+        }
+        state[n] = 1;
+        const BvhNode& b = f.nodes[n];
+        for (int c = 0; c < 4; ++c) {
+            YSpan s = kNone;
+            if (b.child[c] >= 0) {
+                s = node_span(b.child[c]);
+            } else if (b.child[c] != kNodeEmpty) {
+                for (uint32_t k = 0; k < leaf_count(b.child[c]); ++k) {
+                    const SphereRec<double>& sp = f.spheres[primref_index(f.primrefs[leaf_first(b.child[c]) + k])];
+                    const double y1 = (sp.flags & SPH_MOVING) ? sp.c[1] + sp.d[1] : sp.c[1];
+                    s.grow(YSpan{sp.c[1] - sp.r, sp.c[1] + sp.r, y1 - sp.r, y1 + sp.r});
+                }
+            }
+            cspan[n][c] = s;
+            all.grow(s);
+        }
+        state[n] = 2;
+        return all;
+    };
+    if (ART_LDS_MOTION)
+        for (size_t n = 0; n < f.nodes.size(); ++n) node_span(static_cast<int32_t>(n));
     img.assign(kLdsImageBytes, 0);
     auto put = [&](uint32_t off, const void* v, size_t n) { std::memcpy(img.data() + off, v, n); };
+    const float finf = std::numeric_limits<float>::infinity();
+    auto f32_down = [&](double x) {
+        float v = static_cast<float>(x);
+        return static_cast<double>(v) > x ? std::nextafter(v, -finf) : v;
+    };
+    auto f32_up = [&](double x) {
+        float v = static_cast<float>(x);
+        return static_cast<double>(v) < x ? std::nextafter(v, finf) : v;
+    };
     for (size_t n = 0; n < f.nodes.size(); ++n) {
         const BvhNode& b = f.nodes[n];
-        float planes[6][4];
+        float planes[6][4], motion[2][4];
         const float* src[6] = {b.lox, b.hix, b.loy, b.hiy, b.loz, b.hiz};
         int32_t child[4];
         for (int c = 0; c < 4; ++c) {
@@ -1527,12 +1581,29 @@ static std::vector<uint8_t> lds_scene_image(const FlatScene& f, uint32_t& nmov, 
             // a child check, and the astronomically rare ray whose three slab times coincide there finds no primitives
             const bool empty = b.child[c] == kNodeEmpty;
             for (int j = 0; j < 6; ++j) planes[j][c] = empty ? kLdsEmptyBox : src[j][c];
+            motion[0][c] = motion[1][c] = 0.0f;
+            if (ART_LDS_MOTION && !empty) {
+                // y slab at time tm: [lo0 + tm * dlo, hi0 + tm * dhi] in f32, rounded outward and padded as
+                // conservative_box pads (bvh.cpp), so it holds the f64 spheres at every tm in [0, 1]
+                const YSpan& s = cspan[n][c];
+                const double m = std::max({std::fabs(s.lo0), std::fabs(s.hi0), std::fabs(s.lo1), std::fabs(s.hi1), s.hi0 - s.lo0, s.hi1 - s.lo1});
+                const float pad = 1e-6f * static_cast<float>(m) + 1e-30f;
+                const float lo0 = f32_down(s.lo0) - pad, lo1 = f32_down(s.lo1) - pad;
+                const float hi0 = f32_up(s.hi0) + pad, hi1 = f32_up(s.hi1) + pad;
+                planes[2][c] = lo0;
+                planes[3][c] = hi0;
+                motion[0][c] = f32_down(static_cast<double>(lo1) - static_cast<double>(lo0));  // lo0 + dlo <= lo1
+                motion[1][c] = f32_up(static_cast<double>(hi1) - static_cast<double>(hi0));
+            }
             child[c] = empty ? kLdsEmptyChild : b.child[c] >= 0 ? b.child[c] : lds_leaf(leaf_first(b.child[c]), leaf_count(b.child[c]));
         }
-        // per axis: lo, hi, lo (layout.h kLdsNodePlanes), then the child codes
+        // per axis: lo, hi, lo (layout.h kLdsNodePlanes), the child codes, then y motion: dlo, dhi, dlo
         const int order[9] = {0, 1, 0, 2, 3, 2, 4, 5, 4};
-        for (uint32_t j = 0; j < 9; ++j) put(kLdsOffNodes + (j * kLdsNodeCap + static_cast<uint32_t>(n)) * 16, planes[order[j]], 16);
-        put(kLdsOffNodes + (9 * kLdsNodeCap + static_cast<uint32_t>(n)) * 16, child, 16);
+        const uint32_t nn = static_cast<uint32_t>(n);
+        for (uint32_t j = 0; j < 9; ++j) put(kLdsOffNodes + (j * kLdsNodeCap + nn) * 16, planes[order[j]], 16);
+        put(kLdsOffNodes + (kLdsNodePlaneChild * kLdsNodeCap + nn) * 16, child, 16);
+        if (ART_LDS_MOTION)
+            for (uint32_t j = 0; j < 3; ++j) put(kLdsOffNodes + ((kLdsNodePlaneMotion + j) * kLdsNodeCap + nn) * 16, motion[j == 1 ? 1 : 0], 16);
     }
     // shading table: one entry per material (two for a checker of solid colours); anything else keeps the scene off
     // the fused variant (shade_ok = false), which shades from the global scene records instead
@@ -1549,16 +1620,18 @@ static std::vector<uint8_t> lds_scene_image(const FlatScene& f, uint32_t& nmov, 
     for (size_t slot = 0; slot < f.primrefs.size(); ++slot) {
         const uint32_t idx = primref_index(f.primrefs[slot]);
         const auto& sp = f.spheres[idx];
-        const double p0[2] = {sp.c[0], sp.c[1]}, p1[2] = {sp.c[2], sp.r * sp.r}, inv_r = 1.0 / sp.r;
+        // a moving sphere's x and z at time tm are c + tm * (+-0) (moving_sphere.h:72-74) == c + d: the image stores
+        // that value (it differs from c only for c = -0 and d = +0), and the device adds tm * dy to y alone
+        const bool moving = (sp.flags & SPH_MOVING) != 0;
+        const double cx = moving ? sp.c[0] + sp.d[0] : sp.c[0], cz = moving ? sp.c[2] + sp.d[2] : sp.c[2];
+        const double p0[2] = {cx, sp.c[1]}, p1[2] = {cz, sp.r * sp.r}, inv_r = 1.0 / sp.r;
         const uint32_t sl = static_cast<uint32_t>(slot);
         put(kLdsOffSph + sl * 16, p0, 16);
         put(kLdsOffSph + (kLdsSlotCap + sl) * 16, p1, 16);
         put(kLdsOffInvR + sl * 8, &inv_r, 8);
         uint32_t code = idx | (f.mats[sp.mat].type << kLdsRefMatShift);
-        if (sp.flags & SPH_MOVING) {
-            const double m0[2] = {sp.d[0], sp.d[1]}, m1[2] = {sp.d[2], 0.0};
-            put(kLdsOffMov + m * 16, m0, 16);
-            put(kLdsOffMov + (kLdsMovCap + m) * 16, m1, 16);
+        if (moving) {
+            put(kLdsOffMov + m * 8, &sp.d[1], 8);
             code |= (m + 1) << kLdsRefMovShift;
             ++m;
         }

@@ -89,17 +89,28 @@ constexpr int kMaxStackDepth = 64;   // per-lane LDS traversal stack entries (si
 // node and sphere fetches of the traversal never touch the vector-memory (TA/L1) path that bounds the global variant.
 // Every plane is an array of 16-B entries, so lanes fetching different nodes/spheres spread over the 16 four-bank slots
 // of the ds_read_b128 bank row, and the plane strides are compile-time (DS immediate offsets, no address VALU).
-// BVH4 nodes: 10 planes -- per axis (lo, hi, lo again) as float4, so the far plane of either direction sign is one
-// plane above the near one (an immediate DS offset); child codes as int4
-constexpr uint32_t kLdsNodeCap = 256;
-constexpr uint32_t kLdsNodePlanes = 10;
+// BVH4 nodes: 10 (13) planes -- per axis (lo, hi, lo again) as float4, so the far plane of either direction sign is one
+// plane above the near one (an immediate DS offset); child codes as int4; then, with ART_LDS_MOTION, the motion planes of y (dlo, dhi, dlo):
+// the image's spheres move along y only (the reference's moving spheres, scene_manager.cpp:33), so a child's y slab at
+// ray time tm is [lo + tm * dlo, hi + tm * dhi] -- the lerp of its t = 0 and t = 1 boxes, which bounds every linearly
+// moving sphere below it at tm -- instead of the union over the shutter (a moving sphere's box is 1.6x taller)
+// ART_LDS_MOTION (default 0): measured on the random-spheres scene -- 7.6 % fewer node visits and 6.3 % fewer leaf
+// tests, but the two extra plane loads and FMAs per visit (and 21 more VGPR spills at k_paths' 128-VGPR cap) cost
+// more: -1.5 %.  Off, the nodes keep the 10 planes of the union boxes over the shutter.
+#ifndef ART_LDS_MOTION
+#define ART_LDS_MOTION 0
+#endif
+constexpr uint32_t kLdsNodeCap = 320;  // the random scene: 259 nodes (its SAH tree without the hoisted ground sphere)
+constexpr uint32_t kLdsNodePlanes = ART_LDS_MOTION ? 13 : 10;
+constexpr uint32_t kLdsNodePlaneChild = 9;
+constexpr uint32_t kLdsNodePlaneMotion = 10;  // dlo y, dhi y, dlo y
 constexpr uint32_t kLdsSlotCap = 1024;  // leaf slots (= primref array entries): 2 planes (cx, cy), (cz, r) as double2
-constexpr uint32_t kLdsMovCap = 512;    // moving spheres (unit shutter): 2 planes (dx, dy), (dz, 0) as double2
+constexpr uint32_t kLdsMovCap = 512;    // moving spheres (unit shutter, y motion): one plane of dy (f64)
 constexpr uint32_t kLdsOffNodes = 0;
 constexpr uint32_t kLdsOffSph = kLdsOffNodes + kLdsNodePlanes * kLdsNodeCap * 16;
 constexpr uint32_t kLdsOffMov = kLdsOffSph + 2 * kLdsSlotCap * 16;
 // u32 per slot: sphere index (19 bits) | (moving index + 1) << 19 (10 bits) | material type << 29 (3 bits)
-constexpr uint32_t kLdsOffRef = kLdsOffMov + 2 * kLdsMovCap * 16;
+constexpr uint32_t kLdsOffRef = kLdsOffMov + kLdsMovCap * 8;
 // Shading table (fused variant): u16 per slot = material entry e | kLdsMatChecker, and kLdsMatCap 32-B entries
 // (c.x, c.y), (c.z, param): lambertian / diffuse_light colour (a checker of two solid colours takes entries e = even,
 // e + 1 = odd), metal albedo + fuzz, dielectric (-, -, -, ir).  A hit is then shaded without any global load.
@@ -134,7 +145,7 @@ template <class R>
 struct ObjRec {
     int32_t kind;
     int32_t a;      // PRIM: prim ref; BVH: root node; TRANSLATE/ROTATE_Y: child object; MEDIUM: boundary object
-    int32_t b;      // MEDIUM: phase material
+    int32_t b;      // MEDIUM: phase material; BVH: leaf code of its hoisted primitives (tested before the tree), or -1
     int32_t pad;
     R p[4];         // TRANSLATE: offset xyz; ROTATE_Y: sin, cos; MEDIUM: neg_inv_density
 };

@@ -6,6 +6,7 @@
 #include <cctype>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <functional>
@@ -673,6 +674,31 @@ std::string dump_scene(const SceneGraph& g) {
 
 // ------------------------------------------------------------------------------------------------ compile
 namespace {
+// BVH primitive hoisting (Compiler::obj, N_BVH): at most kMaxHoist primitives of a BVH of >= kHoistMinPrims whose box
+// area is >= kHoistAreaShare of the whole BVH's.  ART_HOIST=0 turns it off (builder experiments, tools/).
+constexpr size_t kHoistMinPrims = 8;
+constexpr size_t kMaxHoist = 4;
+constexpr double kHoistAreaShare = 0.5;
+bool hoist_enabled() {
+    static const bool v = [] {
+        const char* e = std::getenv("ART_HOIST");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+AABBd box_union(const AABBd& a, const AABBd& b) {
+    AABBd r;
+    for (int k = 0; k < 3; ++k) {
+        r.mn[k] = std::min(a.mn[k], b.mn[k]);
+        r.mx[k] = std::max(a.mx[k], b.mx[k]);
+    }
+    return r;
+}
+double box_area(const AABBd& b) {
+    const double dx = b.mx[0] - b.mn[0], dy = b.mx[1] - b.mn[1], dz = b.mx[2] - b.mn[2];
+    return 2 * (dx * dy + dy * dz + dz * dx);
+}
+
 struct Compiler {
     const SceneGraph& g;
     FlatScene& f;
@@ -761,7 +787,34 @@ struct Compiler {
                 gather(idx, refs, boxes);
                 int depth = 0, stack = 0;
                 o.kind = OBJ_BVH;
+                // Hoisted primitives (layout.h ObjRec): a primitive whose box is as large as the whole BVH's (the
+                // random scene's r = 1000 ground sphere, scene_manager.cpp:18) is met by nearly every ray, so it
+                // leaves the tree and every traversal tests it first, with all its lanes at once
+                std::vector<uint32_t> hoist;
+                if (hoist_enabled() && refs.size() >= kHoistMinPrims) {
+                    AABBd all = boxes[0];
+                    for (const AABBd& b : boxes) all = box_union(all, b);
+                    const double a_all = box_area(all);
+                    std::vector<uint32_t> r2;
+                    std::vector<AABBd> b2;
+                    for (size_t i = 0; i < refs.size(); ++i) {
+                        if (hoist.size() < kMaxHoist && box_area(boxes[i]) >= kHoistAreaShare * a_all) hoist.push_back(refs[i]);
+                        else {
+                            r2.push_back(refs[i]);
+                            b2.push_back(boxes[i]);
+                        }
+                    }
+                    if (!hoist.empty()) {
+                        refs.swap(r2);
+                        boxes.swap(b2);
+                    }
+                }
                 o.a = build_sah_bvh(boxes, refs, f.nodes, f.primrefs, depth, stack);
+                o.b = kNodeEmpty;
+                if (!hoist.empty()) {
+                    o.b = make_leaf(static_cast<uint32_t>(f.primrefs.size()), static_cast<uint32_t>(hoist.size()));
+                    f.primrefs.insert(f.primrefs.end(), hoist.begin(), hoist.end());
+                }
                 f.max_bvh_depth = std::max(f.max_bvh_depth, depth);
                 f.max_stack = std::max(f.max_stack, stack);
                 return add_obj(o);

@@ -171,6 +171,10 @@ void load_scene_file(const std::string& path, FlatScene& flat, SceneView& view) 
         }
     for (int32_t w : f.world)
         if (w < 0 || static_cast<size_t>(w) >= f.objs.size()) throw std::runtime_error(path + ": world object out of range");
+    for (const ObjRec<double>& o : f.objs)
+        if (o.kind == OBJ_BVH && (o.a < 0 || static_cast<size_t>(o.a) >= f.nodes.size() ||
+                                  (o.b != kNodeEmpty && (o.b >= 0 || leaf_first(o.b) + leaf_count(o.b) > nrefs))))
+            throw std::runtime_error(path + ": BVH object out of range");
     for (const ImageRec& im : f.images)
         if (im.offset + static_cast<uint64_t>(im.w) * im.h * im.bpp > f.texels.size()) throw std::runtime_error(path + ": texture out of range");
     flat = std::move(f);

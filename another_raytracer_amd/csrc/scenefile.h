@@ -13,7 +13,7 @@
 
 namespace art {
 
-constexpr uint32_t kSceneFileVersion = 2;  // 2: feature bit F_MEDIA_G
+constexpr uint32_t kSceneFileVersion = 3;  // 2: feature bit F_MEDIA_G; 3: hoisted BVH primitives (ObjRec::b)
 
 struct SceneView {  // what scene_manager::build returns besides the objects (scene_manager.h:6-14)
     double lookfrom[3] = {0, 0, 0}, lookat[3] = {0, 0, 0}, vfov = 40.0, aperture = 0.0;
