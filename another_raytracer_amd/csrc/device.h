@@ -768,6 +768,7 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                 ucas(q0, q2);
                 ucas(q1, q3);
                 ucas(q1, q2);
+                if (q0 >= kKeyMiss) ART_STAT_LANE(12);  // a dead visit: no child box is entered before tmax
                 st.push(static_cast<int32_t>(q3), q3 < kKeyMiss);
                 st.push(static_cast<int32_t>(q2), q2 < kKeyMiss);
                 st.push(static_cast<int32_t>(q1), q1 < kKeyMiss);
@@ -890,6 +891,7 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                 }
             }
             if (h) {
+                ART_STAT_LANE(13);
                 tmax = tt;
                 t = tt;
                 prim = ref;
