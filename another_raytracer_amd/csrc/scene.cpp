@@ -770,6 +770,46 @@ struct Compiler {
         f.objs.push_back(o);
         return static_cast<int>(f.objs.size()) - 1;
     }
+    // One BVH object over every primitive below the graph items (BVH / list nodes and primitives).
+    int bvh_obj(const std::vector<int>& items) {
+        std::vector<uint32_t> refs;
+        std::vector<AABBd> boxes;
+        for (int it : items) gather(it, refs, boxes);
+        int depth = 0, stack = 0;
+        ObjRec<double> o{};
+        o.kind = OBJ_BVH;
+        // Hoisted primitives (layout.h ObjRec): a primitive whose box is as large as the whole BVH's (the random
+        // scene's r = 1000 ground sphere, scene_manager.cpp:18) is met by nearly every ray, so it leaves the tree and
+        // every traversal tests it first, with all its lanes at once
+        std::vector<uint32_t> hoist;
+        if (hoist_enabled() && refs.size() >= kHoistMinPrims) {
+            AABBd all = boxes[0];
+            for (const AABBd& b : boxes) all = box_union(all, b);
+            const double a_all = box_area(all);
+            std::vector<uint32_t> r2;
+            std::vector<AABBd> b2;
+            for (size_t i = 0; i < refs.size(); ++i) {
+                if (hoist.size() < kMaxHoist && box_area(boxes[i]) >= kHoistAreaShare * a_all) hoist.push_back(refs[i]);
+                else {
+                    r2.push_back(refs[i]);
+                    b2.push_back(boxes[i]);
+                }
+            }
+            if (!hoist.empty()) {
+                refs.swap(r2);
+                boxes.swap(b2);
+            }
+        }
+        o.a = build_sah_bvh(boxes, refs, f.nodes, f.primrefs, depth, stack);
+        o.b = kNodeEmpty;
+        if (!hoist.empty()) {
+            o.b = make_leaf(static_cast<uint32_t>(f.primrefs.size()), static_cast<uint32_t>(hoist.size()));
+            f.primrefs.insert(f.primrefs.end(), hoist.begin(), hoist.end());
+        }
+        f.max_bvh_depth = std::max(f.max_bvh_depth, depth);
+        f.max_stack = std::max(f.max_stack, stack);
+        return add_obj(o);
+    }
     int obj(int idx) {
         const Node& n = g.nodes[idx];
         ObjRec<double> o{};
@@ -781,44 +821,8 @@ struct Compiler {
         }
         switch (n.type) {
             case N_LIST:
-            case N_BVH: {
-                std::vector<uint32_t> refs;
-                std::vector<AABBd> boxes;
-                gather(idx, refs, boxes);
-                int depth = 0, stack = 0;
-                o.kind = OBJ_BVH;
-                // Hoisted primitives (layout.h ObjRec): a primitive whose box is as large as the whole BVH's (the
-                // random scene's r = 1000 ground sphere, scene_manager.cpp:18) is met by nearly every ray, so it
-                // leaves the tree and every traversal tests it first, with all its lanes at once
-                std::vector<uint32_t> hoist;
-                if (hoist_enabled() && refs.size() >= kHoistMinPrims) {
-                    AABBd all = boxes[0];
-                    for (const AABBd& b : boxes) all = box_union(all, b);
-                    const double a_all = box_area(all);
-                    std::vector<uint32_t> r2;
-                    std::vector<AABBd> b2;
-                    for (size_t i = 0; i < refs.size(); ++i) {
-                        if (hoist.size() < kMaxHoist && box_area(boxes[i]) >= kHoistAreaShare * a_all) hoist.push_back(refs[i]);
-                        else {
-                            r2.push_back(refs[i]);
-                            b2.push_back(boxes[i]);
-                        }
-                    }
-                    if (!hoist.empty()) {
-                        refs.swap(r2);
-                        boxes.swap(b2);
-                    }
-                }
-                o.a = build_sah_bvh(boxes, refs, f.nodes, f.primrefs, depth, stack);
-                o.b = kNodeEmpty;
-                if (!hoist.empty()) {
-                    o.b = make_leaf(static_cast<uint32_t>(f.primrefs.size()), static_cast<uint32_t>(hoist.size()));
-                    f.primrefs.insert(f.primrefs.end(), hoist.begin(), hoist.end());
-                }
-                f.max_bvh_depth = std::max(f.max_bvh_depth, depth);
-                f.max_stack = std::max(f.max_stack, stack);
-                return add_obj(o);
-            }
+            case N_BVH:
+                return bvh_obj({idx});
             case N_TRANSLATE:
             case N_ROTATE_Y: {
                 int depth = 0;
@@ -851,12 +855,40 @@ struct Compiler {
         }
         throw std::runtime_error("unsupported object");
     }
-    void top(int idx) {
+    void flatten(int idx, std::vector<int>& out) const {
         if (g.nodes[idx].type == N_LIST) {  // a nested hittable_list has the same closest-hit semantics flattened
-            for (int it : g.nodes[idx].items) top(it);
+            for (int it : g.nodes[idx].items) flatten(it, out);
             return;
         }
-        f.world.push_back(obj(idx));
+        out.push_back(idx);
+    }
+    // The world hittable_list (hittable_list.cpp:5-19).  World merging: a run of consecutive world objects that are
+    // untransformed BVHs or primitives, holding at least one BVH, becomes one BVH over all their primitives (the
+    // Next-Week final scene's box field + light + four spheres; a mesh + its light).  Its closest hit is theirs (up
+    // to exact-t ties, as any BVH); a constant_medium ends a run, so every medium still sees the closest hit of the
+    // objects before it when it clips its interval and decides whether to draw (constant_medium.h:37-62): the RNG
+    // sequence is unchanged.  The loose primitives are then tested only when a ray enters their boxes instead of
+    // once per segment by every lane.  ART_WORLD_MERGE=0 turns it off (experiments, tools/).
+    void world(const std::vector<int>& roots) {
+        std::vector<int> items;
+        for (int w : roots) flatten(w, items);
+        static const bool merge = [] {
+            const char* e = std::getenv("ART_WORLD_MERGE");
+            return !(e && e[0] == '0');
+        }();
+        auto mergeable = [&](int idx) { const NodeType t = g.nodes[idx].type; return t == N_BVH || is_prim(t); };
+        for (size_t i = 0; i < items.size();) {
+            size_t j = i;
+            bool has_bvh = false;
+            while (j < items.size() && mergeable(items[j])) has_bvh |= g.nodes[items[j++]].type == N_BVH;
+            if (merge && has_bvh && j - i >= 2) {
+                f.world.push_back(bvh_obj(std::vector<int>(items.begin() + static_cast<std::ptrdiff_t>(i), items.begin() + static_cast<std::ptrdiff_t>(j))));
+                i = j;
+            } else {
+                f.world.push_back(obj(items[i]));
+                ++i;
+            }
+        }
     }
 };
 }  // namespace
@@ -944,7 +976,7 @@ FlatScene compile_scene(const SceneGraph& g) {
         f.images.push_back(r);
     }
     Compiler c{g, f};
-    for (int w : g.world) c.top(w);
+    c.world(g.world);
     for (int a = 0; a < 3; ++a) f.background[a] = g.background[a];
     if (f.max_stack > kMaxStackDepth) throw std::runtime_error("bvh needs a deeper traversal stack than kMaxStackDepth");
     f.features = (f.spheres.empty() ? 0u : F_SPHERE) | (f.tris.empty() ? 0u : F_TRI) | (f.rects.empty() ? 0u : F_RECT) |

@@ -1,4 +1,10 @@
-"""BVH primitive hoisting (csrc/scene.cpp Compiler::obj, device.h traverse): a primitive whose box is as large as its
+"""Scene-compile restructurings that keep every closest hit and every RNG draw, checked on the CPU through the flat-scene
+file (csrc/scenefile.cpp), whose arrays are the compiled scene.
+
+World merging (csrc/scene.cpp Compiler::world): a run of untransformed BVHs and primitives of the world list, with at
+least one BVH, becomes one BVH; a constant_medium ends a run.
+
+BVH primitive hoisting (csrc/scene.cpp Compiler::bvh_obj, device.h traverse): a primitive whose box is as large as its
 whole BVH's leaves the tree and is recorded as the BVH object's hoisted leaf (layout.h ObjRec::b), which every
 traversal tests first.  Checked on the CPU through the flat-scene file (csrc/scenefile.cpp), whose arrays are the
 compiled scene: the random scene's r = 1000 ground sphere (scene_manager.cpp:18) is hoisted and in no BVH leaf, the
@@ -13,7 +19,7 @@ import another_raytracer_amd as art
 
 # scenefile.cpp FileHeader: magic, version, header_bytes, record_bytes[13], features, has_media, max_bvh_depth,
 # max_stack, (pad), background[3], lookfrom[3], lookat[3], vfov, aperture, offset[13], count[13], payload, checksum
-A_SPHERES, A_PRIMREFS, A_NODES, A_OBJS = 0, 4, 5, 6
+A_SPHERES, A_PRIMREFS, A_NODES, A_OBJS, A_WORLD = 0, 4, 5, 6, 7
 OFF_OFFSET = 176
 OBJ_BVH = 1
 NODE_EMPTY = -1
@@ -96,3 +102,22 @@ def test_out_of_range_hoisted_leaf_is_refused(tmp_path):
     with pytest.raises(art.RTError) as e:
         art.scene_manager().load(p)
     assert "BVH object out of range" in str(e.value)
+
+
+OBJ_PRIM, OBJ_TRANSLATE, OBJ_MEDIUM = 0, 2, 4
+
+
+@pytest.mark.parametrize("name,kinds", [
+    # Next-Week final (scene_manager.cpp:169-235): [box BVH, light, moving sphere, 3 spheres] merge; the two media,
+    # earth, perlin sphere and the translated BVH stay in order
+    ("8", [OBJ_BVH, OBJ_MEDIUM, OBJ_MEDIUM, OBJ_PRIM, OBJ_PRIM, OBJ_TRANSLATE]),
+    ("cow", [OBJ_BVH, OBJ_MEDIUM]),  # mesh BVH + light merge, the mist medium stays
+    ("1", [OBJ_BVH]),
+    ("c1", [OBJ_PRIM, OBJ_PRIM, OBJ_PRIM]),  # no BVH in the run: unchanged
+])
+def test_world_merging(name, kinds, tmp_path):
+    blob = _saved(name, tmp_path)
+    off, cnt = _arrays(blob)
+    objs, _ = _objs(blob)
+    world = np.frombuffer(blob, "<i4", int(cnt[A_WORLD]), int(off[A_WORLD]))
+    assert [int(objs[w]["kind"]) for w in world] == kinds
