@@ -868,20 +868,24 @@ struct Compiler {
     // to exact-t ties, as any BVH); a constant_medium ends a run, so every medium still sees the closest hit of the
     // objects before it when it clips its interval and decides whether to draw (constant_medium.h:37-62): the RNG
     // sequence is unchanged.  The loose primitives are then tested only when a ray enters their boxes instead of
-    // once per segment by every lane.  ART_WORLD_MERGE=0 turns it off (experiments, tools/).
+    // once per segment by every lane.  ART_WORLD_MERGE=0 turns it off, 1 merges BVH runs only (experiments, tools/).
     void world(const std::vector<int>& roots) {
         std::vector<int> items;
         for (int w : roots) flatten(w, items);
-        static const bool merge = [] {
+        static const int merge = [] {
             const char* e = std::getenv("ART_WORLD_MERGE");
-            return !(e && e[0] == '0');
+            return e ? std::atoi(e) : 2;
         }();
         auto mergeable = [&](int idx) { const NodeType t = g.nodes[idx].type; return t == N_BVH || is_prim(t); };
         for (size_t i = 0; i < items.size();) {
             size_t j = i;
             bool has_bvh = false;
             while (j < items.size() && mergeable(items[j])) has_bvh |= g.nodes[items[j++]].type == N_BVH;
-            if (merge && has_bvh && j - i >= 2) {
+            // mode 2 (default) also merges primitive-only runs of >= 3 objects, or that are the whole world (which can
+            // then take the LDS kernel): Cornell box +25..32 %, the two-sphere scenes +6..16 %; a 2-primitive run in a
+            // longer world (the Next-Week final's earth + perlin spheres) measured -1.5 % as a BVH and stays as it is
+            const bool prims_ok = merge >= 2 && (j - i >= 3 || (i == 0 && j == items.size()));
+            if (merge && (has_bvh || prims_ok) && j - i >= 2) {
                 f.world.push_back(bvh_obj(std::vector<int>(items.begin() + static_cast<std::ptrdiff_t>(i), items.begin() + static_cast<std::ptrdiff_t>(j))));
                 i = j;
             } else {

@@ -122,7 +122,7 @@ def test_general_scenes_use_the_hbm_kernels(gpu):
     assert gpu_render("cow", 32, 18, 2, wavefront=True)["stats"]["extend_variant"] == 0
 
 
-@pytest.mark.parametrize("scene", ["cow", "8", "5", "6", "7", "9", "c1"])
+@pytest.mark.parametrize("scene", ["cow", "8", "5", "6", "7", "9", "4"])
 @pytest.mark.parametrize("max_depth", [1, 50])
 def test_hbm_persistent_paths_match_wavefront(gpu, scene, max_depth):
     # every feature (triangles, rects, boxes, transforms, media, noise/image textures, lights) through k_paths_g is bit

@@ -2,7 +2,7 @@
 file (csrc/scenefile.cpp), whose arrays are the compiled scene.
 
 World merging (csrc/scene.cpp Compiler::world): a run of untransformed BVHs and primitives of the world list, with at
-least one BVH, becomes one BVH; a constant_medium ends a run.
+least one BVH (or >= 3 primitives, or the whole world), becomes one BVH; a constant_medium ends a run.
 
 BVH primitive hoisting (csrc/scene.cpp Compiler::bvh_obj, device.h traverse): a primitive whose box is as large as its
 whole BVH's leaves the tree and is recorded as the BVH object's hoisted leaf (layout.h ObjRec::b), which every
@@ -113,7 +113,9 @@ OBJ_PRIM, OBJ_TRANSLATE, OBJ_MEDIUM = 0, 2, 4
     ("8", [OBJ_BVH, OBJ_MEDIUM, OBJ_MEDIUM, OBJ_PRIM, OBJ_PRIM, OBJ_TRANSLATE]),
     ("cow", [OBJ_BVH, OBJ_MEDIUM]),  # mesh BVH + light merge, the mist medium stays
     ("1", [OBJ_BVH]),
-    ("c1", [OBJ_PRIM, OBJ_PRIM, OBJ_PRIM]),  # no BVH in the run: unchanged
+    ("c1", [OBJ_BVH]),  # three spheres, the whole world: merged
+    ("4", [OBJ_PRIM]),  # a single object: unchanged
+    ("7", [OBJ_BVH, OBJ_MEDIUM, OBJ_MEDIUM]),  # Cornell smoke: six rects merged, the two box media stay
 ])
 def test_world_merging(name, kinds, tmp_path):
     blob = _saved(name, tmp_path)
