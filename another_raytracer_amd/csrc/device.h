@@ -677,6 +677,18 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
     bool hit = false;
     LaneStack<B, L> st(stk);
     int32_t node = root;
+#ifdef ART_STATS
+    // diagnostic mirror of the LDS variant's stack with each entry's box entry distance: counts stale visits (a
+    // popped node whose box is entered beyond the current tmax)
+    float dstk[kMaxStackDepth + 2];
+    int dsp = 0;
+    float cur_d = 0.0f;
+#define ART_DPUSH(q, keep) do { if (L) { dstk[dsp] = __uint_as_float(static_cast<uint32_t>(q) & 0xFFFF0000u); dsp += (keep) ? 1 : 0; } } while (0)
+#define ART_DPOP(c) do { if (L && (c)) { cur_d = dsp > 0 ? dstk[dsp - 1] : 0.0f; dsp -= dsp > 0 ? 1 : 0; } } while (0)
+#else
+#define ART_DPUSH(q, keep) do { } while (0)
+#define ART_DPOP(c) do { } while (0)
+#endif
 #if ART_SPECULATIVE
     // Speculative while-while (Aila & Laine 2009): a lane that reaches a leaf parks it and keeps walking inner nodes
     // until every lane of the wave holds a leaf, so the node loop runs with more lanes active; parked leaves are then
@@ -725,6 +737,9 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
         while (node >= 0 && !skip_nodes) {  // skip_nodes: ART_SPECULATIVE only
             ART_STAT_WAVE(0);
             ART_STAT_LANE(1);
+#ifdef ART_STATS
+            if (L && cur_d > tmaxf) ART_STAT_LANE(14);
+#endif
             float4 lx, hx, ly, hy, lz, hz;  // L: near (lx, ly, lz) and far (hx, hy, hz) planes
             int4 ch;
             [[maybe_unused]] float4 dly, dhy;  // L: near / far y motion planes
@@ -772,8 +787,14 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                 st.push(static_cast<int32_t>(q3), q3 < kKeyMiss);
                 st.push(static_cast<int32_t>(q2), q2 < kKeyMiss);
                 st.push(static_cast<int32_t>(q1), q1 < kKeyMiss);
+                ART_DPUSH(q3, q3 < kKeyMiss);
+                ART_DPUSH(q2, q2 < kKeyMiss);
+                ART_DPUSH(q1, q1 < kKeyMiss);
                 near = q0 < kKeyMiss;
                 near_child = static_cast<int16_t>(q0);
+#ifdef ART_STATS
+                if (near) cur_d = __uint_as_float(q0 & 0xFFFF0000u);
+#endif
             } else {
                 float k0, k1, k2, k3;
                 slab4(lx, hx, ly, hy, lz, hz, ch, ix, iy, iz, oix, oiy, oiz, tminf, tmaxf, k0, k1, k2, k3);
@@ -793,11 +814,13 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
             const int32_t top = st.peek();
             node = near ? near_child : top;
             st.pop_if(!near);
+            ART_DPOP(!near);
 #if ART_SPECULATIVE
             if (node < kNodeEmpty && parked == kNodeEmpty) {  // a leaf (codes below -1) and none parked yet: park it
                 parked = node;
                 node = st.peek();
                 st.pop_if(true);
+                ART_DPOP(true);
             }
             if (!__any(parked == kNodeEmpty)) break;  // every lane still walking holds a leaf: test them together
 #endif
@@ -816,12 +839,14 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                 leaf2 = node;
                 node = st.peek();
                 st.pop_if(true);
+                ART_DPOP(true);
             }
         } else {
             if (node == kNodeEmpty) break;
             leaf = node;
             node = st.peek();
             st.pop_if(true);
+            ART_DPOP(true);
         }
 #else
         if (node == kNodeEmpty) break;

@@ -2269,8 +2269,9 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
                      "traversals %llu nodes/trav %.2f leaftests/trav %.2f\n",
                      st[0], st[1], st[1] / (64.0 * st[0]), st[2], st[3], st[3] / (64.0 * st[2]), st[4], st[5], st[5] / (64.0 * st[4]), st[6],
                      double(st[1]) / st[6], double(st[3]) / st[6]);
-        std::fprintf(stderr, "ART_STATS dead node visits (LDS scene) %llu (%.3f of visits), leaf tests that shorten tmax %llu (%.3f of tests)\n",
-                     st[12], double(st[12]) / st[1], st[13], double(st[13]) / st[3]);
+        std::fprintf(stderr, "ART_STATS dead node visits (LDS scene) %llu (%.3f of visits), stale visits (box entered beyond tmax) %llu (%.3f), "
+                     "leaf tests that shorten tmax %llu (%.3f of tests)\n",
+                     st[12], double(st[12]) / st[1], st[14], double(st[14]) / st[1], st[13], double(st[13]) / st[3]);
         const double tt = double(st[8] + st[9] + st[10] + st[11]);
         if (tt > 0) std::fprintf(stderr, "ART_STATS cycles: load/claim %.3f trace %.3f shade %.3f append/store %.3f\n", st[8] / tt, st[9] / tt, st[10] / tt, st[11] / tt);
         std::memset(st, 0, sizeof st);
