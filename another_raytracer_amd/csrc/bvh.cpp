@@ -136,6 +136,200 @@ struct Builder {
     }
 };
 
+// Split BVH (Stich, Friedrich, Dietrich 2009, "Spatial Splits in Bounding Volume Hierarchies"): each node takes the
+// cheaper of the full-sweep object split and a binned spatial split, tried when the object split's children overlap;
+// a spatial split references a straddling primitive from both sides with its clipped boxes.  Tighter boxes for meshes
+// (fewer node visits and leaf tests), at the price of duplicated references (capped by kSbvhRefBudget).
+constexpr double kSbvhRefBudget = 1.5;
+double sbvh_alpha() {  // overlap / root area below which no spatial split is tried
+    static const double v = [] {
+        const char* e = std::getenv("ART_SBVH_ALPHA");
+        return e ? std::atof(e) : 1e-5;
+    }();
+    return v;
+}
+constexpr int kSbvhBins = 32;
+double sbvh_budget() {
+    static const double v = [] {
+        const char* e = std::getenv("ART_SBVH");
+        return e ? std::atof(e) : kSbvhRefBudget;  // 0 (or < 1): object splits only
+    }();
+    return v;
+}
+
+struct SItem {
+    uint32_t ref;
+    AABBd box;
+};
+AABBd box_of(const std::vector<SItem>& v, size_t b, size_t e) {
+    AABBd a = empty_box();
+    for (size_t i = b; i < e; ++i) grow(a, v[i].box);
+    return a;
+}
+AABBd box_and(const AABBd& a, const AABBd& b) {
+    AABBd r;
+    for (int k = 0; k < 3; ++k) {
+        r.mn[k] = std::max(a.mn[k], b.mn[k]);
+        r.mx[k] = std::min(a.mx[k], b.mx[k]);
+    }
+    return r;
+}
+bool box_valid(const AABBd& b) { return b.mn[0] <= b.mx[0] && b.mn[1] <= b.mx[1] && b.mn[2] <= b.mx[2]; }
+
+struct SBuilder {
+    const ClipFn& clip;
+    std::vector<uint32_t>& primrefs;
+    std::vector<BNode> tree;
+    double root_area = 0;
+    size_t refs_left = 0;  // duplicated references still allowed
+
+    int make_leaf_node(const std::vector<SItem>& items, const AABBd& box) {
+        if (items.size() > 127) throw std::runtime_error("bvh leaf too large (depth limit reached)");
+        const uint32_t first = static_cast<uint32_t>(primrefs.size());
+        if (first + items.size() > 0xFFFFFFu) throw std::runtime_error("too many primitives for the bvh encoding");
+        for (const SItem& it : items) primrefs.push_back(it.ref);
+        BNode n;
+        n.box = box;
+        n.leaf = make_leaf(first, static_cast<uint32_t>(items.size()));
+        tree.push_back(n);
+        return static_cast<int>(tree.size()) - 1;
+    }
+
+    int build(std::vector<SItem> items, int depth) {
+        const AABBd box = box_of(items, 0, items.size());
+        const size_t n = items.size();
+        if (n == 1 || depth >= kMaxBvhDepth - 1) return make_leaf_node(items, box);
+        const double parent = std::max(area(box), 1e-300);
+        auto cent = [](const SItem& it, int k) { return 0.5 * (it.box.mn[k] + it.box.mx[k]); };
+        // object split: full sweep over the centroids on each axis
+        double best = std::numeric_limits<double>::infinity();
+        int best_axis = -1;
+        size_t best_split = 0;
+        AABBd best_l{}, best_r{};
+        std::vector<SItem> order;
+        std::vector<double> right_area(n + 1);
+        std::vector<AABBd> right_box(n + 1);
+        for (int k = 0; k < 3; ++k) {
+            order = items;
+            std::stable_sort(order.begin(), order.end(), [&](const SItem& a, const SItem& b) { return cent(a, k) < cent(b, k); });
+            AABBd acc = empty_box();
+            for (size_t i = n - 1; i > 0; --i) {
+                grow(acc, order[i].box);
+                right_area[i] = area(acc);
+                right_box[i] = acc;
+            }
+            acc = empty_box();
+            for (size_t i = 1; i < n; ++i) {
+                grow(acc, order[i - 1].box);
+                const double cost = kCostTraverse + sah_ci() * (area(acc) * double(i) + right_area[i] * double(n - i)) / parent;
+                if (cost < best) {
+                    best = cost;
+                    best_axis = k;
+                    best_split = i;
+                    best_l = acc;
+                    best_r = right_box[i];
+                }
+            }
+        }
+        // spatial split: binned, when the object split's children overlap
+        int sp_axis = -1;
+        double sp_plane = 0, sp_best = best;
+        const AABBd ov = box_and(best_l, best_r);
+        if (refs_left > 0 && best_axis >= 0 && box_valid(ov) && area(ov) > sbvh_alpha() * root_area) {
+            for (int k = 0; k < 3; ++k) {
+                const double lo = box.mn[k], ext = box.mx[k] - box.mn[k];
+                if (!(ext > 0)) continue;
+                AABBd bins[kSbvhBins];
+                int enter[kSbvhBins] = {0}, leave[kSbvhBins] = {0};
+                for (auto& b : bins) b = empty_box();
+                auto bin_of = [&](double x) { return std::min(kSbvhBins - 1, std::max(0, static_cast<int>((x - lo) / ext * kSbvhBins))); };
+                auto plane = [&](int i) { return i == kSbvhBins ? box.mx[k] : lo + ext * i / kSbvhBins; };
+                for (const SItem& it : items) {
+                    const int b0 = bin_of(it.box.mn[k]), b1 = bin_of(it.box.mx[k]);
+                    if (b0 == b1) {
+                        grow(bins[b0], it.box);
+                    } else {
+                        for (int b = b0; b <= b1; ++b) {
+                            AABBd c;
+                            if (clip(it.ref, k, b == b0 ? it.box.mn[k] : plane(b), b == b1 ? it.box.mx[k] : plane(b + 1), it.box, c)) grow(bins[b], c);
+                        }
+                    }
+                    ++enter[b0];
+                    ++leave[b1];
+                }
+                double ra[kSbvhBins];
+                int rn[kSbvhBins];
+                AABBd acc = empty_box();
+                int cnt = 0;
+                for (int i = kSbvhBins - 1; i > 0; --i) {
+                    grow(acc, bins[i]);
+                    cnt += leave[i];
+                    ra[i] = box_valid(acc) ? area(acc) : 0;
+                    rn[i] = cnt;
+                }
+                acc = empty_box();
+                cnt = 0;
+                for (int i = 1; i < kSbvhBins; ++i) {
+                    grow(acc, bins[i - 1]);
+                    cnt += enter[i - 1];
+                    if (cnt == 0 || rn[i] == 0) continue;
+                    const double cost = kCostTraverse + sah_ci() * ((box_valid(acc) ? area(acc) : 0) * cnt + ra[i] * rn[i]) / parent;
+                    if (cost < sp_best) {
+                        sp_best = cost;
+                        sp_axis = k;
+                        sp_plane = plane(i);
+                    }
+                }
+            }
+        }
+        const double leaf_cost = sah_ci() * double(n);
+        if (n <= static_cast<size_t>(sah_leaf()) && leaf_cost <= std::min(best, sp_best)) return make_leaf_node(items, box);
+        std::vector<SItem> left, right;
+        if (sp_axis >= 0) {
+            const int k = sp_axis;
+            for (const SItem& it : items) {
+                if (it.box.mx[k] <= sp_plane) {
+                    left.push_back(it);
+                } else if (it.box.mn[k] >= sp_plane) {
+                    right.push_back(it);
+                } else {
+                    AABBd cl, cr;
+                    const bool hl = clip(it.ref, k, it.box.mn[k], sp_plane, it.box, cl);
+                    const bool hr = clip(it.ref, k, sp_plane, it.box.mx[k], it.box, cr);
+                    if (hl) left.push_back(SItem{it.ref, cl});
+                    if (hr) right.push_back(SItem{it.ref, cr});
+                    if (!hl && !hr) left.push_back(it);  // degenerate clip: keep the reference whole
+                    if (hl && hr) refs_left -= refs_left > 0 ? 1 : 0;
+                }
+            }
+        }
+        if (left.empty() || right.empty()) {  // object split (also when the spatial partition degenerated)
+            left.clear();
+            right.clear();
+            if (best_axis < 0) {
+                if (n <= 127) return make_leaf_node(items, box);
+                best_axis = 0;
+                best_split = n / 2;
+            }
+            order = items;
+            const int k = best_axis;
+            std::stable_sort(order.begin(), order.end(), [&](const SItem& a, const SItem& b) { return cent(a, k) < cent(b, k); });
+            left.assign(order.begin(), order.begin() + static_cast<std::ptrdiff_t>(best_split));
+            right.assign(order.begin() + static_cast<std::ptrdiff_t>(best_split), order.end());
+        }
+        items.clear();
+        items.shrink_to_fit();
+        const int me = static_cast<int>(tree.size());
+        tree.push_back(BNode{});
+        const int l = build(std::move(left), depth + 1);
+        const int r = build(std::move(right), depth + 1);
+        tree[me].box = box;
+        tree[me].left = l;
+        tree[me].right = r;
+        return me;
+    }
+};
+
 // Emits the 4-wide node for binary inner node `bn` (children pulled up greedily by largest surface area) and returns
 // its index; `stack` receives the worst-case traversal stack use below and including it.
 int32_t collapse(const std::vector<BNode>& tree, int bn, std::vector<BvhNode>& out, int& stack, int& depth) {
@@ -207,16 +401,32 @@ void conservative_box(const AABBd& b, float lo[3], float hi[3]) {
 }
 
 int32_t build_sah_bvh(const std::vector<AABBd>& boxes, const std::vector<uint32_t>& refs, std::vector<BvhNode>& nodes,
-                      std::vector<uint32_t>& primrefs, int& max_depth, int& max_stack) {
+                      std::vector<uint32_t>& primrefs, int& max_depth, int& max_stack, const ClipFn* clip) {
     if (boxes.empty() || boxes.size() != refs.size()) throw std::runtime_error("bad bvh input");
     Builder bl{boxes, refs, primrefs, {}, {}, {}};
-    bl.idx.resize(boxes.size());
-    bl.cent.resize(boxes.size());
-    for (size_t i = 0; i < boxes.size(); ++i) {
-        bl.idx[i] = static_cast<uint32_t>(i);
-        for (int k = 0; k < 3; ++k) bl.cent[i][k] = 0.5 * (boxes[i].mn[k] + boxes[i].mx[k]);
+    SBuilder sb{clip ? *clip : ClipFn{}, primrefs, {}, 0, 0};
+    const bool split = clip && sbvh_budget() > 1.0;
+    int root;
+    if (split) {
+        std::vector<SItem> items(boxes.size());
+        AABBd all = empty_box();
+        for (size_t i = 0; i < boxes.size(); ++i) {
+            items[i] = SItem{refs[i], boxes[i]};
+            grow(all, boxes[i]);
+        }
+        sb.root_area = area(all);
+        sb.refs_left = static_cast<size_t>((sbvh_budget() - 1.0) * static_cast<double>(boxes.size()));
+        root = sb.build(std::move(items), 0);
+        bl.tree.swap(sb.tree);
+    } else {
+        bl.idx.resize(boxes.size());
+        bl.cent.resize(boxes.size());
+        for (size_t i = 0; i < boxes.size(); ++i) {
+            bl.idx[i] = static_cast<uint32_t>(i);
+            for (int k = 0; k < 3; ++k) bl.cent[i][k] = 0.5 * (boxes[i].mn[k] + boxes[i].mx[k]);
+        }
+        root = bl.build(0, static_cast<int>(boxes.size()), 0);
     }
-    const int root = bl.build(0, static_cast<int>(boxes.size()), 0);
     if (bl.tree[root].is_leaf()) {  // a single leaf: a root node with one real child
         const int32_t me = static_cast<int32_t>(nodes.size());
         nodes.push_back(BvhNode{});

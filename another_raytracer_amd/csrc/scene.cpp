@@ -800,7 +800,57 @@ struct Compiler {
                 boxes.swap(b2);
             }
         }
-        o.a = build_sah_bvh(boxes, refs, f.nodes, f.primrefs, depth, stack);
+        // split BVH for meshes: a reference's clipped box is the box of the part of its triangle inside the slab (the
+        // polygon clipped by the two planes), or the slab of its box for any other primitive
+        const ClipFn clip = [&](uint32_t ref, int axis, double lo, double hi, const AABBd& cur, AABBd& out) -> bool {
+            AABBd slab = cur;
+            slab.mn[axis] = std::max(cur.mn[axis], lo);
+            slab.mx[axis] = std::min(cur.mx[axis], hi);
+            if (!(slab.mn[axis] <= slab.mx[axis])) return false;
+            if (primref_type(ref) != PRIM_TRIANGLE) {
+                out = slab;
+                return true;
+            }
+            const TriRec<double>& t = f.tris[primref_index(ref)];
+            Vec3 poly[8], next[8];
+            int np = 3;
+            for (int v = 0; v < 3; ++v) poly[v] = Vec3(t.p[3 * v], t.p[3 * v + 1], t.p[3 * v + 2]);
+            for (int side = 0; side < 2 && np > 0; ++side) {  // keep x >= lo, then x <= hi (Sutherland-Hodgman)
+                const double c = side == 0 ? lo : hi;
+                auto inside = [&](const Vec3& q) { return side == 0 ? q[axis] >= c : q[axis] <= c; };
+                int nn = 0;
+                for (int i = 0; i < np; ++i) {
+                    const Vec3& a = poly[i];
+                    const Vec3& b = poly[(i + 1) % np];
+                    const bool ia = inside(a), ib = inside(b);
+                    if (ia) next[nn++] = a;
+                    if (ia != ib) {
+                        const double u = (c - a[axis]) / (b[axis] - a[axis]);
+                        Vec3 q = a + u * (b - a);
+                        q[axis] = c;
+                        next[nn++] = q;
+                    }
+                }
+                np = nn;
+                for (int i = 0; i < np; ++i) poly[i] = next[i];
+            }
+            if (np == 0) return false;
+            AABBd pb{poly[0], poly[0]};
+            for (int i = 1; i < np; ++i)
+                for (int k = 0; k < 3; ++k) {
+                    pb.mn[k] = std::min(pb.mn[k], poly[i][k]);
+                    pb.mx[k] = std::max(pb.mx[k], poly[i][k]);
+                }
+            for (int k = 0; k < 3; ++k) {
+                out.mn[k] = std::max(pb.mn[k], slab.mn[k]);
+                out.mx[k] = std::min(pb.mx[k], slab.mx[k]);
+                if (!(out.mn[k] <= out.mx[k])) return false;
+            }
+            return true;
+        };
+        bool has_tri = false;
+        for (uint32_t r : refs) has_tri |= primref_type(r) == PRIM_TRIANGLE;
+        o.a = build_sah_bvh(boxes, refs, f.nodes, f.primrefs, depth, stack, has_tri ? &clip : nullptr);
         o.b = kNodeEmpty;
         if (!hoist.empty()) {
             o.b = make_leaf(static_cast<uint32_t>(f.primrefs.size()), static_cast<uint32_t>(hoist.size()));

@@ -123,3 +123,14 @@ def test_world_merging(name, kinds, tmp_path):
     objs, _ = _objs(blob)
     world = np.frombuffer(blob, "<i4", int(cnt[A_WORLD]), int(off[A_WORLD]))
     assert [int(objs[w]["kind"]) for w in world] == kinds
+
+
+def test_split_bvh_references_every_triangle(tmp_path):
+    # dino (394 triangles + the merged light rect): spatial splits reference straddling triangles from both sides, so
+    # there are more references than primitives, and every primitive keeps at least one
+    blob = _saved("dino", tmp_path)
+    off, cnt = _arrays(blob)
+    refs = np.frombuffer(blob, "<u4", int(cnt[A_PRIMREFS]), int(off[A_PRIMREFS]))
+    tris = refs[refs >> 30 == 1] & ((1 << 30) - 1)
+    assert len(refs) > 395
+    assert set(tris.tolist()) == set(range(394))
