@@ -519,10 +519,15 @@ __device__ __forceinline__ bool hit_lds_slot(const uint8_t* lds, uint32_t slot, 
     const double2 a = lds_d2(kLdsOffSph + slot * 16u), b = lds_d2(kLdsOffSph + (kLdsSlotCap + slot) * 16u);
     const uint32_t code = lds_u1(kLdsOffRef + slot * 4u);
     V3<double> center{a.x, a.y, b.x};
+#if ART_LDS_DY_SLOT
+    // y motion only (lds_scene_image): c + tm * (+-0, dy, +-0) leaves x and z as they are; static slots hold dy = -0
+    center.y = center.y + r.tm * lds_d1(kLdsOffMov + slot * 8u);
+#else
     const uint32_t mv = (code >> kLdsRefMovShift) & ((1u << (kLdsRefMatShift - kLdsRefMovShift)) - 1);
     if (mv) {  // y motion only (lds_scene_image): c + tm * (+0, dy, +0) leaves x and z exactly as they are
         center.y = center.y + r.tm * lds_d1(kLdsOffMov + (mv - 1u) * 8u);
     }
+#endif
     prim = make_primref(PRIM_SPHERE, code & kLdsRefIndexMask);
     mt = code >> kLdsRefMatShift;
     return sphere_root<double, true>(center, b.y, r, d_a, d_inv_a, tmin, tmax, t);
@@ -584,7 +589,10 @@ struct LaneStack<B, true> {  // LDS-scene variant: 16-bit entries, tracked as th
         top += keep ? kRow : 0u;
     }
     __device__ __forceinline__ int32_t peek() const { return *(__attribute__((address_space(3))) const int16_t*)(size_t)top; }
-    __device__ __forceinline__ void pop_if(bool c) { top -= (c && top != bottom) ? kRow : 0u; }
+    // No empty-stack guard: popping the empty stack yields the sentinel row's kNodeEmpty and leaves top one row below
+    // it, but a walk whose node is kNodeEmpty ends without another peek or pop (traverse), so that row is never read;
+    // the next walk starts from a fresh LaneStack.
+    __device__ __forceinline__ void pop_if(bool c) { top -= c ? kRow : 0u; }
 };
 template <int B>
 struct LaneStack<B, false> {  // 32-bit entries

@@ -409,11 +409,16 @@ __device__ __forceinline__ bool shade_hit_lds(const uint8_t* lds, uint32_t slot,
     const uint32_t code = reinterpret_cast<const uint32_t*>(lds + kLdsOffRef)[slot];
     const uint32_t mi = reinterpret_cast<const uint16_t*>(lds + kLdsOffMatIdx)[slot];
     V3<R> center{a.x, a.y, b.x};
+#if ART_LDS_DY_SLOT
+    center.y = center.y + st.ray.tm * reinterpret_cast<const double*>(lds + kLdsOffMov)[slot];  // dy = -0: static
+    (void)code;
+#else
     const uint32_t mv = (code >> kLdsRefMovShift) & ((1u << (kLdsRefMatShift - kLdsRefMovShift)) - 1);
     if (mv) {  // moving_sphere.h:72-74, as prim_surface; unit shutter, y motion (lds_scene_image): (tm - 0) / 1 == tm,
                // and x + tm * (+0) == x, z + tm * (+0) == z
         center.y = center.y + st.ray.tm * reinterpret_cast<const double*>(lds + kLdsOffMov)[mv - 1];
     }
+#endif
     Surf<R> s;
     s.p = st.ray.at(t);
     set_face_normal(s, st.ray, reinterpret_cast<const double*>(lds + kLdsOffInvR)[slot] * (s.p - center));  // (p - c) / r
@@ -755,7 +760,9 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S, PassGe
     const uint32_t lane = __lane_id();
     const uint64_t below = (1ull << lane) - 1ull;
     const V3<R> bg = mk(S.bg[0], S.bg[1], S.bg[2]);
+#if !ART_RAY_POOL
     uint32_t cur = 0, end = 0;  // this wave's claimed slots [cur, end): wave-uniform
+#endif
     bool busy = false, drained = false;
     uint32_t q = 0;
     int depth = 0;
@@ -1630,8 +1637,12 @@ static std::vector<uint8_t> lds_scene_image(const FlatScene& f, uint32_t& nmov, 
         put(kLdsOffSph + (kLdsSlotCap + sl) * 16, p1, 16);
         put(kLdsOffInvR + sl * 8, &inv_r, 8);
         uint32_t code = idx | (f.mats[sp.mat].type << kLdsRefMatShift);
+        if (ART_LDS_DY_SLOT) {
+            const double dy = moving ? sp.d[1] : -0.0;
+            put(kLdsOffMov + sl * 8, &dy, 8);
+        }
         if (moving) {
-            put(kLdsOffMov + m * 8, &sp.d[1], 8);
+            if (!ART_LDS_DY_SLOT) put(kLdsOffMov + m * 8, &sp.d[1], 8);
             code |= (m + 1) << kLdsRefMovShift;
             ++m;
         }

@@ -105,12 +105,19 @@ constexpr uint32_t kLdsNodePlanes = ART_LDS_MOTION ? 13 : 10;
 constexpr uint32_t kLdsNodePlaneChild = 9;
 constexpr uint32_t kLdsNodePlaneMotion = 10;  // dlo y, dhi y, dlo y
 constexpr uint32_t kLdsSlotCap = 1024;  // leaf slots (= primref array entries): 2 planes (cx, cy), (cz, r) as double2
-constexpr uint32_t kLdsMovCap = 512;    // moving spheres (unit shutter, y motion): one plane of dy (f64)
+constexpr uint32_t kLdsMovCap = 512;    // moving spheres (unit shutter, y motion)
+// ART_LDS_DY_SLOT (default 1): the y motion is a plane of one f64 dy per leaf slot, -0.0 for a static sphere
+// (c.y + tm * -0 == c.y for every c.y and tm >= 0, -0 included), so a leaf test loads it beside the sphere planes and
+// runs one branch-free sequence; 0: one dy per moving sphere, reached through the slot's code (a load that waits
+// on the code load, inside a branch)
+#ifndef ART_LDS_DY_SLOT
+#define ART_LDS_DY_SLOT 1
+#endif
 constexpr uint32_t kLdsOffNodes = 0;
 constexpr uint32_t kLdsOffSph = kLdsOffNodes + kLdsNodePlanes * kLdsNodeCap * 16;
 constexpr uint32_t kLdsOffMov = kLdsOffSph + 2 * kLdsSlotCap * 16;
 // u32 per slot: sphere index (19 bits) | (moving index + 1) << 19 (10 bits) | material type << 29 (3 bits)
-constexpr uint32_t kLdsOffRef = kLdsOffMov + kLdsMovCap * 8;
+constexpr uint32_t kLdsOffRef = kLdsOffMov + (ART_LDS_DY_SLOT ? kLdsSlotCap : kLdsMovCap) * 8;
 // Shading table (fused variant): u16 per slot = material entry e | kLdsMatChecker, and kLdsMatCap 32-B entries
 // (c.x, c.y), (c.z, param): lambertian / diffuse_light colour (a checker of two solid colours takes entries e = even,
 // e + 1 = odd), metal albedo + fuzz, dielectric (-, -, -, ir).  A hit is then shaded without any global load.
