@@ -553,6 +553,13 @@ __device__ __forceinline__ void stat_lane(int k) { atomicAdd(&g_art_stats[k], 1u
 #ifndef ART_SPECULATIVE
 #define ART_SPECULATIVE 1
 #endif
+#ifndef ART_PARK_BRANCHLESS
+// LDS variant, node loop: parking reads the two top stack entries up front (no dependent read in a branch): -1.2 %
+#define ART_PARK_BRANCHLESS 0
+#endif
+#ifndef ART_LEAFSEL_BRANCHLESS
+#define ART_LEAFSEL_BRANCHLESS 1  // LDS variant, leaf-phase entry: one stack read up front, selects instead of branches
+#endif
 #ifndef ART_OBJ_PRIMS
 #define ART_OBJ_PRIMS 1  // prim objects test the per-object primitive copy (DevScene::obj_prims)
 #endif
@@ -589,6 +596,9 @@ struct LaneStack<B, true> {  // LDS-scene variant: 16-bit entries, tracked as th
         top += keep ? kRow : 0u;
     }
     __device__ __forceinline__ int32_t peek() const { return *(__attribute__((address_space(3))) const int16_t*)(size_t)top; }
+    // the entry under the top (garbage, never used, when the stack holds fewer than one entry: the row below the
+    // sentinel is still inside LDS, at the end of the scene image)
+    __device__ __forceinline__ int32_t peek_below() const { return *(__attribute__((address_space(3))) const int16_t*)(size_t)(top - kRow); }
     // No empty-stack guard: popping the empty stack yields the sentinel row's kNodeEmpty and leaves top one row below
     // it, but a walk whose node is kNodeEmpty ends without another peek or pop (traverse), so that row is never read;
     // the next walk starts from a fresh LaneStack.
@@ -819,17 +829,37 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                 near = k0 < inf;
                 near_child = c0;
             }
-            const int32_t top = st.peek();
-            node = near ? near_child : top;
-            st.pop_if(!near);
-            ART_DPOP(!near);
+#if ART_SPECULATIVE && ART_PARK_BRANCHLESS
+            if constexpr (L) {
+                // the next node and the one under it, read together: a lane that parks a leaf takes the second without
+                // a dependent stack read inside a divergent branch
+                const int32_t t0 = st.peek(), t1 = st.peek_below();
+                const int32_t n0 = near ? near_child : t0;  // the next node
+                const int32_t n1 = near ? t0 : t1;          // the stack entry under it
+                const bool park = n0 < kNodeEmpty && parked == kNodeEmpty;  // a leaf and none parked yet: park it
+                parked = park ? n0 : parked;
+                node = park ? n1 : n0;
+                st.pop_if(!near);
+                st.pop_if(park);
+                ART_DPOP(!near);
+                ART_DPOP(park);
+            } else
+#endif
+            {
+                const int32_t top = st.peek();
+                node = near ? near_child : top;
+                st.pop_if(!near);
+                ART_DPOP(!near);
 #if ART_SPECULATIVE
-            if (node < kNodeEmpty && parked == kNodeEmpty) {  // a leaf (codes below -1) and none parked yet: park it
-                parked = node;
-                node = st.peek();
-                st.pop_if(true);
-                ART_DPOP(true);
+                if (node < kNodeEmpty && parked == kNodeEmpty) {  // a leaf (codes below -1) and none parked yet: park it
+                    parked = node;
+                    node = st.peek();
+                    st.pop_if(true);
+                    ART_DPOP(true);
+                }
+#endif
             }
+#if ART_SPECULATIVE
             if (!__any(parked == kNodeEmpty)) break;  // every lane still walking holds a leaf: test them together
 #endif
         }
@@ -841,6 +871,22 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
         skip_nodes = false;
         int32_t leaf = parked;
         int32_t leaf2 = kNodeEmpty;
+#if ART_LEAFSEL_BRANCHLESS
+        if constexpr (L) {
+            // the same choices as below, with the stack read once up front (no dependent read in a divergent branch)
+            const bool has = parked != kNodeEmpty;
+            if (!has && node == kNodeEmpty) break;
+            const int32_t t0 = st.peek();
+            const bool take2 = has && node < kNodeEmpty;  // a second leaf in hand: test both in this phase
+            const bool pop = take2 || !has;
+            leaf = has ? parked : node;
+            leaf2 = take2 ? node : kNodeEmpty;
+            node = pop ? t0 : node;
+            st.pop_if(pop);
+            ART_DPOP(pop);
+            parked = kNodeEmpty;
+        } else
+#endif
         if (leaf != kNodeEmpty) {
             parked = kNodeEmpty;
             if ((L || ART_LEAF2_G) && node < kNodeEmpty) {
