@@ -560,6 +560,12 @@ __device__ __forceinline__ void stat_lane(int k) { atomicAdd(&g_art_stats[k], 1u
 #ifndef ART_LEAFSEL_BRANCHLESS
 #define ART_LEAFSEL_BRANCHLESS 1  // LDS variant, leaf-phase entry: one stack read up front, selects instead of branches
 #endif
+#ifndef ART_LEAFSEL_BRANCHLESS_G
+#define ART_LEAFSEL_BRANCHLESS_G 1  // the same in the HBM-scene variant
+#endif
+#ifndef ART_POP_GUARD_G
+#define ART_POP_GUARD_G 0  // 1: HBM-scene variant stack pops keep the empty-stack guard
+#endif
 #ifndef ART_OBJ_PRIMS
 #define ART_OBJ_PRIMS 1  // prim objects test the per-object primitive copy (DevScene::obj_prims)
 #endif
@@ -614,7 +620,12 @@ struct LaneStack<B, false> {  // 32-bit entries
         sp += keep;
     }
     __device__ __forceinline__ int32_t peek() const { return stk[(sp - 1) * B]; }
+#if ART_POP_GUARD_G
     __device__ __forceinline__ void pop_if(bool c) { sp -= (c && sp > 0) ? 1 : 0; }
+#else
+    // no empty-stack guard, as LaneStack<B, true>: a walk that pops the sentinel's kNodeEmpty ends without reading on
+    __device__ __forceinline__ void pop_if(bool c) { sp -= c ? 1 : 0; }
+#endif
 };
 // Traversal stack entry: node/leaf codes, 16 bits in the LDS-scene variant (layout.h lds_leaf), 32 bits otherwise.
 template <bool L> using StackT = typename std::conditional<L, int16_t, int32_t>::type;
@@ -872,12 +883,12 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
         int32_t leaf = parked;
         int32_t leaf2 = kNodeEmpty;
 #if ART_LEAFSEL_BRANCHLESS
-        if constexpr (L) {
+        if constexpr (L || ART_LEAFSEL_BRANCHLESS_G) {
             // the same choices as below, with the stack read once up front (no dependent read in a divergent branch)
             const bool has = parked != kNodeEmpty;
             if (!has && node == kNodeEmpty) break;
             const int32_t t0 = st.peek();
-            const bool take2 = has && node < kNodeEmpty;  // a second leaf in hand: test both in this phase
+            const bool take2 = has && (L || ART_LEAF2_G) && node < kNodeEmpty;  // a second leaf in hand: test both in this phase
             const bool pop = take2 || !has;
             leaf = has ? parked : node;
             leaf2 = take2 ? node : kNodeEmpty;
