@@ -705,7 +705,11 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
     const R d_inv_a = L ? R(1) / d_a : R(0);
     bool hit = false;
     LaneStack<B, L> st(stk);
-    int32_t node = root;
+    // L: inner nodes are coded by their byte offset in a node plane (index * 16, layout.h), so a visit's plane
+    // addresses are one add each
+    static_assert(kLdsNodeCap * 16 <= 32767, "LDS inner-node codes are 16-bit stack entries");
+    const int32_t root_code = L ? root * 16 : root;
+    int32_t node = root_code;
 #ifdef ART_STATS
     // diagnostic mirror of the LDS variant's stack with each entry's box entry distance: counts stale visits (a
     // popped node whose box is entered beyond the current tmax)
@@ -736,7 +740,7 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
         parked = h;
         skip_nodes = true;
 #else
-        st.push(root, true);
+        st.push(root_code, true);
         node = h;
 #endif
     }
@@ -773,7 +777,7 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
             int4 ch;
             [[maybe_unused]] float4 dly, dhy;  // L: near / far y motion planes
             if constexpr (L) {
-                const uint32_t n16 = static_cast<uint32_t>(node) * 16u;
+                const uint32_t n16 = static_cast<uint32_t>(node);  // index * 16
                 const uint32_t ax = n16 + off_nx, ay = n16 + off_ny, az = n16 + off_nz;
                 lx = lds_f4(ax);
                 hx = lds_f4(ax + kLdsPlane);

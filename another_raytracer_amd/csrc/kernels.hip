@@ -1602,7 +1602,8 @@ static std::vector<uint8_t> lds_scene_image(const FlatScene& f, uint32_t& nmov, 
                 motion[0][c] = f32_down(static_cast<double>(lo1) - static_cast<double>(lo0));  // lo0 + dlo <= lo1
                 motion[1][c] = f32_up(static_cast<double>(hi1) - static_cast<double>(hi0));
             }
-            child[c] = empty ? kLdsEmptyChild : b.child[c] >= 0 ? b.child[c] : lds_leaf(leaf_first(b.child[c]), leaf_count(b.child[c]));
+            // inner nodes by their byte offset in a plane (index * 16: device.h traverse), leaves as lds_leaf codes
+            child[c] = empty ? kLdsEmptyChild : b.child[c] >= 0 ? b.child[c] * 16 : lds_leaf(leaf_first(b.child[c]), leaf_count(b.child[c]));
         }
         // per axis: lo, hi, lo (layout.h kLdsNodePlanes), the child codes, then y motion: dlo, dhi, dlo
         const int order[9] = {0, 1, 0, 2, 3, 2, 4, 5, 4};

@@ -133,7 +133,8 @@ constexpr uint32_t kLdsImageBytes = kLdsOffInvR + kLdsSlotCap * 8;
 constexpr uint32_t kLdsRefMovShift = 19;
 constexpr uint32_t kLdsRefMatShift = 29;
 constexpr uint32_t kMatUnknown = 0xFFu;  // HitOut::mt when the hit did not come from the LDS image
-// Child codes in the image: inner node n as is, leaf ~((count << 10) | first), empty -1 -- all fit the 16-bit LDS
+// Child codes in the image: inner node n as 16 * n (its byte offset in a plane), leaf ~((count << 10) | first), empty
+// -1 -- all fit the 16-bit LDS
 // traversal stack entries of this variant (halving the stack is what lets 1024 lanes share one image).
 constexpr uint32_t kLdsLeafShift = 10;
 constexpr uint32_t kLdsLeafMaxCount = 31;
