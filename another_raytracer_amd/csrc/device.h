@@ -48,7 +48,28 @@ template <class R> __device__ __forceinline__ R len2(V3<R> v) { return v.x * v.x
 template <class R> __device__ __forceinline__ V3<R> cross(V3<R> u, V3<R> v) {
     return {u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x};
 }
-template <class R> __device__ __forceinline__ V3<R> divs(V3<R> v, R t) { return (R(1) / t) * v; }  // vec3.h:97-99
+// 1 / x correctly rounded, as the compiler's f64 division expansion computes it when no operand needs scaling
+// (v_div_scale returns its inputs, v_div_fmas is a plain fma and v_div_fixup passes its input through for
+// 2^-1000 < x < 2^1000): hardware rcp, two Newton steps, the residual fma and the final fma -- the same operations on
+// the same values, without the scale, fmas and fixup instructions.  Other x (0, inf, NaN, extreme exponents) take
+// the division.
+#ifndef ART_RCP_RN
+#define ART_RCP_RN 0  // measured: k_paths -1.1 %, the Next-Week final +0.4 % (GPU parity exact either way)
+#endif
+__device__ __forceinline__ double rcp_rn(double x) {
+#if ART_RCP_RN
+    const double ax = __builtin_fabs(x);
+    if (!(ax > 0x1p-1000 && ax < 0x1p1000)) return 1.0 / x;
+    double r = __builtin_amdgcn_rcp(x);
+    r = fma(fma(-x, r, 1.0), r, r);
+    r = fma(fma(-x, r, 1.0), r, r);
+    return fma(fma(-x, r, 1.0), r, r);
+#else
+    return 1.0 / x;
+#endif
+}
+__device__ __forceinline__ float rcp_rn(float x) { return 1.0f / x; }
+template <class R> __device__ __forceinline__ V3<R> divs(V3<R> v, R t) { return rcp_rn(t) * v; }  // vec3.h:97-99: (1/t) * v
 template <class R> __device__ __forceinline__ V3<R> unit(V3<R> v) { return divs(v, sqrt_rn(len2(v))); }
 template <class R> __device__ __forceinline__ bool near_zero(V3<R> v) {  // vec3.h:49-53
     const R s = R(1e-8);
