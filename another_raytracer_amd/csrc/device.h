@@ -578,6 +578,9 @@ __device__ __forceinline__ void stat_lane(int k) { atomicAdd(&g_art_stats[k], 1u
 // LDS variant, node loop: parking reads the two top stack entries up front (no dependent read in a branch): -1.2 %
 #define ART_PARK_BRANCHLESS 0
 #endif
+#ifndef ART_PARK_PREFETCH
+#define ART_PARK_PREFETCH 0  // 1: the node loop reads the entry under the stack top with the top (-1.4 %)
+#endif
 #ifndef ART_LEAFSEL_BRANCHLESS
 #define ART_LEAFSEL_BRANCHLESS 1  // LDS variant, leaf-phase entry: one stack read up front, selects instead of branches
 #endif
@@ -883,13 +886,24 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
 #endif
             {
                 const int32_t top = st.peek();
+#if ART_SPECULATIVE && ART_PARK_PREFETCH
+                // L: the entry under the top is read with it, so a lane that parks takes its next node without a
+                // dependent stack read inside the branch
+                [[maybe_unused]] int32_t below = 0;
+                if constexpr (L) below = st.peek_below();
+#endif
                 node = near ? near_child : top;
                 st.pop_if(!near);
                 ART_DPOP(!near);
 #if ART_SPECULATIVE
                 if (node < kNodeEmpty && parked == kNodeEmpty) {  // a leaf (codes below -1) and none parked yet: park it
                     parked = node;
+#if ART_PARK_PREFETCH
+                    if constexpr (L) node = near ? top : below;
+                    else node = st.peek();
+#else
                     node = st.peek();
+#endif
                     st.pop_if(true);
                     ART_DPOP(true);
                 }
