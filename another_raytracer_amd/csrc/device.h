@@ -578,6 +578,9 @@ __device__ __forceinline__ void stat_lane(int k) { atomicAdd(&g_art_stats[k], 1u
 // LDS variant, node loop: parking reads the two top stack entries up front (no dependent read in a branch): -1.2 %
 #define ART_PARK_BRANCHLESS 0
 #endif
+#ifndef ART_PUSH_MASKED
+#define ART_PUSH_MASKED 0  // 1: store only kept stack entries (exec-masked ds_write): -0.9 %
+#endif
 #ifndef ART_PARK_PREFETCH
 #define ART_PARK_PREFETCH 0  // 1: the node loop reads the entry under the stack top with the top (-1.4 %)
 #endif
@@ -622,7 +625,12 @@ struct LaneStack<B, true> {  // LDS-scene variant: 16-bit entries, tracked as th
     __device__ __forceinline__ explicit LaneStack(int16_t* stk)
         : bottom(static_cast<uint32_t>(reinterpret_cast<size_t>((__attribute__((address_space(3))) int16_t*)stk)) - kRow), top(bottom) {}
     __device__ __forceinline__ void push(int32_t v, bool keep) {
+#if ART_PUSH_MASKED
+        // the store of a kept entry only (an exec-masked ds_write; skipped by the wave when no lane keeps one)
+        if (keep) *(__attribute__((address_space(3))) int16_t*)(size_t)(top + kRow) = static_cast<int16_t>(v);
+#else
         *(__attribute__((address_space(3))) int16_t*)(size_t)(top + kRow) = static_cast<int16_t>(v);
+#endif
         top += keep ? kRow : 0u;
     }
     __device__ __forceinline__ int32_t peek() const { return *(__attribute__((address_space(3))) const int16_t*)(size_t)top; }
