@@ -1971,7 +1971,12 @@ static void launch_paths_g_ft(int num_cu, hipStream_t st, const DevScene<double>
     const uint32_t fit = head < kPathsGLdsCap ? static_cast<uint32_t>((kPathsGLdsCap - head) / sizeof(BvhNode)) : 0u;
     if (S.n_nodes > 0 && fit >= kLdsPartialMinNodes) {
         DevScene<double> SP = S;
-        SP.n_lds_nodes = std::min<uint32_t>(fit, S.n_nodes);
+        // ART_LDS_NODES_MAX (diagnostic): a cap on the LDS-resident nodes, to measure what each one is worth
+        static const uint32_t cap = [] {
+            const char* e = std::getenv("ART_LDS_NODES_MAX");
+            return e ? static_cast<uint32_t>(std::atoi(e)) : 0xFFFFFFFFu;
+        }();
+        SP.n_lds_nodes = std::min<uint32_t>(std::min<uint32_t>(fit, S.n_nodes), std::max<uint32_t>(cap, kLdsPartialMinNodes));
         const size_t lds_p = head + sizeof(BvhNode) * SP.n_lds_nodes;
         const int blocks = blocks_per_cu(reinterpret_cast<const void*>(k_paths_g<F, TF, 2>), kBlockM, lds_p) * num_cu;
         check_ring_waves(blocks, kBlockM, num_cu);
