@@ -248,6 +248,7 @@ struct DevScene {
     const ImageRec* images;
     const uint8_t* texels;
     const TriRec<R>* leaf_tris;  // leaf_tris[slot] = tris[index of primrefs[slot]] for triangle refs, zeros otherwise
+    const PrimRec80* leaf_prims;  // leaf_prims[slot]: the record of primrefs[slot] of any type (triangle-free kernels)
     const PrimRec80* obj_prims;  // obj_prims[o] = the record of prim object o's primitive (indexed like objs)
     const uint8_t* lds_image;   // layout.h LDS scene image (nullptr unless the scene qualifies)
     uint32_t n_nodes, n_primrefs, n_tris, n_objs;  // array lengths (k_paths_g's LDS copies)
@@ -598,6 +599,9 @@ __device__ __forceinline__ void stat_lane(int k) { atomicAdd(&g_art_stats[k], 1u
 #endif
 #ifndef ART_LEAF_TRIS
 #define ART_LEAF_TRIS 1  // triangle leaves read the leaf-ordered copy (DevScene::leaf_tris)
+#endif
+#ifndef ART_LEAF_PRIMS_G
+#define ART_LEAF_PRIMS_G 1  // triangle-free HBM-scene kernels read leaf records from the leaf-ordered copy
 #endif
 #ifndef ART_LEAF2_G
 #define ART_LEAF2_G 1  // the HBM-scene traversal also tests a lane's two pending leaves in one leaf phase
@@ -1022,6 +1026,18 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                     __asm__ volatile("" : "+v"(p1.x), "+v"(p1.y), "+v"(p1.z), "+v"(p2.x), "+v"(p2.y), "+v"(p2.z), "+v"(p3.x), "+v"(p3.y), "+v"(p3.z));
                     if (F == F_TRI || primref_type(ref) == PRIM_TRIANGLE) h = hit_tri_v(p1, p2, p3, r, tmin, tmax, tt);
                     else h = hit_prim<R, F & ~F_TRI>(S, ref, r, tmin, tmax, tt, fc);
+                } else if constexpr ((F & F_TRI) == 0 && ART_LEAF_PRIMS_G) {
+                    // the leaf-ordered record copy: its loads go out beside the primref's instead of behind it
+                    const uint4* lp = reinterpret_cast<const uint4*>(S.leaf_prims + slot);
+                    uint4 v0 = lp[0], v1 = lp[1], v2 = lp[2], v3 = lp[3], v4 = lp[4];
+                    ref = S.primrefs[slot];
+                    __asm__ volatile("" : "+v"(v0.x), "+v"(v0.y), "+v"(v0.z), "+v"(v0.w), "+v"(v1.x), "+v"(v1.y), "+v"(v1.z), "+v"(v1.w),
+                                          "+v"(v2.x), "+v"(v2.y), "+v"(v2.z), "+v"(v2.w), "+v"(v3.x), "+v"(v3.y), "+v"(v3.z), "+v"(v3.w));
+                    __asm__ volatile("" : "+v"(v4.x), "+v"(v4.y), "+v"(v4.z), "+v"(v4.w));
+                    PrimRec80 rec;
+                    uint4* rp = reinterpret_cast<uint4*>(rec.b);
+                    rp[0] = v0; rp[1] = v1; rp[2] = v2; rp[3] = v3; rp[4] = v4;
+                    h = hit_prim_rec<R, F>(primref_type(ref), rec, r, tmin, tmax, tt, fc);
                 } else {
                     ref = S.primrefs[slot];
                     h = hit_prim<R, F>(S, ref, r, tmin, tmax, tt, fc);

@@ -1731,6 +1731,17 @@ static void build_device_scene(const FlatScene& f, DeviceScene<R>& ds) {
         for (size_t i = 0; i < lt.size(); ++i)
             if (primref_type(f.primrefs[i]) == PRIM_TRIANGLE) lt[i] = tri[primref_index(f.primrefs[i])];
         ds.view.leaf_tris = ds.upload(lt);
+        std::vector<PrimRec80> lp(f.primrefs.size());  // every primitive type in leaf order (triangle-free kernels)
+        for (size_t i = 0; i < lp.size(); ++i) {
+            const uint32_t ref = f.primrefs[i], idx = primref_index(ref);
+            switch (primref_type(ref)) {
+                case PRIM_SPHERE: std::memcpy(lp[i].b, &sph[idx], sizeof(sph[idx])); break;
+                case PRIM_TRIANGLE: std::memcpy(lp[i].b, &tri[idx], sizeof(tri[idx])); break;
+                case PRIM_RECT: std::memcpy(lp[i].b, &rect[idx], sizeof(rect[idx])); break;
+                default: std::memcpy(lp[i].b, &box[idx], sizeof(box[idx])); break;
+            }
+        }
+        ds.view.leaf_prims = ds.upload(lp);
     }
     ds.view.nodes = ds.upload(f.nodes);
     ds.view.objs = ds.upload(objs);
