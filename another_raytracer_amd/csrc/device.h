@@ -473,6 +473,7 @@ __device__ __forceinline__ void slab4(const float4& lx, const float4& hx, const 
 constexpr uint32_t kKeyMiss = 0x7F800000u;
 // x0/y0/z0: entry distances at the near planes, x1/y1/z1: exit distances at the far planes (planes picked by the
 // direction's sign, so no per-axis min/max; a NaN plane distance (0 * inf) drops out of max/min as before).
+template <bool HI = false>
 __device__ __forceinline__ uint32_t slab_key_packed(float x0, float x1, float y0, float y1, float z0, float z1, int32_t child, float tminf,
                                                     float tmaxf) {
     const float lo = fmaxf(fmaxf(x0, y0), fmaxf(z0, tminf));
@@ -481,7 +482,9 @@ __device__ __forceinline__ uint32_t slab_key_packed(float x0, float x1, float y0
     float zt;
     __asm__("v_min_f32 %0, %1, %2" : "=v"(zt) : "v"(z1), "v"(tmaxf));
     const float hi = fminf(fminf(x1, y1), zt);
-    const uint32_t key = (__float_as_uint(lo) & 0xFFFF0000u) | (static_cast<uint32_t>(child) & 0xFFFFu);
+    // HI: the code is the high half of `child` (ART_CHILD16): bytes 3, 2 of lo over bytes 3, 2 of child, one v_perm
+    const uint32_t key = HI ? __builtin_amdgcn_perm(__float_as_uint(lo), static_cast<uint32_t>(child), 0x07060302u)
+                            : (__float_as_uint(lo) & 0xFFFF0000u) | (static_cast<uint32_t>(child) & 0xFFFFu);
     return lo <= hi ? key : kKeyMiss;  // empty slots carry a box no ray enters (layout.h kLdsEmptyChild)
 }
 // dly / dhy: the y motion planes (near, far), tiy = tm * iy: the y plane distances are those of the boxes at the ray's
@@ -506,9 +509,9 @@ __device__ __forceinline__ void slab4_packed(const float4& lx, const float4& hx,
     const f2v z0a = __builtin_elementwise_fma(f2v{lz.x, lz.y}, vz, nz), z0b = __builtin_elementwise_fma(f2v{lz.z, lz.w}, vz, nz);
     const f2v z1a = __builtin_elementwise_fma(f2v{hz.x, hz.y}, vz, nz), z1b = __builtin_elementwise_fma(f2v{hz.z, hz.w}, vz, nz);
     q0 = slab_key_packed(x0a.x, x1a.x, y0a.x, y1a.x, z0a.x, z1a.x, ch.x, tminf, tmaxf);
-    q1 = slab_key_packed(x0a.y, x1a.y, y0a.y, y1a.y, z0a.y, z1a.y, ch.y, tminf, tmaxf);
+    q1 = slab_key_packed<ART_CHILD16 != 0>(x0a.y, x1a.y, y0a.y, y1a.y, z0a.y, z1a.y, ch.y, tminf, tmaxf);
     q2 = slab_key_packed(x0b.x, x1b.x, y0b.x, y1b.x, z0b.x, z1b.x, ch.z, tminf, tmaxf);
-    q3 = slab_key_packed(x0b.y, x1b.y, y0b.y, y1b.y, z0b.y, z1b.y, ch.w, tminf, tmaxf);
+    q3 = slab_key_packed<ART_CHILD16 != 0>(x0b.y, x1b.y, y0b.y, y1b.y, z0b.y, z1b.y, ch.w, tminf, tmaxf);
 }
 __device__ __forceinline__ void ucas(uint32_t& a, uint32_t& b) {
     const uint32_t lo = a < b ? a : b;
@@ -825,7 +828,16 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                 dly = lds_f4(ay + (kLdsNodePlaneMotion - 3) * kLdsPlane);
                 dhy = lds_f4(ay + (kLdsNodePlaneMotion - 2) * kLdsPlane);
 #endif
+#if ART_CHILD16
+                {  // four 16-bit child codes in 8 bytes (layout.h): a ds_read_b64 instead of a ds_read_b128; codes 1
+                   // and 3 stay in the high halves (slab4_packed builds their keys with one byte permute)
+                    typedef unsigned u2v __attribute__((ext_vector_type(2)));
+                    const u2v cw = *(__attribute__((address_space(3))) const u2v*)(size_t)(kLdsOffNodes + kLdsNodePlaneChild * kLdsPlane + n16);
+                    ch = make_int4(static_cast<int32_t>(cw.x), static_cast<int32_t>(cw.x), static_cast<int32_t>(cw.y), static_cast<int32_t>(cw.y));
+                }
+#else
                 ch = lds_i4(kLdsOffNodes + kLdsNodePlaneChild * kLdsPlane + n16);
+#endif
             } else if (PL && static_cast<uint32_t>(node) < S.n_lds_nodes) {
                 // the top levels, copied into LDS: explicit LDS loads (a generic pointer here would be merged with
                 // the global branch's into flat loads)

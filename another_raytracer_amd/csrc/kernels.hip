@@ -1609,7 +1609,13 @@ static std::vector<uint8_t> lds_scene_image(const FlatScene& f, uint32_t& nmov, 
         const int order[9] = {0, 1, 0, 2, 3, 2, 4, 5, 4};
         const uint32_t nn = static_cast<uint32_t>(n);
         for (uint32_t j = 0; j < 9; ++j) put(kLdsOffNodes + (j * kLdsNodeCap + nn) * 16, planes[order[j]], 16);
-        put(kLdsOffNodes + (kLdsNodePlaneChild * kLdsNodeCap + nn) * 16, child, 16);
+        if (ART_CHILD16) {
+            const int16_t c16[8] = {static_cast<int16_t>(child[0]), static_cast<int16_t>(child[1]), static_cast<int16_t>(child[2]),
+                                    static_cast<int16_t>(child[3]), 0, 0, 0, 0};
+            put(kLdsOffNodes + (kLdsNodePlaneChild * kLdsNodeCap + nn) * 16, c16, 16);
+        } else {
+            put(kLdsOffNodes + (kLdsNodePlaneChild * kLdsNodeCap + nn) * 16, child, 16);
+        }
         if (ART_LDS_MOTION)
             for (uint32_t j = 0; j < 3; ++j) put(kLdsOffNodes + ((kLdsNodePlaneMotion + j) * kLdsNodeCap + nn) * 16, motion[j == 1 ? 1 : 0], 16);
     }

@@ -97,6 +97,9 @@ constexpr int kMaxStackDepth = 64;   // per-lane LDS traversal stack entries (si
 // ART_LDS_MOTION (default 0): measured on the random-spheres scene -- 7.6 % fewer node visits and 6.3 % fewer leaf
 // tests, but the two extra plane loads and FMAs per visit (and 21 more VGPR spills at k_paths' 128-VGPR cap) cost
 // more: -1.5 %.  Off, the nodes keep the 10 planes of the union boxes over the shutter.
+#ifndef ART_CHILD16
+#define ART_CHILD16 1  // the child plane holds a node's four codes as int16 in its first 8 bytes (else int32 x 4)
+#endif
 #ifndef ART_LDS_MOTION
 #define ART_LDS_MOTION 0
 #endif
