@@ -451,16 +451,18 @@ __device__ __forceinline__ bool shade_hit_lds(const uint8_t* lds, uint32_t slot,
         att = mk(ma.x, ma.y, mb.x);
         if (!(dot(dir, s.n) > R(0))) return false;
     } else {  // dielectric, material.h:63-99
-        const R ir = (reinterpret_cast<const double2*>(lds + kLdsOffMat) + 2 * e)[1].y;
+        // the table entry holds (1 / ir, r0 of the front face, r0 of the back face, ir), each computed on the host by
+        // the same IEEE operations material.h:74 and :93-94 apply (lds_scene_image): no division per hit
+        const double2* me = reinterpret_cast<const double2*>(lds + kLdsOffMat) + 2 * e;
+        const double2 m0 = me[0], m1 = me[1];
         att = mk(R(1), R(1), R(1));
-        const R ratio = s.ff ? (R(1) / ir) : ir;
+        const R ratio = s.ff ? m0.x : m1.y;  // front_face ? (1.0 / ir) : ir
         const R cos_theta = fmin(dot(-u, s.n), R(1));
         const R sin_theta = sqrt_rn(R(1) - cos_theta * cos_theta);
         const bool cannot = ratio * sin_theta > R(1);
         bool refl = cannot;
         if (!cannot) {
-            R r0 = (R(1) - ratio) / (R(1) + ratio);
-            r0 = r0 * r0;
+            const R r0 = s.ff ? m0.y : m1.x;  // ((1 - ratio) / (1 + ratio))^2
             const R refl_p = r0 + (R(1) - r0) * pow5(R(1) - cos_theta);
             refl = refl_p > uniform<R>(st.rng);
         }
@@ -1656,7 +1658,6 @@ static std::vector<uint8_t> lds_scene_image(const FlatScene& f, uint32_t& nmov, 
         put(kLdsOffRef + sl * 4, &code, 4);
         const auto& mat = f.mats[sp.mat];
         if (entry[sp.mat] < 0) {
-            const double zero[3] = {0, 0, 0};
             if (mat.type == MAT_LAMBERTIAN || mat.type == MAT_LIGHT) {
                 const auto& t = f.texs[mat.tex];
                 if (t.type == TEX_SOLID) {
@@ -1670,7 +1671,14 @@ static std::vector<uint8_t> lds_scene_image(const FlatScene& f, uint32_t& nmov, 
             } else if (mat.type == MAT_METAL) {
                 entry[sp.mat] = static_cast<int32_t>(put_entry(mat.albedo, mat.fuzz));
             } else if (mat.type == MAT_DIELECTRIC) {
-                entry[sp.mat] = static_cast<int32_t>(put_entry(zero, mat.ir));
+                // dielectric (material.h:63-99): 1 / ir, and reflectance()'s r0 = ((1 - ratio) / (1 + ratio))^2 for
+                // both faces, in the device's IEEE double arithmetic (-ffp-contract=off), then ir
+                const double inv = 1.0 / mat.ir;
+                double r0f = (1.0 - inv) / (1.0 + inv), r0b = (1.0 - mat.ir) / (1.0 + mat.ir);
+                r0f = r0f * r0f;
+                r0b = r0b * r0b;
+                const double d3[3] = {inv, r0f, r0b};
+                entry[sp.mat] = static_cast<int32_t>(put_entry(d3, mat.ir));
             } else {
                 shade_ok = false;
             }
