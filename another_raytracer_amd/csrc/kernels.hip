@@ -734,11 +734,19 @@ struct RayRing {
 };
 __host__ __device__ constexpr size_t paths_stack_bytes(uint32_t stack) { return (sizeof(int16_t) * stack * kBlockL + 15u) & ~size_t(15); }
 constexpr size_t kJumpBytes = sizeof(JumpEntry) * kJumpEntries;
-__host__ __device__ constexpr size_t paths_lds_bytes(uint32_t stack) {
-    return kLdsImageBytes + paths_stack_bytes(stack) + kJumpBytes + sizeof(CameraRec<double>) + sizeof(PassGeom);
+// The world list and object records, copied into LDS by every k_paths block: each trace walks them, and from global
+// memory they were three dependent vector loads (world slot -> object -> hoisted leaf) at the start of every trace
+// (vector, not scalar, loads: the kernel stores, so the compiler cannot prove them unclobbered).  The LDS scene
+// path requires a world of at most kPathsWorldCap objects (lds_scene_image; after world merging the benchmark scene
+// has one).
+constexpr uint32_t kPathsWorldCap = 16;
+constexpr size_t kPathsWorldBytes = sizeof(int32_t) * kPathsWorldCap + sizeof(ObjRec<double>) * kPathsWorldCap;
+__host__ __device__ constexpr size_t paths_lds_head(uint32_t stack) {
+    return ((kLdsImageBytes + paths_stack_bytes(stack) + kJumpBytes + sizeof(CameraRec<double>) + sizeof(PassGeom)) + 15u) & ~size_t(15);
 }
+__host__ __device__ constexpr size_t paths_lds_bytes(uint32_t stack) { return paths_lds_head(stack) + kPathsWorldBytes; }
 #if ART_SPLIT_PATHS != 1
-__global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S, PassGeom g, CameraRec<double> cam, Work<double> w, uint32_t* next_slot) {
+__global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S0, PassGeom g, CameraRec<double> cam, Work<double> w, uint32_t* next_slot) {
     using R = double;
     constexpr int B = kBlockL;
     // dynamic LDS only (no static __shared__, so the image starts at LDS address 0 and every image offset is an
@@ -752,11 +760,21 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S, PassGe
     CameraRec<double>& s_cam = *reinterpret_cast<CameraRec<double>*>(smem + kLdsImageBytes + paths_stack_bytes(g.stack) + kJumpBytes);
     PassGeom& s_g = *reinterpret_cast<PassGeom*>(smem + kLdsImageBytes + paths_stack_bytes(g.stack) + kJumpBytes + sizeof(CameraRec<double>));
     stk[-B] = static_cast<StackT<true>>(kNodeEmpty);
-    load_lds_image<B>(S.lds_image, smem);
+    load_lds_image<B>(S0.lds_image, smem);
     if (threadIdx.x < static_cast<uint32_t>(kJumpEntries)) jt[threadIdx.x] = pcg_jump(3u * threadIdx.x);
     if (threadIdx.x == 0) {
         s_cam = cam;
         s_g = g;
+    }
+    DevScene<double> S = S0;
+    {
+        uint8_t* wb = smem + paths_lds_head(g.stack);
+        uint8_t* ob = wb + sizeof(int32_t) * kPathsWorldCap;
+        if (threadIdx.x < static_cast<uint32_t>(S0.nworld)) reinterpret_cast<int32_t*>(wb)[threadIdx.x] = S0.world[threadIdx.x];
+        if (threadIdx.x < S0.n_objs * (sizeof(ObjRec<double>) / 16))
+            reinterpret_cast<uint4*>(ob)[threadIdx.x] = reinterpret_cast<const uint4*>(S0.objs)[threadIdx.x];
+        S.world = reinterpret_cast<const int32_t*>(wb);
+        S.objs = reinterpret_cast<const ObjRec<double>*>(ob);
     }
     __syncthreads();
     const uint32_t lane = __lane_id();
@@ -1511,6 +1529,7 @@ static std::vector<uint8_t> lds_scene_image(const FlatScene& f, uint32_t& nmov, 
     nmov = 0;
     shade_ok = false;
     if ((f.features & ~kFeatSpheres) != 0 || f.nodes.empty() || f.nodes.size() > kLdsNodeCap || f.primrefs.size() > kLdsSlotCap ||
+        f.world.size() > kPathsWorldCap || f.objs.size() > kPathsWorldCap ||
         f.spheres.size() > kLdsRefIndexMask || std::max(extend_lds_bytes(true, stack_rows(f.max_stack)), paths_lds_bytes(stack_rows(f.max_stack))) > kLdsPerCu)
         return img;
     for (uint32_t ref : f.primrefs) {
