@@ -528,6 +528,9 @@ __device__ __forceinline__ void cas(float& ka, int32_t& ca, float& kb, int32_t& 
     ca = c;
 }
 
+#ifndef ART_LDS_LEAF_NOREF
+#define ART_LDS_LEAF_NOREF 0  // 1 (k_paths object, Makefile PATHS_NOREF): the leaf test skips the per-slot code
+#endif
 // Leaf slot test of the LDS scene image (layout.h): the same root selection as hit_sphere on the same f64 values.
 // d_a = |d|^2 and d_inv_a = 1 / d_a come from the traversal (once per ray).  The image sits at LDS address 0, so
 // every read takes an integer LDS byte address (one shift-add, the plane offset folded in).  Moving spheres of the
@@ -542,7 +545,14 @@ __device__ __forceinline__ uint32_t lds_u1(uint32_t addr) { return *(__attribute
 __device__ __forceinline__ bool hit_lds_slot(const uint8_t* lds, uint32_t slot, const Ray<double>& r, double d_a, double d_inv_a,
                                              double tmin, double tmax, double& t, uint32_t& prim, uint32_t& mt) {
     const double2 a = lds_d2(kLdsOffSph + slot * 16u), b = lds_d2(kLdsOffSph + (kLdsSlotCap + slot) * 16u);
+#if ART_LDS_LEAF_NOREF
+    // k_paths (its own object, kernels_paths.o): the hit is shaded by slot, and its material type is read once after
+    // the trace, so the leaf test skips the per-slot code
+    prim = 0;
+    mt = kMatUnknown;
+#else
     const uint32_t code = lds_u1(kLdsOffRef + slot * 4u);
+#endif
     V3<double> center{a.x, a.y, b.x};
 #if ART_LDS_DY_SLOT
     // y motion only (lds_scene_image): c + tm * (+-0, dy, +-0) leaves x and z as they are; static slots hold dy = -0
@@ -553,8 +563,10 @@ __device__ __forceinline__ bool hit_lds_slot(const uint8_t* lds, uint32_t slot, 
         center.y = center.y + r.tm * lds_d1(kLdsOffMov + (mv - 1u) * 8u);
     }
 #endif
+#if !ART_LDS_LEAF_NOREF
     prim = make_primref(PRIM_SPHERE, code & kLdsRefIndexMask);
     mt = code >> kLdsRefMatShift;
+#endif
     return sphere_root<double, true>(center, b.y, r, d_a, d_inv_a, tmin, tmax, t);
 }
 

@@ -859,6 +859,9 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S0, PassG
         if (busy) {
             ++segs;
             hitw = trace_world<R, kFeatSpheres, B, true>(S, lds, st.ray, stk, st.rng, t, h);
+#if ART_LDS_LEAF_NOREF
+            if (hitw) h.mt = reinterpret_cast<const uint32_t*>(lds + kLdsOffRef)[h.obj >> 16] >> kLdsRefMatShift;
+#endif
         }
 #if ART_RAY_POOL
         // the ring stores of this round's refill (issued before the trace) are complete before the next round's loads
