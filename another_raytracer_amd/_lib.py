@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("ART_LIB") or os.path.join(_HERE, "libart.so")  # ART_
 
 RT_OK = 0
 RT_FP64 = 0  # the only fp_mode since ABI 2 (include/art.h)
-RT_ABI_VERSION = 2
+RT_ABI_VERSION = 3
 RT_OUT_DEVICE, RT_PROFILE, RT_GLOBAL_SCENE, RT_SPLIT_SHADE, RT_ADAPTIVE, RT_WAVEFRONT, RT_PARALLEL_IMAGES = 1, 2, 4, 8, 16, 32, 64
 ERRORS = {-1: "RT_E_INVALID", -2: "RT_E_SCENE", -3: "RT_E_DEVICE", -4: "RT_E_INTERNAL"}
 
@@ -83,10 +83,15 @@ SIGNATURES = {
                            ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8))]),
     "rt_image_free": (None, [ctypes.POINTER(ctypes.c_uint8)]),
     "rt_local_rows": (_I, [ctypes.POINTER(rt_params), ctypes.POINTER(ctypes.c_int32)]),
+    "rt_band_block_rows": (_I, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
+    "rt_unpack_bands": (_I, [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P]),
     "rt_multi_create": (_I, [ctypes.c_char_p, ctypes.c_char_p, _IP, _I, ctypes.POINTER(_P)]),
     "rt_multi_from_graph": (_I, [_P, _IP, _I, ctypes.POINTER(_P)]),
     "rt_multi_destroy": (None, [_P]),
     "rt_render_multi": (_I, [_P, ctypes.POINTER(rt_camera), ctypes.POINTER(rt_params), _P, ctypes.POINTER(rt_stats)]),
+    "rt_multi_ngpus": (_I, [_P]),
+    "rt_multi_scene_info": (_I, [_P, ctypes.POINTER(rt_scene_info)]),
+    "rt_multi_device_stats": (_I, [_P, _I, ctypes.POINTER(rt_stats)]),
     "rt_graph_new": (_P, []),
     "rt_graph_free": (None, [_P]),
     "rt_graph_random_double": (_I, [_P, _DP]),
@@ -150,3 +155,27 @@ def check(code, where):
 
 def dvec(v):
     return (ctypes.c_double * 3)(*[float(x) for x in v])
+
+
+def kernel_build_id(path=None):
+    """Identity of the device code in libart.so: the first 16 hex digits of the SHA-256 of its `.hip_fatbin` ELF section
+    (the gfx950 code objects of every kernel; host-only rebuilds keep it).  PMC summaries (tools/pmc_summary.py) are
+    stamped with it, and bench.py uses a summary's per-segment counters only when the stamp equals the loaded build."""
+    import hashlib
+    import struct
+    with open(path or LIB_PATH, "rb") as f:
+        data = f.read()
+    if data[:4] != b"\x7fELF" or data[4] != 2 or data[5] != 1:
+        raise ValueError("not a little-endian ELF64 file")
+    shoff, = struct.unpack_from("<Q", data, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", data, 0x3A)
+    def sec(i):
+        name, _typ, _flags, _addr, off, size = struct.unpack_from("<IIQQQQ", data, shoff + i * shentsize)
+        return name, off, size
+    _, stroff, _ = sec(shstrndx)
+    for i in range(shnum):
+        name, off, size = sec(i)
+        end = data.index(b"\0", stroff + name)
+        if data[stroff + name:end] == b".hip_fatbin":
+            return hashlib.sha256(data[off:off + size]).hexdigest()[:16]
+    raise ValueError("no .hip_fatbin section")

@@ -148,29 +148,31 @@ int rt_scene_build(const char* name, const char* asset_dir, int device, rt_scene
     });
 }
 
-int rt_scene_info_get(const rt_scene* s, rt_scene_info* info) {
-    if (!s || !info) return fail(RT_E_INVALID, "scene and info must be non-NULL");
+static void fill_info(const art::SceneView& view, const art::FlatScene& flat, rt_scene_info* info) {
     std::memset(info, 0, sizeof *info);
     for (int a = 0; a < 3; ++a) {
-        info->lookfrom[a] = s->view.lookfrom[a];
-        info->lookat[a] = s->view.lookat[a];
-        info->background[a] = s->flat.background[a];
+        info->lookfrom[a] = view.lookfrom[a];
+        info->lookat[a] = view.lookat[a];
+        info->background[a] = flat.background[a];
     }
-    info->vfov = s->view.vfov;
-    info->aperture = s->view.aperture;
-    info->spheres = static_cast<int64_t>(s->flat.spheres.size());
-    info->triangles = static_cast<int64_t>(s->flat.tris.size());
-    info->rects = static_cast<int64_t>(s->flat.rects.size());
-    info->boxes = static_cast<int64_t>(s->flat.boxes.size());
-    info->bvh_nodes = static_cast<int64_t>(s->flat.nodes.size());
-    info->objects = static_cast<int64_t>(s->flat.world.size());
-    info->materials = static_cast<int64_t>(s->flat.mats.size());
-    info->textures = static_cast<int64_t>(s->flat.texs.size());
-    info->has_media = s->flat.has_media ? 1 : 0;
-    info->max_bvh_depth = s->flat.max_bvh_depth;
-    if (s->renderer) {
-        info->device_bytes_f64 = s->renderer->scene_bytes();
-    }
+    info->vfov = view.vfov;
+    info->aperture = view.aperture;
+    info->spheres = static_cast<int64_t>(flat.spheres.size());
+    info->triangles = static_cast<int64_t>(flat.tris.size());
+    info->rects = static_cast<int64_t>(flat.rects.size());
+    info->boxes = static_cast<int64_t>(flat.boxes.size());
+    info->bvh_nodes = static_cast<int64_t>(flat.nodes.size());
+    info->objects = static_cast<int64_t>(flat.world.size());
+    info->materials = static_cast<int64_t>(flat.mats.size());
+    info->textures = static_cast<int64_t>(flat.texs.size());
+    info->has_media = flat.has_media ? 1 : 0;
+    info->max_bvh_depth = flat.max_bvh_depth;
+}
+
+int rt_scene_info_get(const rt_scene* s, rt_scene_info* info) {
+    if (!s || !info) return fail(RT_E_INVALID, "scene and info must be non-NULL");
+    fill_info(s->view, s->flat, info);
+    if (s->renderer) info->device_bytes_f64 = s->renderer->scene_bytes();
     return RT_OK;
 }
 
@@ -226,17 +228,28 @@ void rt_scene_destroy(rt_scene* s) {
 }
 
 int rt_local_rows(const rt_params* p, int32_t* rows_out) {
-    std::string why;
     if (!p || p->height < 1 || p->band_rows < 1 || p->band_count < 1 || p->band_index < 0 || p->band_index >= p->band_count)
         return fail(RT_E_INVALID, "invalid band partition");
-    int n = 0;
-    for (int ly = 0;; ++ly) {
-        int gy = (ly / p->band_rows) * (p->band_rows * p->band_count) + p->band_index * p->band_rows + (ly % p->band_rows);
-        if (gy >= p->height) break;
-        if (rows_out) rows_out[n] = gy;
-        ++n;
-    }
+    const int n = art::band_local_rows(p->height, p->band_rows, p->band_count, p->band_index);
+    if (rows_out)
+        for (int ly = 0; ly < n; ++ly) rows_out[ly] = art::band_global_row(ly, p->band_rows, p->band_count, p->band_index);
     return n;
+}
+
+int rt_band_block_rows(int32_t height, int32_t band_rows, int32_t n) {
+    if (height < 1 || band_rows < 1 || n < 1) return fail(RT_E_INVALID, "height, band_rows and n must be >= 1");
+    return art::band_block_rows(height, band_rows, n);
+}
+
+int rt_unpack_bands(const uint8_t* packed, uint8_t* frame, int32_t width, int32_t height, int32_t band_rows, int32_t n, int32_t flags,
+                    void* stream) {
+    if (!packed || !frame) return fail(RT_E_INVALID, "packed and frame must be non-NULL");
+    if (width < 1 || height < 1 || band_rows < 1 || n < 1) return fail(RT_E_INVALID, "width, height, band_rows and n must be >= 1");
+    if (static_cast<int64_t>(width) * height > (int64_t(1) << 31)) return fail(RT_E_INVALID, "image too large");
+    return guard(RT_E_DEVICE, [&] {
+        art::unpack_bands(packed, frame, width, height, band_rows, n, (flags & RT_OUT_DEVICE) != 0, stream);
+        return RT_OK;
+    });
 }
 
 int rt_render(rt_scene* s, const rt_camera* cam, const rt_params* p, uint8_t* out_rgb8, double* out_accum, rt_stats* stats) {
@@ -341,6 +354,31 @@ int rt_render_multi(rt_multi* m, const rt_camera* cam, const rt_params* p, uint8
         fill_stats(st, stats);
         return RT_OK;
     });
+}
+
+int rt_multi_device_stats(const rt_multi* m, int k, rt_stats* stats) {
+    if (!m || !stats) return fail(RT_E_INVALID, "multi and stats must be non-NULL");
+    art::RenderStats st;
+    if (!m->renderer->device_stats(k, st)) return fail(RT_E_INVALID, "no such device index, or no render yet");
+    fill_stats(st, stats);
+    return RT_OK;
+}
+int rt_multi_scene_info(const rt_multi* m, rt_scene_info* info) {
+    if (!m || !info) return fail(RT_E_INVALID, "multi and info must be non-NULL");
+    art::SceneView view;
+    for (int a = 0; a < 3; ++a) {
+        view.lookfrom[a] = m->graph.lookfrom[a];
+        view.lookat[a] = m->graph.lookat[a];
+    }
+    view.vfov = m->graph.vfov;
+    view.aperture = m->graph.aperture;
+    fill_info(view, m->flat, info);
+    info->device_bytes_f64 = m->renderer->scene_bytes();
+    return RT_OK;
+}
+int rt_multi_ngpus(const rt_multi* m) {
+    if (!m) return fail(RT_E_INVALID, "multi is NULL");
+    return m->renderer->ngpus();
 }
 
 // ---------------------------------------------------------------------------------------------- graph builder

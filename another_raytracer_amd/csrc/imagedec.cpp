@@ -697,7 +697,7 @@ DecodedImage decode_png(const uint8_t* b, size_t n) {
     while (at + 8 <= n && !end_seen) {
         const uint32_t len = be32(b + at);
         const uint8_t* type = b + at + 4;
-        if (n - at - 12 < len) pbad("truncated chunk");
+        if (n - at < 12 || n - at - 12 < len) pbad("truncated chunk");  // length + type + data + CRC must all be present
         const uint8_t* d = b + at + 8;
         if (!std::memcmp(type, "IHDR", 4)) {
             if (len != 13) pbad("bad IHDR");
@@ -736,6 +736,13 @@ DecodedImage decode_png(const uint8_t* b, size_t n) {
                           ((ctype == 2 || ctype == 4 || ctype == 6) && (depth == 8 || depth == 16));
     if (!depth_ok) pbad("bad bit depth for the color type");
     if (ctype == 3 && (plte.empty() || plte.size() % 3)) pbad("missing or bad palette");
+    // tRNS as stb_image v2.27 accepts it (stbi__parse_png_file): at most one alpha per palette entry; a colour key of
+    // exactly one 16-bit sample per channel for gray / RGB; none for the types that carry alpha
+    if (!trns.empty()) {
+        if (ctype == 3 && trns.size() > plte.size() / 3) pbad("bad tRNS len");
+        if ((ctype == 0 || ctype == 2) && trns.size() != static_cast<size_t>(2 * chans)) pbad("bad tRNS len");
+        if (ctype == 4 || ctype == 6) pbad("tRNS with alpha");
+    }
     // inflate
     std::vector<uint8_t> raw;
     {

@@ -214,4 +214,22 @@ struct CameraRec {       // camera.h: precomputed on the host in f64 exactly as 
     R lens_radius, time0, time1;
 };
 
+// ---------------------------------------------------------------------------------------------- band partition
+// Row-interleaved bands (the multi-GPU split; ancestor: _run_parallel_stripes' 4 contiguous stripes, engine.h:335-376):
+// global row y belongs to band y / band_rows, rendered by band set (y / band_rows) % n.  Local row ly of band set r
+// is global row band_global_row(ly, ...); band set r owns band_local_rows(H, ...) rows.  One rule for the kernels
+// (kernels.hip global_row), rt_local_rows, the RCCL gather's block size and the unpack (multi.hip).
+ART_HD int band_global_row(int ly, int band_rows, int n, int r) {
+    return (ly / band_rows) * (band_rows * n) + r * band_rows + (ly % band_rows);
+}
+ART_HD int band_local_rows(int H, int band_rows, int n, int r) {
+    // full cycles of n bands, then the part of band set r's band in the last partial cycle
+    const int cycle = band_rows * n, full = H / cycle, rest = H - full * cycle;
+    const int tail = rest - r * band_rows;
+    return full * band_rows + (tail <= 0 ? 0 : (tail < band_rows ? tail : band_rows));
+}
+ART_HD int band_block_rows(int H, int band_rows, int n) {  // the largest band set (band set 0 owns the most rows)
+    return band_local_rows(H, band_rows, n, 0);
+}
+
 }  // namespace art

@@ -7,6 +7,7 @@
 // unpack kernel writes every row to its place in the frame.  The RCCL communicator (ncclCommInitAll) and the per-device
 // scene uploads are made once, when the MultiRenderer is built.
 #pragma once
+#include <cstddef>
 #include <cstdint>
 #include <vector>
 
@@ -28,9 +29,17 @@ public:
     // unpack + output copy).
     void render(const CameraRec<double>& cam, const RenderParams& p, uint8_t* out_rgb, bool out_device, RenderStats& stats);
     int ngpus() const;
+    size_t scene_bytes() const;  // scene bytes on each device
+    // Stats of device k (devices[k]) in the last render: its segments, its own kernel times and launches, its rows.
+    bool device_stats(int k, RenderStats& out) const;
 
 private:
     Impl* impl_;
 };
+
+// Places n packed band blocks (block r = band set r's band_block_rows(H, band_rows, n) rows in local order, padding
+// rows after its band_local_rows) into the H-row frame.  device: both pointers on the current device, a kernel on
+// `stream` (hipStream_t); else host memory, copied on the calling thread.
+void unpack_bands(const uint8_t* recv, uint8_t* frame, int W, int H, int band_rows, int n, bool device, void* stream);
 
 }  // namespace art

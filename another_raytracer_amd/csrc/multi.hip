@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstring>
 #include <exception>
 #include <memory>
 #include <stdexcept>
@@ -27,26 +28,47 @@ namespace art {
         if (r_ != ncclSuccess) throw std::runtime_error(std::string(#x) + ": " + ncclGetErrorString(r_)); \
     } while (0)
 
-// Global row of local row ly of band partition (band_rows, n, r): the rule of kernels.hip global_row / rt_local_rows.
-__host__ __device__ inline int band_global_row(int ly, int band_rows, int n, int r) {
-    return (ly / band_rows) * (band_rows * n) + r * band_rows + (ly % band_rows);
-}
-static int band_local_rows(int H, int band_rows, int n, int r) {
-    int rows = 0;
-    while (band_global_row(rows, band_rows, n, r) < H) ++rows;
-    return rows;
-}
-
-// recv holds n packed blocks of max_rows rows (block r = device r's rows in local order); one block per (r, ly).
+// recv holds n packed blocks of max_rows rows (block r = band set r's rows in local order, padding rows after them);
+// one block of threads per (r, ly).  Rows whose byte count and both addresses are 16-B aligned move as uint4.
 __global__ void k_unpack_bands(const uint8_t* __restrict__ recv, uint8_t* __restrict__ frame, int W, int H, int band_rows, int n,
-                               int max_rows) {
+                               int max_rows, int wide) {
     const int r = static_cast<int>(blockIdx.x) / max_rows, ly = static_cast<int>(blockIdx.x) % max_rows;
     const int gy = band_global_row(ly, band_rows, n, r);
-    if (gy >= H) return;  // padding rows of a shorter band
+    if (gy >= H) return;  // padding rows of a shorter band set
     const size_t row_bytes = static_cast<size_t>(W) * 3;
     const uint8_t* src = recv + (static_cast<size_t>(r) * max_rows + ly) * row_bytes;
     uint8_t* dst = frame + static_cast<size_t>(gy) * row_bytes;
-    for (size_t i = threadIdx.x; i < row_bytes; i += blockDim.x) dst[i] = src[i];
+    if (wide) {
+        const uint4* s4 = reinterpret_cast<const uint4*>(src);
+        uint4* d4 = reinterpret_cast<uint4*>(dst);
+        for (size_t i = threadIdx.x; i < row_bytes / 16; i += blockDim.x) d4[i] = s4[i];
+    } else {
+        for (size_t i = threadIdx.x; i < row_bytes; i += blockDim.x) dst[i] = src[i];
+    }
+}
+
+static void launch_unpack(const uint8_t* recv, uint8_t* frame, int W, int H, int band_rows, int n, int max_rows, hipStream_t stream) {
+    if (max_rows <= 0) return;
+    const size_t row_bytes = static_cast<size_t>(W) * 3;
+    const int wide = (row_bytes % 16 == 0 && reinterpret_cast<uintptr_t>(recv) % 16 == 0 && reinterpret_cast<uintptr_t>(frame) % 16 == 0);
+    hipLaunchKernelGGL(k_unpack_bands, dim3(static_cast<unsigned>(n * max_rows)), dim3(256), 0, stream, recv, frame, W, H, band_rows, n,
+                       max_rows, wide);
+    HIP_CHECK(hipGetLastError());
+}
+
+void unpack_bands(const uint8_t* recv, uint8_t* frame, int W, int H, int band_rows, int n, bool device, void* stream) {
+    if (W < 1 || H < 1 || band_rows < 1 || n < 1) throw std::invalid_argument("unpack_bands: W, H, band_rows, n must be >= 1");
+    const int max_rows = band_block_rows(H, band_rows, n);
+    if (device) {
+        launch_unpack(recv, frame, W, H, band_rows, n, max_rows, static_cast<hipStream_t>(stream));
+        return;
+    }
+    const size_t row_bytes = static_cast<size_t>(W) * 3;
+    for (int r = 0; r < n; ++r)
+        for (int ly = 0; ly < max_rows; ++ly) {
+            const int gy = band_global_row(ly, band_rows, n, r);
+            if (gy < H) std::memcpy(frame + static_cast<size_t>(gy) * row_bytes, recv + (static_cast<size_t>(r) * max_rows + ly) * row_bytes, row_bytes);
+        }
 }
 
 struct DeviceBuf {
@@ -84,6 +106,7 @@ struct MultiRenderer::Impl {
     std::vector<hipStream_t> streams;                  // gather / unpack streams, one per device
     std::vector<DeviceBuf> send;                       // packed local rows, one per device
     DeviceBuf recv, frame;                             // on devices[0]
+    std::vector<RenderStats> last;                     // per-device stats of the last render
 
     ~Impl() {
         for (auto c : comms)
@@ -127,13 +150,18 @@ MultiRenderer::MultiRenderer(const FlatScene& flat, const std::vector<int>& devi
 
 MultiRenderer::~MultiRenderer() { delete impl_; }
 int MultiRenderer::ngpus() const { return static_cast<int>(impl_->devices.size()); }
+size_t MultiRenderer::scene_bytes() const { return impl_->renderers.empty() ? 0 : impl_->renderers[0]->scene_bytes(); }
+bool MultiRenderer::device_stats(int k, RenderStats& out) const {
+    if (k < 0 || k >= static_cast<int>(impl_->last.size())) return false;
+    out = impl_->last[k];
+    return true;
+}
 
 void MultiRenderer::render(const CameraRec<double>& cam, const RenderParams& p, uint8_t* out_rgb, bool out_device, RenderStats& stats) {
     Impl& I = *impl_;
     const int n = static_cast<int>(I.devices.size());
     const int W = p.width, H = p.height, band_rows = std::max(1, p.band_rows);
-    int max_rows = 0;
-    for (int r = 0; r < n; ++r) max_rows = std::max(max_rows, band_local_rows(H, band_rows, n, r));
+    const int max_rows = band_block_rows(H, band_rows, n);
     const size_t row_bytes = static_cast<size_t>(W) * 3, block = static_cast<size_t>(max_rows) * row_bytes;
     for (int k = 0; k < n; ++k) I.send[k].ensure(std::max<size_t>(block, 1));
     I.recv.ensure(std::max<size_t>(block * n, 1));
@@ -171,10 +199,7 @@ void MultiRenderer::render(const CameraRec<double>& cam, const RenderParams& p, 
     // phase 3: the root places every row and hands the frame over
     HIP_CHECK(hipSetDevice(I.devices[0]));
     uint8_t* dst = out_device ? out_rgb : static_cast<uint8_t*>(I.frame.p);
-    if (max_rows > 0)
-        hipLaunchKernelGGL(k_unpack_bands, dim3(static_cast<unsigned>(n * max_rows)), dim3(256), 0, I.streams[0],
-                           static_cast<const uint8_t*>(I.recv.p), dst, W, H, band_rows, n, max_rows);
-    HIP_CHECK(hipGetLastError());
+    launch_unpack(static_cast<const uint8_t*>(I.recv.p), dst, W, H, band_rows, n, max_rows, I.streams[0]);
     if (!out_device) HIP_CHECK(hipMemcpyAsync(out_rgb, I.frame.p, row_bytes * H, hipMemcpyDeviceToHost, I.streams[0]));
     for (int k = 0; k < n; ++k) {
         HIP_CHECK(hipSetDevice(I.devices[k]));
@@ -182,6 +207,7 @@ void MultiRenderer::render(const CameraRec<double>& cam, const RenderParams& p, 
     }
     const auto t1 = std::chrono::steady_clock::now();
 
+    I.last = st;
     stats = RenderStats{};
     for (int k = 0; k < n; ++k) {
         stats.segments += st[k].segments;

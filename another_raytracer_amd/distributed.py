@@ -1,6 +1,8 @@
 """Multi-GPU frame rendering, two drivers of the same partition (row-interleaved bands, one RCCL gather):
 
-* one process per GPU (torch.distributed over RCCL; bench.py under torchrun): render_frame / gather_frame below;
+* one process per GPU (torch.distributed over RCCL; bench.py under torchrun): frame_renderer / gather_frame below --
+  each rank renders its bands into its padded gather block, one dist.gather moves the blocks, and libart's
+  rt_unpack_bands places the rows (the same layout and unpack kernel as rt_render_multi);
 * one process, one host thread per GPU, RCCL inside libart (rt_render_multi, include/art.h): multi_engine below.
 
 
@@ -17,7 +19,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from ._lib import RT_OUT_DEVICE, check, lib, rt_params, rt_stats
+from ._lib import RT_OUT_DEVICE, RT_PROFILE, check, lib, rt_params, rt_stats
 
 DEFAULT_BAND_ROWS = 8
 
@@ -33,43 +35,85 @@ def band_rows_of(height, band_rows, band_count, band_index):
     return list(rows[:n])
 
 
-def gather_frame(local, height, band_rows, group=None, dst=0):
-    """Gather each rank's packed rows (tensor [rows_r, W, C]) to `dst` and place them; returns the [H, W, C] frame on
-    dst (None elsewhere).  Blocks are padded to the largest band so the collective moves equal-sized buffers."""
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
-    width, chans = local.shape[1], local.shape[2]
-    max_rows = max(len(band_rows_of(height, band_rows, world, r)) for r in range(world))
-    send = torch.zeros((max_rows, width, chans), dtype=local.dtype, device=local.device)
-    send[: local.shape[0]] = local
-    if world == 1:
-        return local.clone()
-    gather_list = [torch.empty_like(send) for _ in range(world)] if rank == dst else None
-    dist.gather(send, gather_list, dst=dst, group=group)
-    if rank != dst:
-        return None
-    frame = torch.empty((height, width, chans), dtype=local.dtype, device=local.device)
-    for r in range(world):
-        rows = band_rows_of(height, band_rows, world, r)
-        if rows:
-            idx = torch.tensor(rows, device=local.device, dtype=torch.long)
-            frame.index_copy_(0, idx, gather_list[r][: len(rows)])
+def block_rows(height, band_rows, world):
+    """Rows of every rank's gather block: the largest band set's row count (libart's rt_band_block_rows)."""
+    return check(lib.rt_band_block_rows(int(height), int(band_rows), int(world)), "rt_band_block_rows")
+
+
+def unpack_bands(packed, frame, height, band_rows, world, stream=None):
+    """Places `world` concatenated band blocks (packed: [world * block_rows, W, 3] uint8) into frame [H, W, 3]: libart's
+    rt_unpack_bands, the same code rt_render_multi runs after its ncclGather (a kernel on the tensors' device, on
+    `stream` or torch's current stream; numpy arrays are unpacked on the host)."""
+    width = int(frame.shape[1])
+    if isinstance(packed, torch.Tensor):
+        assert packed.is_contiguous() and frame.is_contiguous() and packed.dtype == torch.uint8 and frame.dtype == torch.uint8
+        if packed.is_cuda:
+            assert frame.is_cuda and frame.device == packed.device, "packed and frame must be on one device"
+            st = stream if stream is not None else torch.cuda.current_stream(packed.device).cuda_stream
+            check(lib.rt_unpack_bands(ctypes.c_void_p(packed.data_ptr()), ctypes.c_void_p(frame.data_ptr()), width, int(height),
+                                      int(band_rows), int(world), RT_OUT_DEVICE, ctypes.c_void_p(st)), "rt_unpack_bands")
+            return frame
+        packed, frame_np = packed.numpy(), frame.numpy()
+    else:
+        frame_np = frame
+    assert packed.flags.c_contiguous and frame_np.flags.c_contiguous
+    check(lib.rt_unpack_bands(packed.ctypes.data_as(ctypes.c_void_p), frame_np.ctypes.data_as(ctypes.c_void_p), width, int(height),
+                              int(band_rows), int(world), 0, None), "rt_unpack_bands")
     return frame
 
 
-def render_frame(eng, band_rows=DEFAULT_BAND_ROWS, group=None, dst=0, device=None, profile=False, out_local=None):
+def gather_frame(send, height, band_rows, group=None, dst=0, recv=None, frame=None):
+    """Gathers every rank's padded block `send` ([block_rows, W, C]: its band rows first, as rendered in place by
+    render_frame) to `dst` with one collective (RCCL on GPUs, gloo on CPU), then places the rows with rt_unpack_bands.
+    Returns the [H, W, C] frame on dst (None elsewhere)."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    if rank != dst:
+        dist.gather(send, None, dst=dst, group=group)
+        return None
+    width, chans = send.shape[1], send.shape[2]
+    if recv is None:
+        recv = torch.empty((world * send.shape[0], width, chans), dtype=send.dtype, device=send.device)
+    dist.gather(send, list(recv.chunk(world)), dst=dst, group=group)  # views of one contiguous buffer
+    if frame is None:
+        frame = torch.empty((height, width, chans), dtype=send.dtype, device=send.device)
+    return unpack_bands(recv, frame, height, band_rows, world)
+
+
+class frame_renderer:
+    """One rank's share of a multi-process frame (one process per GPU): renders its bands straight into its padded
+    gather block and gathers on `dst` (the buffers are allocated once, so a step allocates nothing)."""
+
+    def __init__(self, eng, band_rows=DEFAULT_BAND_ROWS, group=None, dst=0, device=None):
+        self.eng, self.band_rows, self.group, self.dst = eng, int(band_rows), group, dst
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.rows = band_rows_of(eng.height, self.band_rows, self.world, self.rank)
+        self.block = block_rows(eng.height, self.band_rows, self.world)
+        self.send = torch.zeros((self.block, eng.width, 3), dtype=torch.uint8, device=self.device)
+        self.recv = self.frame = None
+        if self.world > 1 and self.rank == dst:
+            self.recv = torch.empty((self.world * self.block, eng.width, 3), dtype=torch.uint8, device=self.device)
+            self.frame = torch.empty((eng.height, eng.width, 3), dtype=torch.uint8, device=self.device)
+
+    def __call__(self, profile=False):
+        """Returns (frame on dst / None elsewhere, this rank's render stats)."""
+        if self.rows:
+            self.eng.run(self.send[: len(self.rows)], band_rows=self.band_rows, band_count=self.world, band_index=self.rank,
+                         profile=profile)
+            stats = dict(self.eng.stats)
+        else:
+            stats = {"segments": 0, "primary": 0, "ms": 0.0, "extend_ms": 0.0, "shade_ms": 0.0, "extend_launches": 0,
+                     "shade_launches": 0, "passes": 0, "samples_per_pass": 0, "local_rows": 0, "extend_variant": -1}
+        if self.world == 1:
+            return self.send, stats
+        return gather_frame(self.send, self.eng.height, self.band_rows, self.group, self.dst, self.recv, self.frame), stats
+
+
+def render_frame(eng, band_rows=DEFAULT_BAND_ROWS, group=None, dst=0, device=None, profile=False):
     """Renders `eng`'s frame across all ranks of `group` and gathers it on `dst`.  Returns (frame_or_None, stats)."""
-    world = dist.get_world_size(group) if dist.is_initialized() else 1
-    rank = dist.get_rank(group) if dist.is_initialized() else 0
-    rows = band_rows_of(eng.height, band_rows, world, rank)
-    dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
-    local = out_local if out_local is not None else torch.empty((len(rows), eng.width, 3), dtype=torch.uint8, device=dev)
-    if rows:
-        eng.run(local, band_rows=band_rows, band_count=world, band_index=rank, profile=profile)
-    stats = dict(eng.stats)
-    if world == 1:
-        return local, stats
-    return gather_frame(local, eng.height, band_rows, group=group, dst=dst), stats
+    return frame_renderer(eng, band_rows, group, dst, device)(profile=profile)
 
 
 class multi_engine:
@@ -94,12 +138,22 @@ class multi_engine:
             for o in scene.objects:
                 check(lib.rt_graph_add_world(g, o.id), "rt_graph_add_world")
             check(lib.rt_multi_from_graph(g, devs, len(self.devices), ctypes.byref(self._m)), "rt_multi_from_graph")
-        self.background = tuple(background) if background is not None else (0.0, 0.0, 0.0)
+        from ._lib import rt_scene_info
+        info = rt_scene_info()
+        check(lib.rt_multi_scene_info(self._m, ctypes.byref(info)), "rt_multi_scene_info")
+        self.info = {f: (tuple(getattr(info, f)) if isinstance(getattr(info, f), ctypes.Array) else getattr(info, f))
+                     for f, _ in info._fields_}
+        # engine::set_scene(world, background) (engine.h:24-28): a builtin scene's own background unless overridden
+        self.background = tuple(background) if background is not None else (
+            tuple(info.background) if isinstance(scene, str) else (0.0, 0.0, 0.0))
         self.stats = {}
 
-    def run(self, out):
-        """Renders the whole frame into `out` (uint8 H x W x 3: numpy, or a torch tensor on devices[0]); returns ms."""
+    def run(self, out, profile=False):
+        """Renders the whole frame into `out` (uint8 H x W x 3: numpy, or a torch tensor on devices[0]); returns ms.
+        profile: time every path-kernel launch with HIP events (stats extend_ms; per device in device_stats)."""
         from .engine import _pointer
+        if isinstance(out, torch.Tensor) and out.is_cuda and out.device.index != self.devices[0]:
+            raise ValueError(f"a device output must live on devices[0] = cuda:{self.devices[0]}, not {out.device}")
         p = rt_params()
         p.width, p.height, p.spp, p.max_depth, p.seed = self.width, self.height, self.samples_per_pixel, self.max_depth, self.seed
         p.band_rows, p.band_count, p.band_index = self.band_rows, 1, 0
@@ -108,11 +162,22 @@ class multi_engine:
         ptr, dev = _pointer(out, self.width * self.height * 3)
         if dev:
             p.flags |= RT_OUT_DEVICE
+        if profile:
+            p.flags |= RT_PROFILE
         st = rt_stats()
         check(lib.rt_render_multi(self._m, ctypes.byref(self.cam.c), ctypes.byref(p), ctypes.c_void_p(ptr), ctypes.byref(st)),
               "rt_render_multi")
         self.stats = st.as_dict()
         return st.ms
+
+    def device_stats(self):
+        """Per-device stats of the last run (devices[k] at index k): segments, kernel time, rows."""
+        out = []
+        for k in range(len(self.devices)):
+            st = rt_stats()
+            check(lib.rt_multi_device_stats(self._m, k, ctypes.byref(st)), "rt_multi_device_stats")
+            out.append(st.as_dict())
+        return out
 
     def __del__(self):
         if getattr(self, "_m", None) and self._m.value and lib is not None:

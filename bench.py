@@ -1,27 +1,34 @@
 """Benchmark: Msamples/s (primary + secondary rays) of the HIP path on BASELINE.json's headline workload.
 
     python bench.py [--gpus N --steps K --warmup W] [--scene 1 --width 1920 --height 1080 --spp 1024]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...     (one process per GPU)
 
-One step = one full frame of configs[1] ("'One Weekend' final random-spheres scene, 1920x1080, 1024 spp"): every
-rank renders its row-interleaved bands (another_raytracer_amd/distributed.py) and rank 0 gathers the RGB8 frame over
-RCCL.  The total work per step is fixed as N grows ("scaling": "strong"); value = all segments traced by all ranks /
-max-over-ranks wall time of the K timed steps.  A segment is one ray traced through the world (one world.hit call of
-engine.h:453), counted exactly on the device from the wavefront queue sizes.
+One step = one full frame of configs[1] ("'One Weekend' final random-spheres scene, 1920x1080, 1024 spp"), split into
+row-interleaved bands (8 rows; band b on GPU b mod N) and gathered as RGB8 on GPU 0.  Two drivers of that partition:
+  * plain `python bench.py --gpus N` (the default, N = 1): this process drives GPUs 0..N-1 through the C ABI,
+    rt_render_multi (csrc/multi.hip: one host thread and one RCCL rank per GPU, ncclGather of the packed band blocks to
+    GPU 0 + an unpack kernel).  Fewer than N visible GPUs is an error, never a silent 1-GPU run.
+  * under torchrun (WORLD_SIZE = N ranks; --gpus must equal it): one process per GPU, each renders its bands into its
+    padded block, dist.gather over RCCL to rank 0, libart's rt_unpack_bands places the rows (the same layout and unpack
+    kernel).
+The total work per step is fixed as N grows ("scaling": "strong"); value = all segments traced on all GPUs / wall time
+of the K timed steps (max over ranks under torchrun), gather and unpack included.  A segment is one ray traced through
+the world (one world.hit call of engine.h:453), counted exactly on the device.
+C5 (BASELINE configs[4]): python bench.py --gpus 8 --scene dino --width 4096 --height 4096 --spp 8192 --steps 1 --warmup 0
 
 Extra fields:
-  roofline      dominant kernel (k_paths / k_paths_g, or k_extend for the per-depth variants), timed live with HIP events
-                on the render stream during the timed steps.  The persistent path kernels are VALU-issue / divergence
-                bound: bound "valu", achieved = VALU lane-instruction slots issued per second (the newest
-                committed PMC summary's wave-instructions per segment x 64 x this run's segments / kernel time), peak
-                78.6 T/s (2 cycles per wave-instruction per SIMD at 2.4 GHz), lane_util from the same summary; the
-                SURVEY.md §8(d) HBM figure (128 B per segment + 12 B per pixel + the flat scene once per launch, vs
-                8 TB/s) sits under `hbm`.  Without a PMC summary for the scene/variant the HBM figure is the roofline.
-                `traffic` = FETCH_SIZE*2 + WRITE_SIZE per segment from the committed rocprofv3 PMC summary
-                (profiles/, MI355X_MICROARCH.md "HBM") scaled to this run, or null.
+  roofline      the dominant kernel (k_paths / k_paths_g) on the slowest GPU, each launch timed live with HIP events on
+                its render stream during the timed steps.  bound "hbm": achieved = SURVEY.md §8(d) algorithmic bytes per
+                launch (128 B per segment + 12 B per pixel + the flat scene) / average launch time, vs 8 TB/s; `traffic`
+                = measured HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE per segment, MI355X_MICROARCH.md "HBM")
+                from the committed PMC summary (profiles/*pmc*.json) stamped with this library's device-code build id,
+                else null.  The kernels' actual limiter, VALU issue and lane divergence, is under `valu`
+                from the same build-matched summary: VALU lane-slots issued per second vs 78.6 T/s, lane_util,
+                useful_frac.
   cpu_baseline  the reference itself (oracle/_ref/ref_harness = /root/reference/src compiled unmodified), its own
                 CPU-parallel mode (engine.h:335-376: 4 row stripes, 4 threads, shared global RNG) on a bounded sample
-                of the same workload (same scene, full 1920x1080, reduced spp), median of 3 runs, rank 0 at N=1 only;
-                plus `all_cores`: the oracle's restatement on every host thread the job may use (median of 3).
+                of the same workload (same scene, full 1920x1080, reduced spp), median and spread of 5 runs, N = 1 only;
+                plus `all_cores`: the oracle's restatement on every host thread the job may use (median of 5).
 """
 import argparse
 import glob
@@ -69,7 +76,7 @@ def survey_algorithmic_bytes(segments, pixels, scene_bytes):
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="GPUs (default 1; under torchrun: WORLD_SIZE)")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--scene", default="1")
@@ -94,7 +101,7 @@ def _median(xs):
     return xs[len(xs) // 2]
 
 
-def cpu_baseline(args, repeats=3):
+def cpu_baseline(args, repeats=5):
     """Two CPU figures on the box's host cores, each the median of `repeats` bounded samples of the same workload
     (same scene, full width and height, reduced spp: the per-segment cost does not depend on spp):
       * the reference itself (oracle/_ref/ref_harness = /root/reference/src compiled unmodified by oracle/Makefile) in
@@ -124,7 +131,8 @@ def cpu_baseline(args, repeats=3):
            "sample": f"scene {args.scene} {args.width}x{args.height}x{args.cpu_baseline_spp}spp "
                      f"({last['segments']} segments, {last['ms'] / 1e3:.1f} s per run), median of {repeats} runs, "
                      f"engine_mode::parallel_stripes semantics (4 threads, shared global mt19937); per-segment cost is spp-independent",
-           "runs_Msamples_s": [round(x, 4) for x in runs], "cpu_model": model, "host_cpus": os.cpu_count()}
+           "runs_Msamples_s": [round(x, 4) for x in runs], "spread_Msamples_s": [round(min(runs), 4), round(max(runs), 4)],
+           "cpu_model": model, "host_cpus": os.cpu_count()}
     try:
         from tests.oracle_lib import oracle_render
         env = os.environ.get("OMP_NUM_THREADS", "")
@@ -145,48 +153,95 @@ def cpu_baseline(args, repeats=3):
     return res
 
 
-def latest_pmc(precision, scene, variant):
-    """The newest committed PMC summary (tools/pmc_summary.py format: per-segment wave-instruction counts of the
-    dominant kernel) for this scene and extend variant, or None."""
+def latest_pmc(precision, scene, variant, build):
+    """The newest committed PMC summary (tools/pmc_summary.py format) for this scene and kernel variant whose
+    `libart_build` stamp equals the loaded library's device code (another_raytracer_amd._lib.kernel_build_id), or None:
+    counters of another build never price this run."""
     best = None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):  # tags sort by round and letter
         try:
             d = json.load(open(path))
         except (OSError, ValueError):
             continue
-        k = d.get("dominant_kernel")
-        if (d.get("precision") == precision and str(d.get("scene")) == str(scene) and d.get("extend_variant") == variant and k
-                and (d.get("kernels", {}).get(k, {}).get("per_segment_wave_instructions"))):
+        if (d.get("precision") == precision and str(d.get("scene")) == str(scene) and d.get("extend_variant") == variant
+                and d.get("libart_build") == build):
             d["_file"] = os.path.relpath(path, ROOT)
             best = d
     return best
 
 
-def latest_traffic(precision, scene, variant):
-    """Per-segment HBM bytes of k_extend from the newest committed PMC summary (profiles/*pmc*.json) of this extend
-    variant, or None."""
-    best = None
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
-        try:
-            d = json.load(open(path))
-        except (OSError, ValueError):
-            continue
-        if (d.get("precision") == precision and str(d.get("scene")) == str(scene) and d.get("extend_bytes_per_segment")
-                and d.get("extend_variant", 1) == variant):
-            best = d
-    return best
+def choose_driver(gpus, world_env, device_count):
+    """How `bench.py --gpus N` runs: ("procs", N) under torchrun (one process per GPU, WORLD_SIZE = N ranks), else
+    ("multi", N): this one process drives N GPUs through the C ABI (rt_render_multi: one host thread and one RCCL rank
+    per device, ncclGather + unpack kernel on device 0).  Never silently fewer GPUs than asked: SystemExit instead."""
+    if world_env > 1:
+        if gpus is not None and gpus != world_env:
+            raise SystemExit(f"bench.py: --gpus {gpus} but torchrun started WORLD_SIZE={world_env} ranks")
+        return "procs", world_env
+    n = 1 if gpus is None else gpus
+    if n < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1 (got {n})")
+    if device_count < n:
+        raise SystemExit(f"bench.py: --gpus {n} needs {n} visible GPUs, found {device_count}: refusing to measure fewer")
+    return "multi", n
+
+
+def roofline_of(dev_stats, width, scene_bytes, variant, precision, scene, build):
+    """`roofline` of the dominant kernel on the slowest device (the one that sets the step time).  SURVEY.md §8(d)'s
+    contract: bound "hbm", achieved = algorithmic bytes per launch (128 B per segment + 12 B per pixel + the flat scene
+    once) / the kernel's average launch time measured live with HIP events on its stream; `traffic` = HBM bytes per
+    launch from the build-matched PMC summary (2 x FETCH_SIZE + WRITE_SIZE per segment x segments per launch), else null.
+    The kernel's real limiter -- VALU issue and lane divergence -- is under `valu` when a build-matched
+    PMC summary exists."""
+    slow = max(dev_stats, key=lambda d: d["extend_ms"])
+    launches = max(int(slow["extend_launches"]), 1)
+    per_launch_ms = slow["extend_ms"] / launches
+    segs = slow["segments"] / launches
+    pixels = slow["local_rows"] * width * slow["steps"] / launches
+    alg = survey_algorithmic_bytes(segs, pixels, scene_bytes)
+    achieved = alg / (per_launch_ms * 1e-3) / 1e9
+    kernel = {3: "k_paths", 4: "k_paths_g"}.get(variant, "k_extend")
+    moved = extend_moved_bytes(precision, variant, slow["segments"], slow["primary"])
+    pm = latest_pmc(precision, scene, variant, build)
+    tr = pm.get("extend_bytes_per_segment") if pm else None
+    roof = {"kernel": kernel, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": round(tr * segs) if tr else None,
+            "algorithmic_bytes_per_launch": round(alg),
+            "algorithmic_bytes": "SURVEY 8(d): 128 B/segment + 12 B/pixel + scene bytes, per launch of the slowest device",
+            "segments_per_launch": round(segs), "avg_launch_ms": round(per_launch_ms, 4), "launches": launches,
+            "devices": len(dev_stats), "extend_variant": variant, "libart_build": build,
+            "moved_bytes_per_segment": round(moved / max(slow["segments"], 1), 2)}
+    if pm and variant in (3, 4):
+        # VALU lane-instruction slots issued per second: the summary's wave-instructions per segment x 64 lanes x the
+        # segments of a launch / the launch time measured here; lane_util = the share of those slots doing work
+        k = pm.get("dominant_kernel")
+        ps = pm.get("kernels", {}).get(k, {}).get("per_segment_wave_instructions", {})
+        if ps.get("insts_valu"):
+            slots = ps["insts_valu"] * 64 * segs / (per_launch_ms * 1e-3) / 1e12
+            lu = pm.get("valu_lane_util", 0)
+            roof["valu"] = {"achieved": round(slots, 3), "peak": round(VALU_PEAK_TLANE, 2), "unit": "Tlane-inst/s",
+                            "frac": round(slots / VALU_PEAK_TLANE, 4), "lane_util": lu,
+                            "useful_frac": round(slots / VALU_PEAK_TLANE * lu, 4),
+                            "valu_wave_insts_per_segment": round(ps["insts_valu"], 2),
+                            "issue_util_calibrated": pm.get("valu_issue_util_calibrated"),
+                            "wave_frac_wait_waitcnt": pm.get("wave_frac_wait_waitcnt"),
+                            "wave_frac_wait_dependency": pm.get("wave_frac_wait_inst_dependency")}
+        roof["pmc_summary"] = pm["_file"]
+    return roof
 
 
 def main():
     args = parse()
-    import numpy as np
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    driver, n = choose_driver(args.gpus, world_env, torch.cuda.device_count())
     rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if driver == "procs":
+        local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        if local_rank >= torch.cuda.device_count():
+            raise SystemExit(f"bench.py: rank {rank} has LOCAL_RANK {local_rank} but only {torch.cuda.device_count()} GPUs are visible")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
@@ -195,114 +250,120 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
 
     import another_raytracer_amd as art
-    from another_raytracer_amd.distributed import band_rows_of, render_frame
+    from another_raytracer_amd._lib import kernel_build_id
+    from another_raytracer_amd.distributed import frame_renderer, multi_engine
 
-    world_scene = art.scene_manager(device=dev.index).build(args.scene)
-    scene_bytes = int(world_scene.info["device_bytes_f64"])
-    cam = art.camera(world_scene.lookfrom, world_scene.lookat, (0, 1, 0), world_scene.vfov, args.width / args.height,
-                     world_scene.aperture, 10.0, 0.0, 1.0)
-    eng = art.engine(cam, art.engine_mode.parallel_stripes, width=args.width, height=args.height,
-                     samples_per_pixel=args.spp, max_depth=args.max_depth, device=dev.index, precision=args.precision,
-                     samples_per_pass=args.samples_per_pass)
-    eng.set_scene(world_scene.objects, world_scene.background)
-    eng.global_scene = args.global_scene
-    eng.split_shade = args.split_shade
-    eng.wavefront = args.wavefront
-    rows = band_rows_of(args.height, args.band_rows, world, rank)
-    local = torch.empty((len(rows), args.width, 3), dtype=torch.uint8, device=dev)
+    build = kernel_build_id()
     profile = not args.no_profile
+    if driver == "multi":
+        if args.global_scene or args.split_shade or args.wavefront or args.samples_per_pass:
+            raise SystemExit("bench.py: --global-scene / --split-shade / --wavefront / --samples-per-pass are one-process-per-GPU "
+                             "A/B switches (run them under torchrun)")
+        devices = list(range(n))
+        probe = art.scene_manager(device=0).build(args.scene)  # the scene_manager view (camera placement)
+        cam = art.camera(probe.lookfrom, probe.lookat, (0, 1, 0), probe.vfov, args.width / args.height, probe.aperture, 10.0, 0.0, 1.0)
+        del probe
+        eng = multi_engine(args.scene, devices, cam, args.width, args.height, args.spp, max_depth=args.max_depth,
+                           band_rows=args.band_rows)
+        scene_bytes = int(eng.info["device_bytes_f64"])
+        frame = torch.empty((args.height, args.width, 3), dtype=torch.uint8, device=dev)
 
-    def step():
-        return render_frame(eng, band_rows=args.band_rows, device=dev, profile=profile, out_local=local)
+        def step():
+            eng.run(frame, profile=profile)
+            return eng.stats, eng.device_stats()
+
+        def sync():
+            for d in devices:
+                torch.cuda.synchronize(d)
+        parallelism = (f"1 GPU, rt_render_multi (row-bands({args.band_rows}), single-rank gather + unpack)" if n == 1 else
+                       f"row-bands({args.band_rows}) over {n} GPUs, one process: rt_render_multi (one host thread + RCCL rank "
+                       f"per GPU, ncclGather to GPU 0 + unpack kernel)")
+    else:
+        world_scene = art.scene_manager(device=dev.index).build(args.scene)
+        scene_bytes = int(world_scene.info["device_bytes_f64"])
+        cam = art.camera(world_scene.lookfrom, world_scene.lookat, (0, 1, 0), world_scene.vfov, args.width / args.height,
+                         world_scene.aperture, 10.0, 0.0, 1.0)
+        eng = art.engine(cam, art.engine_mode.parallel_stripes, width=args.width, height=args.height,
+                         samples_per_pixel=args.spp, max_depth=args.max_depth, device=dev.index, precision=args.precision,
+                         samples_per_pass=args.samples_per_pass)
+        eng.set_scene(world_scene.objects, world_scene.background)
+        eng.global_scene = args.global_scene
+        eng.split_shade = args.split_shade
+        eng.wavefront = args.wavefront
+        fr = frame_renderer(eng, band_rows=args.band_rows, device=dev)
+
+        def step():
+            _, st = fr(profile=profile)
+            return st, [st]
+
+        def sync():
+            torch.cuda.synchronize(dev)
+        parallelism = (f"row-bands({args.band_rows}) over {n} GPUs, one process per GPU (torchrun): dist.gather over RCCL "
+                       f"to rank 0 + rt_unpack_bands")
 
     for _ in range(args.warmup):
         step()
-    if world > 1:
+    if driver == "procs":
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
-    segs = 0
-    ext_ms = shade_ms = gpu_ms = 0.0
-    ext_launches = 0
-    primary_segs = 0
-    variant = 0
-    frame = None
+    segs = primary_segs = 0
+    variant = -1
+    acc = None  # per-device totals over the timed steps
     for _ in range(args.steps):
-        frame, st = step()
+        st, per_dev = step()
         segs += st["segments"]
-        ext_ms += st["extend_ms"]
-        shade_ms += st["shade_ms"]
-        gpu_ms += st["ms"]
-        ext_launches += st["extend_launches"]
         primary_segs += st["primary"]
-        variant = st["extend_variant"]
-    torch.cuda.synchronize()
-    if world > 1:
+        variant = max(variant, st["extend_variant"])
+        if acc is None:
+            acc = [{"segments": 0, "primary": 0, "extend_ms": 0.0, "extend_launches": 0, "local_rows": d["local_rows"], "steps": 0}
+                   for d in per_dev]
+        for a, d in zip(acc, per_dev):
+            a["segments"] += d["segments"]
+            a["primary"] += d["primary"]
+            a["extend_ms"] += d["extend_ms"]
+            a["extend_launches"] += d["extend_launches"]
+            a["steps"] += 1
+    sync()
+    if driver == "procs":
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    stats = torch.tensor([elapsed, float(segs), ext_ms, shade_ms, float(ext_launches), float(primary_segs)],
-                         dtype=torch.float64, device=dev)
-    if world > 1:
-        t_max = stats[:1].clone()
-        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-        tot = stats[1:].clone()
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        elapsed = float(t_max.item())
-        segs, ext_ms, shade_ms, ext_launches, primary_segs = (float(x) for x in tot.tolist())
+    if driver == "procs":
+        # max wall time over ranks; all ranks' segments; every rank's per-device totals for the roofline
+        mine = torch.tensor([elapsed, float(segs), float(primary_segs), float(variant), acc[0]["segments"], acc[0]["primary"],
+                             acc[0]["extend_ms"], acc[0]["extend_launches"], acc[0]["local_rows"], acc[0]["steps"]],
+                            dtype=torch.float64, device=dev)
+        allr = [torch.empty_like(mine) for _ in range(n)]
+        dist.all_gather(allr, mine)
+        rows = [t.tolist() for t in allr]
+        elapsed = max(r[0] for r in rows)
+        segs = sum(r[1] for r in rows)
+        primary_segs = sum(r[2] for r in rows)
+        variant = int(max(r[3] for r in rows))
+        acc = [{"segments": r[4], "primary": r[5], "extend_ms": r[6], "extend_launches": r[7], "local_rows": int(r[8]), "steps": int(r[9])}
+               for r in rows]
     if rank == 0:
         value = segs / elapsed / 1e6
         primary = args.width * args.height * args.spp * args.steps
         line = {
             "metric": "Msamples/sec (primary+secondary rays) at 1920x1080x1024spp; 1/2/4/8 GPU",
-            "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
+            "value": round(value, 3), "unit": "Msamples/s", "n_gpus": n, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": args.precision, "data": "synthetic",
             "config": {"workload": f"scene_alias {args.scene} ('One Weekend' final random spheres)" if args.scene == "1"
                        else f"scene {args.scene}", "width": args.width, "height": args.height, "spp": args.spp,
-                       "max_depth": args.max_depth, "parallelism": f"row-bands({args.band_rows}) x {world} + rccl gather",
+                       "max_depth": args.max_depth, "parallelism": parallelism, "driver": driver,
                        "segments_per_step": int(segs / args.steps), "primary_rays_per_step": primary // args.steps,
                        "mprimary_per_s": round(primary / elapsed / 1e6, 3)},
         }
-        if profile and ext_ms > 0:
-            launches = max(ext_launches, 1)
-            per_launch_ms = ext_ms / launches
-            pixels = args.width * args.height * args.steps
-            alg = survey_algorithmic_bytes(segs, pixels, scene_bytes * ext_launches)
-            achieved = alg / (ext_ms * 1e-3) / 1e9
-            moved = extend_moved_bytes(args.precision, variant, segs, primary_segs)
-            tr = latest_traffic(args.precision, args.scene, variant)
-            kernel = {3: "k_paths", 4: "k_paths_g"}.get(variant, "k_extend")
-            hbm = {"achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                   "algorithmic_bytes_per_launch": round(alg / launches),
-                   "algorithmic_bytes": "SURVEY 8(d): 128 B/segment + 12 B/pixel + scene bytes per launch",
-                   "moved_bytes_per_segment": round(moved / max(segs, 1), 2)}
-            roof = {"kernel": kernel, "traffic": (round(tr["extend_bytes_per_segment"] * segs / launches) if tr else None),
-                    "extend_variant": variant, "avg_launch_ms": round(per_launch_ms, 4), "launches": int(ext_launches),
-                    "extend_ms_total": round(ext_ms, 2), "shade_ms_total": round(shade_ms, 2)}
-            pm = latest_pmc(args.precision, args.scene, variant) if variant in (3, 4) else None
-            if pm:
-                # The persistent path kernels are bound by VALU issue and lane divergence, not HBM (the
-                # scene lives in LDS / L2, ~9-30 B of HBM per segment).  achieved = VALU lane-instruction slots issued
-                # per second: the PMC summary's wave-instructions per segment x 64 lanes x the segments of this run /
-                # the kernel time measured live; lane_util = the share of those slots doing work (SQ_THREAD_CYCLES_VALU)
-                ps = pm["kernels"][pm["dominant_kernel"]]["per_segment_wave_instructions"]
-                slots = ps["insts_valu"] * 64 * segs / (ext_ms * 1e-3) / 1e12
-                roof.update({"bound": "valu", "achieved": round(slots, 3), "peak": round(VALU_PEAK_TLANE, 2), "unit": "Tlane-inst/s",
-                             "frac": round(slots / VALU_PEAK_TLANE, 4),
-                             "valu_wave_insts_per_segment": round(ps["insts_valu"], 2),
-                             "lane_util": pm.get("valu_lane_util"), "useful_frac": round(slots / VALU_PEAK_TLANE * pm.get("valu_lane_util", 0), 4),
-                             "issue_util_calibrated_pmc": pm.get("valu_issue_util_calibrated"),
-                             "wave_frac_wait_waitcnt_pmc": pm.get("wave_frac_wait_waitcnt"),
-                             "wave_frac_wait_dependency_pmc": pm.get("wave_frac_wait_inst_dependency"),
-                             "pmc_summary": pm["_file"], "hbm": hbm})
-            else:
-                roof.update({"bound": "hbm", "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm["frac"]})
-                roof.update({k: v for k, v in hbm.items() if k not in roof})
-            line["roofline"] = roof
-        if world == 1 and not args.no_cpu_baseline:
+        if n > 1:
+            line["config"]["per_gpu_kernel_ms_per_step"] = [round(a["extend_ms"] / max(a["steps"], 1), 3) for a in acc]
+        if profile and acc and any(a["extend_ms"] > 0 for a in acc):
+            line["roofline"] = roofline_of(acc, args.width, scene_bytes, variant, args.precision, args.scene, build)
+        if n == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if driver == "procs":
         dist.destroy_process_group()
 
 

@@ -44,8 +44,10 @@ extern "C" {
 #endif
 
 /* ABI 2: rt_params.fp_mode 0 = RT_FP64 (the only arithmetic: the reference's IEEE double), rt_scene_info's f32 byte count
- * dropped, rt_multi_* (multi-GPU render over RCCL), rt_render_progressive, rt_scene_save / rt_scene_load, rt_image_load. */
-#define RT_ABI_VERSION 2
+ * dropped, rt_multi_* (multi-GPU render over RCCL), rt_render_progressive, rt_scene_save / rt_scene_load, rt_image_load.
+ * ABI 3 (additive): rt_band_block_rows, rt_unpack_bands (the gather layout for callers that move the bands themselves,
+ * e.g. one process per GPU over torch.distributed), rt_multi_ngpus, rt_multi_scene_info, rt_multi_device_stats. */
+#define RT_ABI_VERSION 3
 
 /* return codes */
 #define RT_OK 0
@@ -173,8 +175,19 @@ int rt_render_progressive(rt_scene* scene, const rt_camera* cam, const rt_params
  * NULL): n x 3 face normals as hit_record holds them (set_face_normal, hittable.h:18-22), 0 on a miss.  Ray i draws
  * its constant_medium uniforms from the PCG stream keyed (seed 0, pixel i, sample 0).  Host buffers; blocking. */
 int rt_trace_rays(rt_scene* scene, const double* rays, int64_t n, int32_t flags, double* t_out, double* normal_out);
-/* Number of rows a band partition owns, and optionally their global indices (rows_out may be NULL). */
+/* Number of rows a band partition owns, and optionally their global indices (rows_out may be NULL).  Global row y
+ * belongs to band set (y / band_rows) % band_count; local row ly of set r is global row
+ * (ly / band_rows) * band_rows * band_count + r * band_rows + ly % band_rows. */
 int rt_local_rows(const rt_params* params, int32_t* rows_out);
+/* Gather layout of an n-way band partition (what rt_render_multi's ncclGather moves): every band set sends one block of
+ * rt_band_block_rows(height, band_rows, n) rows (the largest set's row count; a shorter set pads after its rows).
+ * rt_unpack_bands places the n concatenated blocks (packed: n * block_rows * width * 3 bytes, block r = set r's rows in
+ * local order) into the height-row frame (row 0 = top): device pointers and a kernel on `stream` (hipStream_t, NULL =
+ * default) with RT_OUT_DEVICE, else host memory.  Replaces the reference's in-place stripe writes into one frame
+ * (engine.h:343-355). */
+int rt_band_block_rows(int32_t height, int32_t band_rows, int32_t n);
+int rt_unpack_bands(const uint8_t* packed, uint8_t* frame, int32_t width, int32_t height, int32_t band_rows, int32_t n, int32_t flags,
+                    void* stream);
 
 /* ---- images (imageio::load_image, imageio.cpp:11-15: stbi_load(path, &w, &h, &c, 0) of stb_image v2.27) ----
  * Decodes a JPEG (baseline or progressive) or PNG file to 8-bit samples, native channel count, row 0 = top, the bytes
@@ -199,6 +212,12 @@ int rt_multi_create(const char* name, const char* asset_dir, const int* devices,
 int rt_multi_from_graph(rt_graph* g, const int* devices, int ngpus, rt_multi** out);
 void rt_multi_destroy(rt_multi* m);
 int rt_render_multi(rt_multi* m, const rt_camera* cam, const rt_params* params, uint8_t* out_rgb8, rt_stats* stats);
+int rt_multi_ngpus(const rt_multi* m);
+/* The scene_manager view and sizes of the multi's scene (as rt_scene_info_get; device_bytes_f64 = bytes on each device). */
+int rt_multi_scene_info(const rt_multi* m, rt_scene_info* info);
+/* Stats of devices[k] alone in the last rt_render_multi: its segments, primaries, rows and (RT_PROFILE) its own kernel
+ * times and launches; ms = that device's render time (before the gather). */
+int rt_multi_device_stats(const rt_multi* m, int k, rt_stats* stats);
 
 /* ---- scene graph builder (one call per reference constructor; returns an id >= 0 or a negative code) ----
  * Scene-build randomness (noise textures' perlin tables, rt_graph_bvh's node draws) comes from the graph's own

@@ -10,7 +10,7 @@ import torch.distributed as dist
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import another_raytracer_amd as art  # noqa: E402
-from another_raytracer_amd.distributed import band_rows_of, gather_frame  # noqa: E402
+from another_raytracer_amd.distributed import band_rows_of, block_rows, gather_frame  # noqa: E402
 
 SCENE, W, H, SPP, BAND = "8", 96, 54, 4, 8
 
@@ -24,10 +24,10 @@ def main():
     eng = art.engine(cam, art.engine_mode.parallel_stripes, width=W, height=H, samples_per_pixel=SPP)
     eng.set_scene(w.objects, w.background)
     rows = band_rows_of(H, BAND, world, rank)
-    local = torch.zeros((len(rows), W, 3), dtype=torch.uint8, device="cuda:0")
+    send = torch.zeros((block_rows(H, BAND, world), W, 3), dtype=torch.uint8, device="cuda:0")  # padded gather block
     if rows:
-        eng.run(local, band_rows=BAND, band_count=world, band_index=rank)
-    frame = gather_frame(local.cpu(), H, BAND)
+        eng.run(send[: len(rows)], band_rows=BAND, band_count=world, band_index=rank)
+    frame = gather_frame(send.cpu(), H, BAND)
     if rank == 0:
         np.save(sys.argv[1], frame.numpy())
     dist.destroy_process_group()

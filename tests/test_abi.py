@@ -27,7 +27,7 @@ def test_every_declared_symbol_is_exported_and_bound():
     exported = set(re.findall(r" T (rt_\w+)", nm))
     assert set(decl) <= exported, set(decl) - exported
     assert set(decl) == set(_lib.SIGNATURES), set(decl) ^ set(_lib.SIGNATURES)
-    assert _lib.lib.rt_abi_version() == _lib.RT_ABI_VERSION == 2
+    assert _lib.lib.rt_abi_version() == _lib.RT_ABI_VERSION == 3
 
 
 def test_struct_layouts_match_the_header(tmp_path):

@@ -1,5 +1,6 @@
 """Multi-rank frame assembly (another_raytracer_amd/distributed.py) on CPU with gloo, world_size 2 and 3: the
-row-interleaved bands gathered to rank 0 rebuild the frame exactly.  The per-rank renders are the oracle's ORC_PCG
+row-interleaved bands, each rank's rows in its padded gather block, gathered to rank 0 and placed by libart's
+rt_unpack_bands (host path), rebuild the frame exactly.  The per-rank renders are the oracle's ORC_PCG
 rows (same PCG streams as the HIP path), so this also shows band renders are independent of the partition."""
 import os
 import socket
@@ -10,7 +11,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from another_raytracer_amd.distributed import band_rows_of, gather_frame
+from another_raytracer_amd.distributed import band_rows_of, block_rows, gather_frame
 
 W, H, SPP, BAND = 24, 37, 2, 4
 
@@ -29,8 +30,10 @@ def _worker(rank, world, port, q):
     from tests.oracle_lib import oracle_render
     rows = band_rows_of(H, BAND, world, rank)
     parts = [oracle_render("c1", W, H, SPP, mode="pcg", row0=r, nrows=1, threads=1)["rgb"] for r in rows]
-    local = torch.from_numpy(np.concatenate(parts) if parts else np.zeros((0, W, 3), np.uint8))
-    frame = gather_frame(local, H, BAND)
+    send = torch.zeros((block_rows(H, BAND, world), W, 3), dtype=torch.uint8)  # the padded gather block
+    if parts:
+        send[: len(rows)] = torch.from_numpy(np.concatenate(parts))
+    frame = gather_frame(send, H, BAND)
     if rank == 0:
         q.put(frame.numpy())
     dist.destroy_process_group()

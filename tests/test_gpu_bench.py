@@ -31,6 +31,11 @@ def test_bench_line_contract(gpu, scene, variant, kernel):
     assert c["segments_per_step"] >= c["primary_rays_per_step"]
     # value is the whole job's segments over the timed wall time
     assert d["value"] == pytest.approx(c["segments_per_step"] * d["steps"] / (d["ms_per_step"] * d["steps"] * 1e3), rel=2e-3)
+    assert c["driver"] == "multi" and "rt_render_multi" in c["parallelism"]
     r = d["roofline"]
-    assert r["kernel"] == kernel and r["extend_variant"] == variant and r["launches"] == 2
-    assert 0 < r["frac"] and r["peak"] > 0 and r["avg_launch_ms"] > 0
+    assert r["kernel"] == kernel and r["extend_variant"] == variant and r["launches"] == 2 and r["devices"] == 1
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0 and r["avg_launch_ms"] > 0
+    # achieved = the algorithmic bytes of one launch over its measured duration
+    assert r["achieved"] == pytest.approx(r["algorithmic_bytes_per_launch"] / (r["avg_launch_ms"] * 1e-3) / 1e9, rel=1e-3)
+    assert r["frac"] == pytest.approx(r["achieved"] / r["peak"], rel=1e-3)
+    assert r["segments_per_launch"] == c["segments_per_step"]

@@ -51,3 +51,51 @@ def test_corrupt_files_fail_loudly(tmp_path):
         p.write_bytes(blob)
         with pytest.raises(RTError):
             load_image(p)
+
+
+def _png(chunks):
+    import struct
+    import zlib
+    out = b"\x89PNG\r\n\x1a\n"
+    for typ, data in chunks:
+        out += struct.pack(">I", len(data)) + typ + data + struct.pack(">I", zlib.crc32(typ + data) & 0xFFFFFFFF)
+    return out
+
+
+def _rgb_png_chunks(ctype=2, extra=()):
+    import struct
+    import zlib
+    chans = {0: 1, 2: 3}[ctype]
+    raw = b"".join(b"\x00" + bytes(range(2 * chans)) for _ in range(2))  # 2x2, filter 0
+    return [(b"IHDR", struct.pack(">IIBBBBB", 2, 2, 8, ctype, 0, 0, 0)), *extra, (b"IDAT", zlib.compress(raw))]
+
+
+def test_truncated_and_malformed_png_chunks_are_refused(tmp_path):
+    # a chunk header with fewer than 12 bytes left (8..11) must not pass the length check, and a tRNS colour
+    # key shorter than one 16-bit sample per channel must not be read past its end (stb_image: "bad tRNS len")
+    import struct
+    from another_raytracer_amd._lib import RTError
+    ok = _png(_rgb_png_chunks() + [(b"IEND", b"")])
+    p = tmp_path / "ok.png"
+    p.write_bytes(ok)
+    assert load_image(p).shape == (2, 2, 3)
+    body = _png(_rgb_png_chunks())
+    cases = {
+        "trailing_header_8": body + struct.pack(">I", 4) + b"IDAT",
+        "trailing_header_10": body + struct.pack(">I", 4) + b"IDAT" + b"\x00\x00",
+        "trailing_header_11": body + struct.pack(">I", 0) + b"tEXt" + b"\x00\x00\x00",
+        "huge_len": body + struct.pack(">I", 0xFFFFFFF0) + b"IDAT" + b"\x00" * 16,
+        "rgb_trns_1_byte": _png(_rgb_png_chunks(2, [(b"tRNS", b"\x05")]) + [(b"IEND", b"")]),
+        "rgb_trns_5_bytes": _png(_rgb_png_chunks(2, [(b"tRNS", b"\x00\x01\x00\x02\x00")]) + [(b"IEND", b"")]),
+        "gray_trns_1_byte": _png(_rgb_png_chunks(0, [(b"tRNS", b"\x01")]) + [(b"IEND", b"")]),
+    }
+    for name, blob in cases.items():
+        p = tmp_path / f"{name}.png"
+        p.write_bytes(blob)
+        with pytest.raises(RTError):
+            load_image(p)
+    # a well-formed key is accepted: gray + tRNS -> gray + alpha
+    p = tmp_path / "gray_key.png"
+    p.write_bytes(_png(_rgb_png_chunks(0, [(b"tRNS", b"\x00\x01")]) + [(b"IEND", b"")]))
+    a = load_image(p)
+    assert a.shape == (2, 2, 2) and list(a[:, :, 1].reshape(-1)) == [255, 0, 255, 0]

@@ -52,3 +52,79 @@ def test_damaged_files_are_refused(tmp_path):
         assert e.value.code == -2, why
     with pytest.raises(art.RTError):
         art.scene_manager().load(tmp_path / "missing.artscene")
+
+
+class _Header(__import__("ctypes").Structure):
+    """csrc/scenefile.cpp FileHeader (13 arrays: spheres, tris, rects, boxes, primrefs, nodes, objs, world, mats, texs,
+    perlins, images, texels)."""
+    import ctypes as _c
+    _fields_ = [("magic", _c.c_char * 8), ("version", _c.c_uint32), ("header_bytes", _c.c_uint32), ("record_bytes", _c.c_uint32 * 13),
+                ("features", _c.c_uint32), ("has_media", _c.c_int32), ("max_bvh_depth", _c.c_int32), ("max_stack", _c.c_int32),
+                ("background", _c.c_double * 3), ("lookfrom", _c.c_double * 3), ("lookat", _c.c_double * 3), ("vfov", _c.c_double),
+                ("aperture", _c.c_double), ("offset", _c.c_uint64 * 13), ("count", _c.c_uint64 * 13), ("payload_bytes", _c.c_uint64),
+                ("checksum", _c.c_uint64)]
+
+
+def _fnv1a(data):
+    h = 1469598103934665603
+    for b in data:
+        h = ((h ^ b) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def test_tampered_header_and_payload_are_refused(tmp_path):
+    # ADVICE r2: the header is outside the checksum, so its array table must not wrap and its derived fields
+    # (max_stack sizes the LDS traversal stacks) must equal what the arrays imply; a payload whose indices point
+    # outside the arrays is refused even when its checksum is right
+    import ctypes
+    w = art.scene_manager().build("1")
+    p = tmp_path / "s.artscene"
+    art.save_scene(w, p)
+    blob = bytes(p.read_bytes())
+    hsz = ctypes.sizeof(_Header)
+    h0 = _Header.from_buffer_copy(blob[:hsz])
+    assert h0.header_bytes == hsz and h0.magic == b"ARTSCN"
+    start = (hsz + 63) // 64 * 64
+    assert art.scene_manager().load(p) is not None
+
+    def with_header(**kw):
+        h = _Header.from_buffer_copy(blob[:hsz])
+        for k, v in kw.items():
+            if isinstance(v, tuple):
+                getattr(h, k)[v[0]] = v[1]
+            else:
+                setattr(h, k, v)
+        return bytes(h) + blob[hsz:]
+
+    def with_payload(edit):
+        h = _Header.from_buffer_copy(blob[:hsz])
+        pay = bytearray(blob[start:])
+        edit(h, pay)
+        h.checksum = _fnv1a(pay)
+        return bytes(h) + blob[hsz:start] + bytes(pay)
+
+    def prim0_out_of_range(h, pay):
+        off = h.offset[4] - start
+        pay[off:off + 4] = (h.count[0] + 5).to_bytes(4, "little")  # sphere index past the spheres
+
+    def child_to_parent(h, pay):
+        off = h.offset[5] - start + 96  # node 0's child[0] (BvhNode: 6 x float4 planes, then int32 child[4])
+        pay[off:off + 4] = (0).to_bytes(4, "little")  # node 0 -> node 0: a cycle the GPU would walk forever
+
+    cases = {
+        "offset wraps": with_header(offset=(0, 2 ** 64 - 64)),
+        "count wraps": with_header(count=(5, 2 ** 61)),
+        "count past end": with_header(count=(12, h0.count[12] + 10 ** 6)),
+        "max_stack too small": with_header(max_stack=max(h0.max_stack - 1, 0) if h0.max_stack else 5),
+        "max_stack too large": with_header(max_stack=1000),
+        "features": with_header(features=h0.features | 2),
+        "has_media": with_header(has_media=1 - h0.has_media),
+        "primref out of range": with_payload(prim0_out_of_range),
+        "bvh cycle": with_payload(child_to_parent),
+    }
+    for why, data in cases.items():
+        q = tmp_path / f"bad_{why.replace(' ', '_')}.artscene"
+        q.write_bytes(data)
+        with pytest.raises(art.RTError) as e:
+            art.scene_manager().load(q)
+        assert e.value.code == -2, why

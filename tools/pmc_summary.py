@@ -130,7 +130,10 @@ def main(tag, scene, prec, segments_per_step, variant=2, root="gpurun_out"):
         kernels[short] = e
     ext = {k: v for k, v in kernels.items() if k.startswith("art::k_extend") or k.startswith("art::k_paths")}
     total = lambda key: sum(v.get(key, 0) for v in ext.values())
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from another_raytracer_amd._lib import LIB_PATH, kernel_build_id
     res = {"tag": tag, "scene": scene, "precision": prec, "segments": segments_per_step, "extend_variant": variant,
+           "libart_build": kernel_build_id(LIB_PATH),  # bench.py uses this summary only with the same device code
            "kernels": kernels,
            "note": "hbm_read_bytes_corrected = 2*FETCH_SIZE*1024 (gfx950 half-count correction), hbm_write_bytes = WRITE_SIZE*1024; "
                    "bound analysis units: tools/pmc_summary.py docstring"}
