@@ -159,7 +159,7 @@ void validate(const std::string& path, FlatScene& f) {
             case OBJ_BVH: {
                 // a single-leaf BVH's root node holds one real child and no stack entries (bvh.cpp build_sah_bvh)
                 if (o.a < 0 || static_cast<size_t>(o.a) >= nn) bad(path, "BVH object out of range");
-                if (o.b != kNodeEmpty && !leaf_ok(o.b)) bad(path, "BVH object's hoisted leaf out of range");
+                if (o.b != kNodeEmpty && !leaf_ok(o.b)) bad(path, "BVH object out of range (hoisted leaf)");
                 f.max_stack = std::max(f.max_stack, stack[o.a]);
                 f.max_bvh_depth = std::max(f.max_bvh_depth, depth[o.a]);
                 break;
