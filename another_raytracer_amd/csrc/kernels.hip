@@ -150,10 +150,21 @@ template <class R> struct ResRec;  // final per-slot radiance
 template <> struct ResRec<float> { float4 v; };
 template <> struct ResRec<double> { double x, y, z; };  // 24 B, unpadded: k_accum streams these at HBM rate
 __device__ __forceinline__ void store_res(ResRec<float>* res, uint32_t q, V3<float> L) { res[q].v = make_float4(L.x, L.y, L.z, 0.0f); }
+// ART_RES_NT: the radiance records stream out with non-temporal stores (read once, by k_accum after the pass), so they
+// do not evict the L2-resident camera-ray rings of k_paths
+#ifndef ART_RES_NT
+#define ART_RES_NT 1
+#endif
 __device__ __forceinline__ void store_res(ResRec<double>* res, uint32_t q, V3<double> L) {
+#if ART_RES_NT
+    __builtin_nontemporal_store(L.x, &res[q].x);
+    __builtin_nontemporal_store(L.y, &res[q].y);
+    __builtin_nontemporal_store(L.z, &res[q].z);
+#else
     res[q].x = L.x;
     res[q].y = L.y;
     res[q].z = L.z;
+#endif
 }
 __device__ __forceinline__ void load_res(const ResRec<float>* res, uint32_t q, double& r, double& g, double& b) {
     const float4 v = res[q].v;

@@ -12,10 +12,11 @@ fixtures pin:
                        scene build incl. BVH-build draws) and the sha256 of the canonical scene dump
   * render_<scene>.npz reference renders (engine_mode::single semantics): RGB8, f64 per-pixel sums and the
                        exact segment count (world.hit calls)
-  * render_stat_1_384x216x16.npz  the headline scene (alias 1) rendered by the reference twice with independent
-                       sample sequences -- engine_mode::single, and parallel_stripes with 4 threads (its shared
-                       global RNG) -- for the statistical parity test of the f64 GPU path (SURVEY.md §8(d)
-                       tolerance 3: the pair's RMSE is the noise floor); `make_golden.py stat` makes only this
+  * render_stat_<scene>_384x216x<spp>.npz  the headline scene (alias 1, 16 spp), the cow mesh scene (16 spp) and the
+                       Next-Week final (alias 8, 32 spp) rendered by the reference twice with independent sample
+                       sequences -- engine_mode::single, and parallel_stripes with 4 threads (its shared global RNG)
+                       -- for the statistical parity test of the f64 GPU path (SURVEY.md §8(d) tolerance 3: the
+                       pair's RMSE is the noise floor); `make_golden.py stat [scene ...]` makes only these
   * images.npz         small JPEG / PNG files of every variant libart's decoder handles (baseline, progressive,
                        4:4:4 / 4:2:2 / 4:2:0, grayscale, CMYK, restart intervals, extreme quantizers; PNG gray 1..16
                        bits, palette +- tRNS, RGB(A), gray+alpha) made with PIL from a fixed pattern, each with the
@@ -87,11 +88,16 @@ def images_mode_fixtures():
         print("images", sc, info)
 
 
-STAT = ("1", 384, 216, 16)
+STAT = [("1", 384, 216, 16), ("cow", 384, 216, 16), ("8", 384, 216, 32)]
 
 
-def stat_fixtures():
-    sc, W, H, spp = STAT
+def stat_fixtures(only=None):
+    for sc, W, H, spp in STAT:
+        if only is None or sc in only:
+            stat_fixture(sc, W, H, spp)
+
+
+def stat_fixture(sc, W, H, spp):
     rgb, acc, info = render(sc, W, H, spp)
     tmp = "/tmp/golden_stat_stripes"
     info2 = json.loads(run("render", sc, W, H, spp, tmp, "stripes", 4).strip().splitlines()[-1])
@@ -192,8 +198,8 @@ def main():
     if sys.argv[1:] == ["adaptive"]:
         adaptive_fixtures()
         return
-    if sys.argv[1:] == ["stat"]:
-        stat_fixtures()
+    if sys.argv[1:2] == ["stat"]:
+        stat_fixtures(sys.argv[2:] or None)
         return
     if sys.argv[1:] == ["images"]:
         image_fixtures()

@@ -5,10 +5,13 @@
 * Independence from the partition: band-interleaved renders reassemble to the bit-identical image.
 * Statistical parity with the reference program itself (independent RNG, SURVEY.md §8(d) tolerance 3), f64 path:
   - configs[0] (tests/golden/render_c1_400x225x64.npz): RMSE <= 1.1x the oracle's seed-to-seed noise floor;
-  - the headline scene (alias 1) at 384x216x16 (tests/golden/render_stat_1_384x216x16.npz: the reference's single
-    and 4-thread stripes renders): RMSE vs the single render <= 1.1x the single-vs-stripes RMSE, the same on 8x8
-    block means (x1.25: noise / 8, so a bias of ~1 LSB shows), and the per-channel mean within 0.5 LSB.
+  - the headline scene (alias 1) at 384x216x16, the cow mesh scene at 384x216x16 and the Next-Week final at
+    384x216x32 (tests/golden/render_stat_*.npz: the reference's single and 4-thread stripes renders): RMSE vs the
+    single render <= 1.1x the single-vs-stripes RMSE, the same on 8x8 block means (x1.25: noise / 8, so a bias of
+    ~1 LSB shows), the per-channel mean within 0.5 LSB, and segments per primary within 1 %.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -154,17 +157,23 @@ def _rmse(a, b):
     return float(np.sqrt(np.mean((a.astype(np.float64) - b.astype(np.float64)) ** 2)))
 
 
+STAT = {"1": "render_stat_1_384x216x16.npz", "cow": "render_stat_cow_384x216x16.npz", "8": "render_stat_8_384x216x32.npz"}
+
+
 @pytest.mark.parametrize("seed", [0, 1])
-def test_statistical_parity_headline_scene_f64(gpu, seed):
-    """The f64 GPU path vs the reference program's own render of the headline scene (independent RNG)."""
-    ref = np.load("tests/golden/render_stat_1_384x216x16.npz")
+@pytest.mark.parametrize("scene", list(STAT))
+def test_statistical_parity_headline_scene_f64(gpu, scene, seed):
+    """The f64 GPU path vs the reference program's own render (independent RNG) of the headline scene, the cow mesh
+    (triangle.h:22-88 under the mist medium, constant_medium.h:37-82) and the Next-Week final (boxes, instances, two
+    media, textures)."""
+    ref = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", STAT[scene]))
     W, H, spp = int(ref["W"]), int(ref["H"]), int(ref["spp"])
     single, stripes = ref["rgb_single"], ref["rgb_stripes"]
     floor, bfloor = _rmse(single, stripes), _rmse(_block_means(single), _block_means(stripes))
-    g = gpu_render("1", W, H, spp, "f64", seed=seed, accum=False)
+    g = gpu_render(scene, W, H, spp, "f64", seed=seed, accum=False)
     rmse, brmse = _rmse(g["rgb"], single), _rmse(_block_means(g["rgb"]), _block_means(single))
     bias = (g["rgb"].astype(np.float64) - single).mean(axis=(0, 1))
-    print(f"seed {seed}: rmse {rmse:.3f} (floor {floor:.3f}) block rmse {brmse:.3f} (floor {bfloor:.3f}) bias {bias}")
+    print(f"scene {scene} seed {seed}: rmse {rmse:.3f} (floor {floor:.3f}) block rmse {brmse:.3f} (floor {bfloor:.3f}) bias {bias}")
     assert rmse <= 1.1 * floor
     assert brmse <= 1.25 * bfloor
     assert np.all(np.abs(bias) <= 0.5)

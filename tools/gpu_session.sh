@@ -7,6 +7,8 @@
 #   bench:TAG[:ARGS]            bench.py line -> gpurun_out/bench_TAG.log
 #   prof:TAG[:ARGS]             rocprofv3 --kernel-trace --stats of a bench run -> gpurun_out/prof_TAG
 #   configs:TAG                 tools/configs.sh (one bench line per BASELINE GPU config)
+#   stats:TAG                   tools/stats_configs.sh over the four GPU configs (libart_stats.so: divergence counters
+#                               and the per-phase cycle split) -> gpurun_out/stats_TAG.txt
 # Usage (GPU box): bash tools/gpu_session.sh tests ab:libart_x.so,libart.so pmc:r2b:1
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
 export TMPDIR=/tmp
@@ -43,6 +45,10 @@ for step in "$@"; do
       tail -1 gpurun_out/rocprof_$a.log ;;
     configs)
       TAG=$a bash tools/configs.sh || exit 1 ;;
+    stats)
+      CFGS="--scene 1 --spp 64|--scene cow --spp 64|--scene 8 --spp 64|--scene dino --width 4096 --height 4096 --spp 16" bash tools/stats_configs.sh \
+        > gpurun_out/stats_$a.txt 2>&1 || exit 1
+      cat gpurun_out/stats_$a.txt ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac
