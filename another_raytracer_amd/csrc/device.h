@@ -250,6 +250,7 @@ struct DevScene {
     const TriRec<R>* leaf_tris;  // leaf_tris[slot] = tris[index of primrefs[slot]] for triangle refs, zeros otherwise
     const PrimRec80* leaf_prims;  // leaf_prims[slot]: the record of primrefs[slot] of any type (triangle-free kernels)
     const PrimRec80* obj_prims;  // obj_prims[o] = the record of prim object o's primitive (indexed like objs)
+    const ObjBox* obj_box;       // obj_box[o]: world-space cull box of instance o (indexed like objs)
     const uint8_t* lds_image;   // layout.h LDS scene image (nullptr unless the scene qualifies)
     uint32_t n_nodes, n_primrefs, n_tris, n_objs;  // array lengths (k_paths_g's LDS copies)
     uint32_t nodes_lds;         // k_paths_g LM 2: LDS byte address of the copy of nodes [0, n_lds_nodes) (top levels)
@@ -449,6 +450,36 @@ __device__ __forceinline__ float slab_key(float x0, float x1, float y0, float y1
     const float lo = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), tminf));
     const float hi = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), tmaxf));
     return (lo <= hi && child != kNodeEmpty) ? lo : __builtin_inff();
+}
+// ART_NEAR_FAR_G: the HBM-scene traversal loads each axis' near and far planes by the direction's sign (as the LDS
+// variant does), so a child's entry is max(x0, y0, z0, tmin) and its exit min(x1, y1, z1, tmax) without the per-axis
+// min/max.  For 1/d > 0, t(lo) <= t(hi) (the FMA rounding is monotone in the plane), so the selected planes give
+// exactly the values the min/max picked (and an empty slot's +-FLT_MAX box stays missed): same keys, 24 fewer VALU per
+// node visit.
+#ifndef ART_NEAR_FAR_G
+#define ART_NEAR_FAR_G 1
+#endif
+__device__ __forceinline__ float slab_key_nf(float x0, float x1, float y0, float y1, float z0, float z1, float tminf, float tmaxf) {
+    const float lo = fmaxf(fmaxf(x0, y0), fmaxf(z0, tminf));
+    const float hi = fminf(fminf(x1, y1), fminf(z1, tmaxf));
+    return lo <= hi ? lo : __builtin_inff();
+}
+// x0/y0/z0 (lx, ly, lz): near planes, x1/y1/z1 (hx, hy, hz): far planes
+__device__ __forceinline__ void slab4_nf(const float4& lx, const float4& hx, const float4& ly, const float4& hy, const float4& lz, const float4& hz,
+                                        float ix, float iy, float iz, float oix, float oiy, float oiz, float tminf, float tmaxf, float& k0,
+                                        float& k1, float& k2, float& k3) {
+    const f2v vx = {ix, ix}, vy = {iy, iy}, vz = {iz, iz};
+    const f2v nx = {-oix, -oix}, ny = {-oiy, -oiy}, nz = {-oiz, -oiz};
+    const f2v x0a = __builtin_elementwise_fma(f2v{lx.x, lx.y}, vx, nx), x0b = __builtin_elementwise_fma(f2v{lx.z, lx.w}, vx, nx);
+    const f2v x1a = __builtin_elementwise_fma(f2v{hx.x, hx.y}, vx, nx), x1b = __builtin_elementwise_fma(f2v{hx.z, hx.w}, vx, nx);
+    const f2v y0a = __builtin_elementwise_fma(f2v{ly.x, ly.y}, vy, ny), y0b = __builtin_elementwise_fma(f2v{ly.z, ly.w}, vy, ny);
+    const f2v y1a = __builtin_elementwise_fma(f2v{hy.x, hy.y}, vy, ny), y1b = __builtin_elementwise_fma(f2v{hy.z, hy.w}, vy, ny);
+    const f2v z0a = __builtin_elementwise_fma(f2v{lz.x, lz.y}, vz, nz), z0b = __builtin_elementwise_fma(f2v{lz.z, lz.w}, vz, nz);
+    const f2v z1a = __builtin_elementwise_fma(f2v{hz.x, hz.y}, vz, nz), z1b = __builtin_elementwise_fma(f2v{hz.z, hz.w}, vz, nz);
+    k0 = slab_key_nf(x0a.x, x1a.x, y0a.x, y1a.x, z0a.x, z1a.x, tminf, tmaxf);
+    k1 = slab_key_nf(x0a.y, x1a.y, y0a.y, y1a.y, z0a.y, z1a.y, tminf, tmaxf);
+    k2 = slab_key_nf(x0b.x, x1b.x, y0b.x, y1b.x, z0b.x, z1b.x, tminf, tmaxf);
+    k3 = slab_key_nf(x0b.y, x1b.y, y0b.y, y1b.y, z0b.y, z1b.y, tminf, tmaxf);
 }
 __device__ __forceinline__ void slab4(const float4& lx, const float4& hx, const float4& ly, const float4& hy, const float4& lz, const float4& hz,
                                       const int4& ch, float ix, float iy, float iz, float oix, float oiy, float oiz, float tminf, float tmaxf,
@@ -850,15 +881,44 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
 #else
                 ch = lds_i4(kLdsOffNodes + kLdsNodePlaneChild * kLdsPlane + n16);
 #endif
+            }
+            // !L (ART_NEAR_FAR_G): byte offsets of each axis' near plane in a BvhNode (lo x / y / z at 0 / 32 / 64, its hi
+            // plane 16 above), from the direction's sign; the far plane is the other one (offset ^ 16).  Recomputed per
+            // visit from 1/d (live anyway; the empty asm keeps the compiler from hoisting three more loop-carried VGPRs)
+            [[maybe_unused]] uint32_t nfx = 0, nfy = 0, nfz = 0;
+            if constexpr (!L) {
+                if (ART_NEAR_FAR_G) {
+                    uint32_t sx, sy, sz;  // sign bits of 1/d, extracted in the loop (volatile: not hoisted)
+                    __asm__ volatile("v_lshrrev_b32 %0, 31, %1" : "=v"(sx) : "v"(ix));
+                    __asm__ volatile("v_lshrrev_b32 %0, 31, %1" : "=v"(sy) : "v"(iy));
+                    __asm__ volatile("v_lshrrev_b32 %0, 31, %1" : "=v"(sz) : "v"(iz));
+                    nfx = sx << 4;
+                    nfy = 32u + (sy << 4);
+                    nfz = 64u + (sz << 4);
+                }
+            }
+            if constexpr (L) {
             } else if (PL && static_cast<uint32_t>(node) < S.n_lds_nodes) {
                 // the top levels, copied into LDS: explicit LDS loads (a generic pointer here would be merged with
                 // the global branch's into flat loads)
                 const uint32_t a = S.nodes_lds + static_cast<uint32_t>(node) * static_cast<uint32_t>(sizeof(BvhNode));
-                lx = lds_f4(a); hx = lds_f4(a + 16); ly = lds_f4(a + 32); hy = lds_f4(a + 48); lz = lds_f4(a + 64); hz = lds_f4(a + 80);
+                if (ART_NEAR_FAR_G) {  // lx/ly/lz: near planes, hx/hy/hz: far planes
+                    lx = lds_f4(a + nfx); hx = lds_f4(a + (nfx ^ 16u)); ly = lds_f4(a + nfy); hy = lds_f4(a + (nfy ^ 16u));
+                    lz = lds_f4(a + nfz); hz = lds_f4(a + (nfz ^ 16u));
+                } else {
+                    lx = lds_f4(a); hx = lds_f4(a + 16); ly = lds_f4(a + 32); hy = lds_f4(a + 48); lz = lds_f4(a + 64); hz = lds_f4(a + 80);
+                }
                 ch = lds_i4(a + 96);
             } else {
                 const float4* np = reinterpret_cast<const float4*>(S.nodes + node);
-                lx = np[0]; hx = np[1]; ly = np[2]; hy = np[3]; lz = np[4]; hz = np[5];
+                if (ART_NEAR_FAR_G) {
+                    const char* nb = reinterpret_cast<const char*>(np);
+                    lx = *reinterpret_cast<const float4*>(nb + nfx); hx = *reinterpret_cast<const float4*>(nb + (nfx ^ 16u));
+                    ly = *reinterpret_cast<const float4*>(nb + nfy); hy = *reinterpret_cast<const float4*>(nb + (nfy ^ 16u));
+                    lz = *reinterpret_cast<const float4*>(nb + nfz); hz = *reinterpret_cast<const float4*>(nb + (nfz ^ 16u));
+                } else {
+                    lx = np[0]; hx = np[1]; ly = np[2]; hy = np[3]; lz = np[4]; hz = np[5];
+                }
                 ch = reinterpret_cast<const int4*>(np)[6];
             }
             // branchless pushes (far to near) after a sorting network (ascending entry distance, misses last): every
@@ -890,7 +950,8 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
 #endif
             } else {
                 float k0, k1, k2, k3;
-                slab4(lx, hx, ly, hy, lz, hz, ch, ix, iy, iz, oix, oiy, oiz, tminf, tmaxf, k0, k1, k2, k3);
+                if (ART_NEAR_FAR_G) slab4_nf(lx, hx, ly, hy, lz, hz, ix, iy, iz, oix, oiy, oiz, tminf, tmaxf, k0, k1, k2, k3);
+                else slab4(lx, hx, ly, hy, lz, hz, ch, ix, iy, iz, oix, oiy, oiz, tminf, tmaxf, k0, k1, k2, k3);
                 int32_t c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
                 cas(k0, c0, k1, c1);
                 cas(k2, c2, k3, c3);
@@ -1099,9 +1160,32 @@ __device__ __forceinline__ Ray<R> xform_in(const ObjRec<R>& o, const Ray<R>& r) 
 }
 
 // Any non-medium object: prim, BVH, or a translate/rotate_y chain (<= kMaxXformChain) over one of them.
+// ART_XFORM_CULL: an instance is first tested against its world-space cull box (layout.h ObjBox) with the traversal's
+// own conservative f32 slab arithmetic; a miss skips the transform into object space and the whole object test.
+#ifndef ART_XFORM_CULL
+#define ART_XFORM_CULL 1
+#endif
+template <class R>
+__device__ __forceinline__ bool cull_box_hit(const ObjBox& b, const Ray<R>& r, R tmin, R tmax) {
+    const float ix = __builtin_amdgcn_rcpf(f32_dir(r.d.x)), iy = __builtin_amdgcn_rcpf(f32_dir(r.d.y)), iz = __builtin_amdgcn_rcpf(f32_dir(r.d.z));
+    const float oix = static_cast<float>(r.o.x) * ix, oiy = static_cast<float>(r.o.y) * iy, oiz = static_cast<float>(r.o.z) * iz;
+    const float x0 = fmaf(b.lo[0], ix, -oix), x1 = fmaf(b.hi[0], ix, -oix);
+    const float y0 = fmaf(b.lo[1], iy, -oiy), y1 = fmaf(b.hi[1], iy, -oiy);
+    const float z0 = fmaf(b.lo[2], iz, -oiz), z1 = fmaf(b.hi[2], iz, -oiz);
+    const float lo = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), f_lo(tmin)));
+    const float hi = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), f_hi(tmax)));
+    return lo <= hi;
+}
 template <class R, uint32_t F, int B, bool L, bool PL = false, bool RES = false>
 __device__ __forceinline__ bool hit_object(const DevScene<R>& S, const uint8_t* lds, int32_t oi, Ray<R> r, R tmin, R tmax, StackT<L>* stk,
                                            R& t, uint32_t& prim, uint32_t& face, uint32_t& mt, TravResume* rs = nullptr) {
+    if constexpr ((F & F_XFORM) != 0 && ART_XFORM_CULL) {
+        // a resumed traversal passed the box when it started
+        if (!RES || rs->fresh) {
+            const ObjBox& b = S.obj_box[oi];
+            if (b.valid && !cull_box_hit(b, r, tmin, tmax)) return false;
+        }
+    }
     if (F & F_XFORM) {
 #pragma unroll
         for (int c = 0; c < kMaxXformChain; ++c) {

@@ -951,7 +951,7 @@ __host__ __device__ constexpr size_t paths_g_head_bytes(uint32_t stack, int bloc
 // LM kernels also hold the world list and the object records (a few KiB): every segment walks them, and a prim
 // object's test otherwise waits on three dependent L1 loads (world slot -> object -> primitive)
 __host__ __device__ constexpr size_t paths_g_world_bytes(int32_t nworld, uint32_t n_objs) {
-    return align16(sizeof(int32_t) * static_cast<uint32_t>(nworld)) + (sizeof(ObjRec<double>) + sizeof(PrimRec80)) * n_objs;
+    return align16(sizeof(int32_t) * static_cast<uint32_t>(nworld)) + (sizeof(ObjRec<double>) + sizeof(PrimRec80) + sizeof(ObjBox)) * n_objs;
 }
 __host__ __device__ constexpr size_t paths_g_mesh_bytes(uint32_t n_nodes, uint32_t n_primrefs, uint32_t n_tris) {  // n_tris: 0 unless F_TRI
     return sizeof(BvhNode) * n_nodes + align16(sizeof(uint32_t) * n_primrefs) + sizeof(TriRec<double>) * n_tris;
@@ -984,9 +984,13 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
         uint8_t* pb = ob + sizeof(ObjRec<double>) * S0.n_objs;
         const uint4* ps = reinterpret_cast<const uint4*>(S0.obj_prims);
         for (uint32_t i = threadIdx.x; i < S0.n_objs * (sizeof(PrimRec80) / 16); i += B) reinterpret_cast<uint4*>(pb)[i] = ps[i];
+        uint8_t* bb = pb + sizeof(PrimRec80) * S0.n_objs;
+        const uint4* bs = reinterpret_cast<const uint4*>(S0.obj_box);
+        for (uint32_t i = threadIdx.x; i < S0.n_objs * (sizeof(ObjBox) / 16); i += B) reinterpret_cast<uint4*>(bb)[i] = bs[i];
         S.world = reinterpret_cast<const int32_t*>(wb);
         S.objs = reinterpret_cast<const ObjRec<double>*>(ob);
         S.obj_prims = reinterpret_cast<const PrimRec80*>(pb);
+        S.obj_box = reinterpret_cast<const ObjBox*>(bb);
         lm_off += paths_g_world_bytes(S0.nworld, S0.n_objs);
     }
     if constexpr (LM == 2) {  // the first n_lds_nodes nodes (the top levels of every BVH) into LDS
@@ -1727,6 +1731,117 @@ static std::vector<uint8_t> lds_scene_image(const FlatScene& f, uint32_t& nmov, 
     return img;
 }
 
+// World-space cull boxes of the instances (layout.h ObjBox; device.h hit_object): each translate / rotate_y chain's
+// object-space bounds -- the root node's child boxes and hoisted primitives of a BVH, or a primitive's own extent --
+// carried through the chain's object-to-world maps (hittable.cpp:3-85: rotate_y's inverse x = c x' + s z',
+// z = -s x' + c z', then + offset) at the 8 corners in f64, rounded outward to f32 and padded by 1e-5 relative: far
+// more than the f64 rounding between a world-space ray and its object-space image, so a ray that misses the box
+// misses the instance.
+static void prim_bounds(const FlatScene& f, uint32_t ref, double lo[3], double hi[3]) {
+    const uint32_t i = primref_index(ref);
+    switch (primref_type(ref)) {
+        case PRIM_SPHERE: {  // a moving sphere over the unit shutter (its BVH boxes' range, bvh_node(list, 0, 1))
+            const auto& sp = f.spheres[i];
+            for (int a = 0; a < 3; ++a) {
+                double c0 = sp.c[a], c1 = sp.c[a];
+                if (sp.flags & SPH_MOVING) {
+                    c0 = sp.c[a] + ((0.0 - sp.t0) / sp.dt) * sp.d[a];
+                    c1 = sp.c[a] + ((1.0 - sp.t0) / sp.dt) * sp.d[a];
+                }
+                lo[a] = std::min(c0, c1) - std::fabs(sp.r);
+                hi[a] = std::max(c0, c1) + std::fabs(sp.r);
+            }
+            break;
+        }
+        case PRIM_TRIANGLE: {
+            const auto& t = f.tris[i];
+            for (int a = 0; a < 3; ++a) {
+                lo[a] = std::min({t.p[a], t.p[3 + a], t.p[6 + a]});
+                hi[a] = std::max({t.p[a], t.p[3 + a], t.p[6 + a]});
+            }
+            break;
+        }
+        case PRIM_RECT: {  // aarect.h:16-21: the plane coordinate padded by 1e-4
+            const auto& r = f.rects[i];
+            const int ia = r.axis == 2 ? 1 : 0, ib = r.axis == 0 ? 1 : 2, ik = r.axis == 0 ? 2 : r.axis == 1 ? 1 : 0;
+            lo[ia] = r.a0; hi[ia] = r.a1;
+            lo[ib] = r.b0; hi[ib] = r.b1;
+            lo[ik] = r.k - 1e-4; hi[ik] = r.k + 1e-4;
+            break;
+        }
+        default: {
+            const auto& b = f.boxes[i];
+            for (int a = 0; a < 3; ++a) { lo[a] = b.mn[a]; hi[a] = b.mx[a]; }
+        }
+    }
+}
+static std::vector<ObjBox> instance_cull_boxes(const FlatScene& f) {
+    std::vector<ObjBox> out(f.objs.size());
+    const double dinf = std::numeric_limits<double>::infinity();
+    for (size_t o = 0; o < f.objs.size(); ++o) {
+        out[o] = ObjBox{};
+        if (f.objs[o].kind != OBJ_TRANSLATE && f.objs[o].kind != OBJ_ROTATE_Y) continue;
+        std::vector<size_t> chain;  // outermost first
+        size_t in = o;
+        while (f.objs[in].kind == OBJ_TRANSLATE || f.objs[in].kind == OBJ_ROTATE_Y) {
+            chain.push_back(in);
+            in = static_cast<size_t>(f.objs[in].a);
+        }
+        double lo[3] = {dinf, dinf, dinf}, hi[3] = {-dinf, -dinf, -dinf};
+        auto grow = [&](const double l[3], const double h[3]) {
+            for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], l[a]); hi[a] = std::max(hi[a], h[a]); }
+        };
+        const ObjRec<double>& inner = f.objs[in];
+        if (inner.kind == OBJ_PRIM) {
+            double l[3], h[3];
+            prim_bounds(f, static_cast<uint32_t>(inner.a), l, h);
+            grow(l, h);
+        } else if (inner.kind == OBJ_BVH) {
+            const BvhNode& n = f.nodes[static_cast<size_t>(inner.a)];
+            for (int c = 0; c < 4; ++c)
+                if (n.child[c] != kNodeEmpty) {
+                    const double l[3] = {n.lox[c], n.loy[c], n.loz[c]}, h[3] = {n.hix[c], n.hiy[c], n.hiz[c]};
+                    grow(l, h);
+                }
+            if (inner.b != kNodeEmpty)
+                for (uint32_t k = 0; k < leaf_count(inner.b); ++k) {
+                    double l[3], h[3];
+                    prim_bounds(f, f.primrefs[leaf_first(inner.b) + k], l, h);
+                    grow(l, h);
+                }
+        } else {
+            continue;  // no box: the object is tested as before
+        }
+        if (!(lo[0] <= hi[0] && lo[1] <= hi[1] && lo[2] <= hi[2])) continue;
+        double wl[3] = {dinf, dinf, dinf}, wh[3] = {-dinf, -dinf, -dinf};
+        for (int k = 0; k < 8; ++k) {
+            double p[3] = {(k & 1) ? hi[0] : lo[0], (k & 2) ? hi[1] : lo[1], (k & 4) ? hi[2] : lo[2]};
+            for (size_t j = chain.size(); j-- > 0;) {  // innermost transform first
+                const ObjRec<double>& x = f.objs[chain[j]];
+                if (x.kind == OBJ_TRANSLATE) {
+                    for (int a = 0; a < 3; ++a) p[a] += x.p[a];
+                } else {  // object -> world of rotate_y (s = p[0], c = p[1])
+                    const double sn = x.p[0], cs = x.p[1], px = p[0], pz = p[2];
+                    p[0] = cs * px + sn * pz;
+                    p[2] = -sn * px + cs * pz;
+                }
+            }
+            for (int a = 0; a < 3; ++a) { wl[a] = std::min(wl[a], p[a]); wh[a] = std::max(wh[a], p[a]); }
+        }
+        ObjBox b{};
+        for (int a = 0; a < 3; ++a) {
+            const double m = std::max({std::fabs(wl[a]), std::fabs(wh[a]), wh[a] - wl[a]});
+            const double pad = 1e-5 * m + 1e-30;
+            b.lo[a] = std::nextafter(static_cast<float>(wl[a] - pad), -std::numeric_limits<float>::infinity());
+            b.hi[a] = std::nextafter(static_cast<float>(wh[a] + pad), std::numeric_limits<float>::infinity());
+        }
+        b.valid = std::isfinite(b.lo[0]) && std::isfinite(b.lo[1]) && std::isfinite(b.lo[2]) && std::isfinite(b.hi[0]) &&
+                  std::isfinite(b.hi[1]) && std::isfinite(b.hi[2]);
+        out[o] = b;
+    }
+    return out;
+}
+
 template <class R>
 static void build_device_scene(const FlatScene& f, DeviceScene<R>& ds) {
     std::vector<SphereRec<R>> sph(f.spheres.size());
@@ -1812,6 +1927,7 @@ static void build_device_scene(const FlatScene& f, DeviceScene<R>& ds) {
                       sizeof(RectRec<R>) <= sizeof(PrimRec80) && sizeof(BoxRec<R>) <= sizeof(PrimRec80), "PrimRec80 holds every record");
         ds.view.obj_prims = ds.upload(op);
     }
+    ds.view.obj_box = ds.upload(instance_cull_boxes(f));
     ds.view.world = ds.upload(f.world);
     ds.view.mats = ds.upload(mats);
     ds.view.texs = ds.upload(texs);

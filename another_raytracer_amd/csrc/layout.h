@@ -161,6 +161,15 @@ struct ObjRec {
     R p[4];         // TRANSLATE: offset xyz; ROTATE_Y: sin, cos; MEDIUM: neg_inv_density
 };
 constexpr int kMaxXformChain = 2;  // translate(rotate_y(X)) is the deepest chain in the reference scenes
+// World-space cull box of an instance (translate / rotate_y chain, hittable.cpp:3-85), indexed like objs: the
+// f32-rounded-outward, padded box of its transformed object-space bounds (DevScene::obj_box).  A ray that misses it
+// cannot hit the instance, so the object-space transform and traversal are skipped (valid == 0: no box, test the object).
+struct alignas(16) ObjBox {
+    float lo[3];
+    uint32_t valid;
+    float hi[3];
+    uint32_t pad;
+};
 // Scene features: kernels are instantiated for feature subsets (spheres only / meshes / everything).
 // F_MEDIA: constant_medium objects; F_MEDIA_G: one of them has a boundary that is not a sphere primitive (its two
 // boundary hits are whole object traversals; a sphere boundary is one quadratic, device.h hit_medium)

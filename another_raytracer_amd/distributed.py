@@ -138,14 +138,10 @@ class multi_engine:
             for o in scene.objects:
                 check(lib.rt_graph_add_world(g, o.id), "rt_graph_add_world")
             check(lib.rt_multi_from_graph(g, devs, len(self.devices), ctypes.byref(self._m)), "rt_multi_from_graph")
-        from ._lib import rt_scene_info
-        info = rt_scene_info()
-        check(lib.rt_multi_scene_info(self._m, ctypes.byref(info)), "rt_multi_scene_info")
-        self.info = {f: (tuple(getattr(info, f)) if isinstance(getattr(info, f), ctypes.Array) else getattr(info, f))
-                     for f, _ in info._fields_}
+        self.info = self.scene_info()
         # engine::set_scene(world, background) (engine.h:24-28): a builtin scene's own background unless overridden
         self.background = tuple(background) if background is not None else (
-            tuple(info.background) if isinstance(scene, str) else (0.0, 0.0, 0.0))
+            tuple(self.info["background"]) if isinstance(scene, str) else (0.0, 0.0, 0.0))
         self.stats = {}
 
     def run(self, out, profile=False):
@@ -169,6 +165,13 @@ class multi_engine:
               "rt_render_multi")
         self.stats = st.as_dict()
         return st.ms
+
+    def scene_info(self):
+        """rt_multi_scene_info: the scene_manager view and sizes (device_bytes_f64 per device, once rendered)."""
+        from ._lib import rt_scene_info
+        info = rt_scene_info()
+        check(lib.rt_multi_scene_info(self._m, ctypes.byref(info)), "rt_multi_scene_info")
+        return {f: (tuple(getattr(info, f)) if isinstance(getattr(info, f), ctypes.Array) else getattr(info, f)) for f, _ in info._fields_}
 
     def device_stats(self):
         """Per-device stats of the last run (devices[k] at index k): segments, kernel time, rows."""

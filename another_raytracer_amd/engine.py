@@ -79,6 +79,15 @@ class engine:
         self.background = tuple(float(x) for x in background)
         self._scene = None if world is None or world.empty() else compile_world(world, self.device)
 
+    def scene_info(self):
+        """rt_scene_info of the engine's compiled scene (device_bytes_f64 is set once a render uploaded it)."""
+        from ._lib import rt_scene_info
+        if self._scene is None:
+            raise ValueError("no scene set")
+        info = rt_scene_info()
+        check(lib.rt_scene_info_get(self._scene, ctypes.byref(info)), "rt_scene_info_get")
+        return {f: (tuple(getattr(info, f)) if isinstance(getattr(info, f), ctypes.Array) else getattr(info, f)) for f, _ in info._fields_}
+
     def params(self, band_rows=None, band_count=1, band_index=0, flags=0, stream=None):
         p = rt_params()
         p.width, p.height = self.width, self.height

@@ -265,7 +265,6 @@ def main():
         del probe
         eng = multi_engine(args.scene, devices, cam, args.width, args.height, args.spp, max_depth=args.max_depth,
                            band_rows=args.band_rows)
-        scene_bytes = int(eng.info["device_bytes_f64"])
         frame = torch.empty((args.height, args.width, 3), dtype=torch.uint8, device=dev)
 
         def step():
@@ -275,12 +274,14 @@ def main():
         def sync():
             for d in devices:
                 torch.cuda.synchronize(d)
+
+        def scene_bytes_now():  # uploaded at the first render
+            return int(eng.scene_info()["device_bytes_f64"])
         parallelism = (f"1 GPU, rt_render_multi (row-bands({args.band_rows}), single-rank gather + unpack)" if n == 1 else
                        f"row-bands({args.band_rows}) over {n} GPUs, one process: rt_render_multi (one host thread + RCCL rank "
                        f"per GPU, ncclGather to GPU 0 + unpack kernel)")
     else:
         world_scene = art.scene_manager(device=dev.index).build(args.scene)
-        scene_bytes = int(world_scene.info["device_bytes_f64"])
         cam = art.camera(world_scene.lookfrom, world_scene.lookat, (0, 1, 0), world_scene.vfov, args.width / args.height,
                          world_scene.aperture, 10.0, 0.0, 1.0)
         eng = art.engine(cam, art.engine_mode.parallel_stripes, width=args.width, height=args.height,
@@ -298,11 +299,17 @@ def main():
 
         def sync():
             torch.cuda.synchronize(dev)
+
+        def scene_bytes_now():  # uploaded at the first render
+            return int(eng.scene_info()["device_bytes_f64"])
         parallelism = (f"row-bands({args.band_rows}) over {n} GPUs, one process per GPU (torchrun): dist.gather over RCCL "
                        f"to rank 0 + rt_unpack_bands")
 
     for _ in range(args.warmup):
         step()
+    if args.warmup == 0:
+        step()  # the scene upload and workspace allocation happen at the first render: never inside the timed steps
+    scene_bytes = scene_bytes_now()
     if driver == "procs":
         dist.barrier()
     sync()
