@@ -455,7 +455,7 @@ __device__ __forceinline__ float slab_key(float x0, float x1, float y0, float y1
 // variant does), so a child's entry is max(x0, y0, z0, tmin) and its exit min(x1, y1, z1, tmax) without the per-axis
 // min/max.  For 1/d > 0, t(lo) <= t(hi) (the FMA rounding is monotone in the plane), so the selected planes give
 // exactly the values the min/max picked (and an empty slot's +-FLT_MAX box stays missed): same keys, 24 fewer VALU per
-// node visit.
+// node visit.  Measured (r3c): cow +3.6 %, Next-Week final +5.6 %, dino 4096^2 +3.9 %.
 #ifndef ART_NEAR_FAR_G
 #define ART_NEAR_FAR_G 1
 #endif
@@ -1162,8 +1162,10 @@ __device__ __forceinline__ Ray<R> xform_in(const ObjRec<R>& o, const Ray<R>& r) 
 // Any non-medium object: prim, BVH, or a translate/rotate_y chain (<= kMaxXformChain) over one of them.
 // ART_XFORM_CULL: an instance is first tested against its world-space cull box (layout.h ObjBox) with the traversal's
 // own conservative f32 slab arithmetic; a miss skips the transform into object space and the whole object test.
+// Measured on the Next-Week final (its 1000-sphere cluster under translate(rotate_y)): -0.3 % (6 628 vs 6 650
+// Msamples/s at 256 spp): the root node's own test rejects the same rays, and every ray pays the box test.  Off.
 #ifndef ART_XFORM_CULL
-#define ART_XFORM_CULL 1
+#define ART_XFORM_CULL 0
 #endif
 template <class R>
 __device__ __forceinline__ bool cull_box_hit(const ObjBox& b, const Ray<R>& r, R tmin, R tmax) {
@@ -1387,6 +1389,20 @@ __device__ __forceinline__ void rect_surface(Surf<R>& s, int axis, R a0, R a1, R
     set_face_normal(s, r, n);
     s.p = r.at(t);
 }
+// ART_SPHERE_UV_CALL: get_sphere_uv (sphere.h:24-37) out of line.  Inlined, the f64 polynomial constants of acos and
+// atan2 are hoisted out of the path loop (into VGPRs, 29 of them spilled to scratch at kernel start) in the
+// image-texture kernels; out of line the final-scene kernel drops from 168 VGPRs + 58 spilled to 151 and none, but the
+// call costs more than the reloads, which only earth-texture hits run: -1.0 % on the Next-Week final.  Off.
+#ifndef ART_SPHERE_UV_CALL
+#define ART_SPHERE_UV_CALL 0
+#endif
+[[maybe_unused]] static __device__ __noinline__ void sphere_uv_call(double ox, double oy, double oz, double& u, double& v) {
+    const double pi = 3.1415926535897932385;
+    const double theta = acos(-oy);
+    const double phi = atan2(-oz, ox) + pi;
+    u = phi / (2.0 * pi);
+    v = theta / pi;
+}
 template <class R, uint32_t F, bool UV = true>
 __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref, uint32_t face, const Ray<R>& r, R t, Surf<R>& s) {
     const uint32_t idx = primref_index(ref);
@@ -1402,11 +1418,15 @@ __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref,
             set_face_normal(s, r, outward);
             // u,v only feed image textures: acos/atan2 are skipped for materials that never sample them
             if (UV && !moving && (S.mats[sp.mat].flags & MATF_NEEDS_UV)) {
+#if ART_SPHERE_UV_CALL
+                sphere_uv_call(outward.x, outward.y, outward.z, s.u, s.v);
+#else
                 const R pi = R(3.1415926535897932385);
                 const R theta = acos(-outward.y);
                 const R phi = atan2(-outward.z, outward.x) + pi;
                 s.u = phi / (R(2) * pi);
                 s.v = theta / pi;
+#endif
             } else {
                 s.u = R(0);
                 s.v = R(0);

@@ -205,7 +205,7 @@ def roofline_of(dev_stats, width, scene_bytes, variant, precision, scene, build)
     pm = latest_pmc(precision, scene, variant, build)
     tr = pm.get("extend_bytes_per_segment") if pm else None
     roof = {"kernel": kernel, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": round(tr * segs) if tr else None,
+            "frac": float(f"{achieved / HBM_PEAK_GBS:.6g}"), "traffic": round(tr * segs) if tr else None,
             "algorithmic_bytes_per_launch": round(alg),
             "algorithmic_bytes": "SURVEY 8(d): 128 B/segment + 12 B/pixel + scene bytes, per launch of the slowest device",
             "segments_per_launch": round(segs), "avg_launch_ms": round(per_launch_ms, 4), "launches": launches,
@@ -220,7 +220,7 @@ def roofline_of(dev_stats, width, scene_bytes, variant, precision, scene, build)
             slots = ps["insts_valu"] * 64 * segs / (per_launch_ms * 1e-3) / 1e12
             lu = pm.get("valu_lane_util", 0)
             roof["valu"] = {"achieved": round(slots, 3), "peak": round(VALU_PEAK_TLANE, 2), "unit": "Tlane-inst/s",
-                            "frac": round(slots / VALU_PEAK_TLANE, 4), "lane_util": lu,
+                            "frac": float(f"{slots / VALU_PEAK_TLANE:.6g}"), "lane_util": lu,
                             "useful_frac": round(slots / VALU_PEAK_TLANE * lu, 4),
                             "valu_wave_insts_per_segment": round(ps["insts_valu"], 2),
                             "issue_util_calibrated": pm.get("valu_issue_util_calibrated"),
