@@ -307,9 +307,6 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    if args.warmup == 0:
-        step()  # the scene upload and workspace allocation happen at the first render: never inside the timed steps
-    scene_bytes = scene_bytes_now()
     if driver == "procs":
         dist.barrier()
     sync()
@@ -335,6 +332,7 @@ def main():
     if driver == "procs":
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    scene_bytes = scene_bytes_now()  # uploaded by the first render
     if driver == "procs":
         # max wall time over ranks; all ranks' segments; every rank's per-device totals for the roofline
         mine = torch.tensor([elapsed, float(segs), float(primary_segs), float(variant), acc[0]["segments"], acc[0]["primary"],

@@ -2,6 +2,7 @@
 # One GPU-box session made of steps, each under its own time limit, stopping at the first failure:
 #   tests                       pytest -m gpu (tests/, one process)
 #   calib                       tools/valu_calib (VALU issue-cost calibration, plain run)
+#   uvcheck                     tools/uv_check (device vs glibc get_sphere_uv texel choice) -> gpurun_out/uv_check.json
 #   ab:LIB1,LIB2[:ARGS]         tools/ab_quick.sh over in-tree libart builds (bench.py ARGS, default --spp 256)
 #   pmc:TAG:SCENE[:SPP]         tools/pmc.sh counter passes + kernel trace of the current libart (ART_LIB honoured)
 #   bench:TAG[:ARGS]            bench.py line -> gpurun_out/bench_TAG.log
@@ -28,6 +29,9 @@ for step in "$@"; do
     calib)
       run 120 ./tools/valu_calib > gpurun_out/valu_calib.jsonl 2>&1
       cat gpurun_out/valu_calib.jsonl ;;
+    uvcheck)
+      run 300 ./tools/uv_check > gpurun_out/uv_check.json 2>&1
+      cat gpurun_out/uv_check.json ;;
     ab)
       LIBS="${a//,/ }" ARGS="${b:---spp 256}" bash tools/ab_quick.sh || exit 1 ;;
     pmc)

@@ -159,4 +159,7 @@ def main(tag, scene, prec, segments_per_step, variant=2, root="gpurun_out"):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]), int(sys.argv[5]) if len(sys.argv) > 5 else 2)
+    # argv: tag scene precision segments_per_render [variant [renders]]: renders = path-kernel renders the profiled
+    # process ran (counters are summed over all of them)
+    renders = int(sys.argv[6]) if len(sys.argv) > 6 else 1
+    main(sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]) * renders, int(sys.argv[5]) if len(sys.argv) > 5 else 2)
