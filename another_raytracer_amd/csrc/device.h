@@ -1210,6 +1210,9 @@ __device__ __forceinline__ bool hit_object(const DevScene<R>& S, const uint8_t* 
 
 // Out of line: measured +0.2 % (cow) to +1.8 % (Next-Week final) over the inlined body, which raised the register
 // pressure of the whole path loop for a function most segments do not reach.
+#ifndef ART_MEDIUM_FASTREJECT
+#define ART_MEDIUM_FASTREJECT 1  // hit_medium: decide "no scatter" from an f32 log2 bound before the exact glibc log
+#endif
 static __device__ __noinline__ double glibc_log_call(double x) { return glibc_log(x); }
 // constant_medium.h:37-82.  Consumes one uniform when the clamped interval is non-empty.
 template <class R, uint32_t F, int B, bool L, bool PL = false>
@@ -1265,7 +1268,21 @@ __device__ __forceinline__ bool hit_medium(const DevScene<R>& S, const uint8_t* 
     // f64 log differs from it in the last bit for 445 762 of the 2^24 arguments a uniform can take, which moves a
     // scattering path's t and every sum after it.  glibc_log.h restates glibc's log operation by operation (equal for
     // every k * 2^-24); it replaced a 128 MiB table of glibc's values, whose random reads (an L2 miss per draw) cost 5-10 % on the medium scenes.
-    const R hit_distance = m.p[0] * glibc_log_call(static_cast<double>(uniform_k(rng)) * 0x1p-24);
+    const uint32_t k = uniform_k(rng);
+#if ART_MEDIUM_FASTREJECT
+    {
+        // decided without the exact log when hit_distance > inside by far more than the approximation's error: the
+        // uniform k * 2^-24 is exact in f32, v_log_f32 (log2) is within ~2^-21 relative + 2^-22 absolute, so
+        // |approx - hit_distance| < 2^-12 |approx| + 2^-16 |neg_inv_density| with a wide margin.  Most segments in the
+        // r = 5000 mist of the mesh scenes do not scatter (P(scatter) ~ 1 - e^-0.5), and they skip the out-of-line
+        // glibc log and its table load.  ξ = 0: log2(0) = -inf -> +inf > inside, as the exact path decides.
+        const double nid = static_cast<double>(m.p[0]);
+        const double approx = nid * (0.69314718055994531 * static_cast<double>(__builtin_amdgcn_logf(static_cast<float>(k) * 0x1p-24f)));
+        const double err = 0x1p-12 * __builtin_fabs(approx) + 0x1p-16 * __builtin_fabs(nid);
+        if (approx > static_cast<double>(inside) + err) return false;
+    }
+#endif
+    const R hit_distance = m.p[0] * glibc_log_call(static_cast<double>(k) * 0x1p-24);
     if (hit_distance > inside) return false;
     t = t1 + hit_distance / ray_length;
     return true;
