@@ -41,3 +41,16 @@ def test_bench_exits_nonzero_without_the_gpus():
     if r.returncode == 0:
         pytest.fail("bench.py --gpus 2 succeeded on a box without 2 GPUs")
     assert "needs 2 visible GPUs" in r.stderr and not r.stdout.strip()
+
+
+def test_roofline_prices_the_slowest_gpu():
+    # two GPUs: the slower one's launches set the roofline (SURVEY §8(d) bytes of its own launches / its launch time)
+    devs = [{"segments": 4_000_000, "primary": 1_000_000, "extend_ms": 20.0, "extend_launches": 2, "local_rows": 100, "steps": 2},
+            {"segments": 6_000_000, "primary": 1_000_000, "extend_ms": 30.0, "extend_launches": 2, "local_rows": 100, "steps": 2}]
+    r = bench.roofline_of(devs, 100, 1000, 3, "f64", "1", "no-such-build")
+    segs, pix = 3_000_000, 100 * 100
+    alg = 128 * segs + 12 * pix + 1000
+    assert r["algorithmic_bytes_per_launch"] == alg and r["avg_launch_ms"] == 15.0 and r["devices"] == 2
+    assert r["achieved"] == pytest.approx(alg / 15e-3 / 1e9, rel=1e-4)
+    assert r["bound"] == "hbm" and r["frac"] == pytest.approx(r["achieved"] / 8000.0, rel=1e-4)
+    assert r["traffic"] is None and "valu" not in r  # no summary of this build
