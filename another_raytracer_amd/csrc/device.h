@@ -1210,8 +1210,11 @@ __device__ __forceinline__ bool hit_object(const DevScene<R>& S, const uint8_t* 
 
 // Out of line: measured +0.2 % (cow) to +1.8 % (Next-Week final) over the inlined body, which raised the register
 // pressure of the whole path loop for a function most segments do not reach.
+// ART_MEDIUM_FASTREJECT: hit_medium decides "no scatter" from an f32 log2 bound before the exact glibc log.  Exact
+// (the bound is far wider than v_log_f32's error) but measured -0.2 % (cow) to -1.2 % (dino) (r3k): a lane's
+// rejection skips nothing while any lane of its wave scatters, and nearly every wave has one.  Off.
 #ifndef ART_MEDIUM_FASTREJECT
-#define ART_MEDIUM_FASTREJECT 1  // hit_medium: decide "no scatter" from an f32 log2 bound before the exact glibc log
+#define ART_MEDIUM_FASTREJECT 0
 #endif
 static __device__ __noinline__ double glibc_log_call(double x) { return glibc_log(x); }
 // constant_medium.h:37-82.  Consumes one uniform when the clamped interval is non-empty.

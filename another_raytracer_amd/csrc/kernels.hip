@@ -364,17 +364,19 @@ __device__ __forceinline__ void gen_ray(const PassGeom& g, const CameraRec<R>& c
 
 // material.h scatter() for one hit of material type M (compile time: one shade kernel per material type, so a wave
 // never carries another material's code or registers); returns false when the path ends here.
+// pre: the lane's random_in_unit_sphere() draw, already taken by the wave (coop_unit_sphere), or null.
 template <class R, uint32_t M, uint32_t TF>
-__device__ __forceinline__ bool scatter(const DevScene<R>& S, const MatRec<R>& m, const Surf<R>& s, PathState<R>& st, V3<R>& att, V3<R>& dir) {
+__device__ __forceinline__ bool scatter(const DevScene<R>& S, const MatRec<R>& m, const Surf<R>& s, PathState<R>& st, V3<R>& att, V3<R>& dir,
+                                        const V3<R>* pre = nullptr) {
     if (M == MAT_LAMBERTIAN) {  // material.h:20-43
-        const V3<R> rv = unit(in_unit_sphere<R>(st.rng));
+        const V3<R> rv = unit(pre ? *pre : in_unit_sphere<R>(st.rng));
         dir = s.n + rv;
         if (near_zero(dir)) dir = s.n;
         att = tex_value<R, TF>(S, m.tex, s.u, s.v, s.p);
         return true;
     } else if (M == MAT_METAL) {  // material.h:45-61
         const V3<R> reflected = reflect(unit(st.ray.d), s.n);
-        dir = reflected + m.fuzz * in_unit_sphere<R>(st.rng);
+        dir = reflected + m.fuzz * (pre ? *pre : in_unit_sphere<R>(st.rng));
         att = ld3(m.albedo);
         return dot(dir, s.n) > R(0);
     } else if (M == MAT_DIELECTRIC) {  // material.h:63-99
@@ -394,7 +396,7 @@ __device__ __forceinline__ bool scatter(const DevScene<R>& S, const MatRec<R>& m
         dir = refl ? reflect(ud, s.n) : refract(ud, s.n, ratio);
         return true;
     } else if (M == MAT_ISOTROPIC) {  // material.h:120-135
-        dir = in_unit_sphere<R>(st.rng);
+        dir = pre ? *pre : in_unit_sphere<R>(st.rng);
         att = tex_value<R, TF>(S, m.tex, s.u, s.v, s.p);
         return true;
     }
@@ -927,6 +929,11 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S0, PassG
 #define ART_LDS_PARTIAL 1  // k_paths_g LM 2: the top BVH levels in LDS when the whole BVH does not fit
 #endif
 constexpr uint32_t kLdsPartialMinNodes = 64;
+#ifndef ART_COOP_SPHERE_G
+// k_paths_g: the wave-cooperative random_in_unit_sphere of k_paths (coop_unit_sphere) for lambertian, metal and
+// isotropic hits: measured +0.8 % (cow), +1.3 % (Next-Week final), +2.4 % (dino 4096^2) (r3k)
+#define ART_COOP_SPHERE_G 1
+#endif
 #ifndef ART_PATHS_G_WAVES
 #define ART_PATHS_G_WAVES 3  // 3 waves per SIMD (<= 168 VGPRs): measured best over 2 and 4 (cow +22 %, final +18 %, dino +21 % over 2)
 #endif
@@ -945,8 +952,8 @@ constexpr int kBlockM = 256 * ART_PATHS_G_WAVES;  // one LM block per CU at the 
 constexpr size_t kPathsGLdsCap = 160 * 1024;
 __host__ __device__ constexpr size_t align16(size_t x) { return (x + 15u) & ~size_t(15); }
 __host__ __device__ constexpr size_t paths_g_stack_bytes(uint32_t stack, int block) { return sizeof(StackT<false>) * stack * block; }
-__host__ __device__ constexpr size_t paths_g_head_bytes(uint32_t stack, int block) {  // stack, camera, pass geometry
-    return align16(paths_g_stack_bytes(stack, block) + sizeof(CameraRec<double>) + sizeof(PassGeom));
+__host__ __device__ constexpr size_t paths_g_head_bytes(uint32_t stack, int block) {  // stack, camera, pass geometry, jumps
+    return align16(paths_g_stack_bytes(stack, block) + sizeof(CameraRec<double>) + sizeof(PassGeom)) + (ART_COOP_SPHERE_G ? kJumpBytes : 0);
 }
 // LM kernels also hold the world list and the object records (a few KiB): every segment walks them, and a prim
 // object's test otherwise waits on three dependent L1 loads (world slot -> object -> primitive)
@@ -973,6 +980,8 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
         s_cam = cam;
         s_g = g;
     }
+    [[maybe_unused]] JumpEntry* jt = reinterpret_cast<JumpEntry*>(smem + align16(paths_g_stack_bytes(g.stack, B) + sizeof(CameraRec<double>) + sizeof(PassGeom)));
+    if (ART_COOP_SPHERE_G && threadIdx.x < static_cast<uint32_t>(kJumpEntries)) jt[threadIdx.x] = pcg_jump(3u * threadIdx.x);
     DevScene<double> S = S0;
     size_t lm_off = paths_g_head_bytes(g.stack, B);  // LM: world list and objects, then the BVH arrays
     if constexpr (LM != 0) {
@@ -1119,10 +1128,12 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
             continue;
         }
         const bool allow = SUSP && __ballot(drained) == 0;  // suspend only while there are paths to start
+        R t;
+        HitOut h{0, 0, kMatUnknown};
+        bool hitw = false, susp = false;
+        Surf<R> s;
+        [[maybe_unused]] uint32_t mtype = MAT_LIGHT;
         if (busy) {
-            R t;
-            HitOut h{0, 0, kMatUnknown};
-            bool cont = false;
             const bool fresh = !in_trace;
             if (fresh) {
                 ++segs;
@@ -1134,7 +1145,6 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
                        ART_DBITS(st.ray.o.y), ART_DBITS(st.ray.o.z), ART_DBITS(st.ray.d.x), ART_DBITS(st.ray.d.y), ART_DBITS(st.ray.d.z),
                        ART_DBITS(st.ray.tm), static_cast<unsigned long long>(st.rng));
 #endif
-            bool hitw;
             if constexpr (SUSP) {
                 ts.tr.allow = allow;
                 ts.tr.lanes = kSuspLanes;
@@ -1145,15 +1155,30 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
             } else {
                 hitw = trace_world<R, F, B, false, LM == 2>(S, nullptr, st.ray, stk, st.rng, t, h);
             }
-            const bool susp = in_trace;  // suspended: nothing to shade this round
+            susp = in_trace;  // suspended: nothing to shade this round
 #if ART_RAY_POOL_G
             __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring stores before the next round's loads
 #endif
             ART_TICK(tm_trace);
+            if (!susp && hitw) {
+                world_surface<R, F, (TF & TF_IMAGE) != 0>(S, h, st.ray, t, s);
+                mtype = S.mats[s.mat].type;
+            }
+        }
+#if ART_COOP_SPHERE_G
+        // the whole wave draws random_in_unit_sphere for its lambertian, metal and isotropic hits (material.h:33, :55,
+        // :129: each scatters with it first; metal's unit_vector draws nothing), as k_paths does
+        const bool need = busy && !susp && hitw && (mtype == MAT_LAMBERTIAN || mtype == MAT_METAL || mtype == MAT_ISOTROPIC) &&
+                          depth + 1 < max_depth;
+        const V3<R> ps = coop_unit_sphere<R>(need, st.rng, jt);
+        const V3<R>* pre = &ps;
+#else
+        const V3<R>* pre = nullptr;
+#endif
+        if (busy) {
+            bool cont = false;
             if (susp) {
             } else if (hitw) {
-                Surf<R> s;
-                world_surface<R, F, (TF & TF_IMAGE) != 0>(S, h, st.ray, t, s);
 #ifdef ART_TRACE
                 if (tracing)
                     printf("TRACE hit t=%016llx p=%016llx,%016llx,%016llx n=%016llx,%016llx,%016llx ff=%d mat=%d prim=%08x obj=%08x\n", ART_DBITS(t),
@@ -1167,10 +1192,10 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
                     V3<R> att, dir;
                     bool sc = false;
                     switch (mat.type) {
-                        case MAT_LAMBERTIAN: sc = scatter<R, MAT_LAMBERTIAN, TF>(S, mat, s, st, att, dir); break;
-                        case MAT_METAL: sc = scatter<R, MAT_METAL, TF>(S, mat, s, st, att, dir); break;
+                        case MAT_LAMBERTIAN: sc = scatter<R, MAT_LAMBERTIAN, TF>(S, mat, s, st, att, dir, pre); break;
+                        case MAT_METAL: sc = scatter<R, MAT_METAL, TF>(S, mat, s, st, att, dir, pre); break;
                         case MAT_DIELECTRIC: sc = scatter<R, MAT_DIELECTRIC, TF>(S, mat, s, st, att, dir); break;
-                        case MAT_ISOTROPIC: sc = scatter<R, MAT_ISOTROPIC, TF>(S, mat, s, st, att, dir); break;
+                        case MAT_ISOTROPIC: sc = scatter<R, MAT_ISOTROPIC, TF>(S, mat, s, st, att, dir, pre); break;
                         default: break;
                     }
                     if (sc) {
