@@ -382,15 +382,53 @@ __device__ __forceinline__ void box_face(const BoxRec<R>& b, int f, int& axis, R
     else if (pair == 1) { a0 = b.mn[0]; a1 = b.mx[0]; b0 = b.mn[2]; b1 = b.mx[2]; k = hi ? b.mx[1] : b.mn[1]; }
     else { a0 = b.mn[1]; a1 = b.mx[1]; b0 = b.mn[2]; b1 = b.mx[2]; k = hi ? b.mx[0] : b.mn[0]; }
 }
+// ART_BOX_RCP: a box's six plane distances (k - o) / d take one reciprocal per axis (two faces share it) and
+// div_rcp (Markstein: the division's bits for a normal divisor away from the extremes).  A component outside
+// [2^-500, 2^500] in magnitude -- in particular the +-0 of an axis-parallel ray, whose division gives +-inf or, for
+// k == o, the NaN the reference also carries (aarect.cpp) -- keeps the true division.
+#ifndef ART_BOX_RCP
+#define ART_BOX_RCP 1
+#endif
+template <class R>
+__device__ __forceinline__ bool hit_rect_inv(int axis, R a0, R a1, R b0, R b1, R k, const Ray<R>& r, R inv, bool use_inv, R tmin, R tmax, R& t) {
+    const int ka = axis == 0 ? 2 : (axis == 1 ? 1 : 0);
+    const int ia = axis == 2 ? 1 : 0;
+    const int ib = axis == 0 ? 1 : 2;
+    const R num = k - comp(r.o, ka), den = comp(r.d, ka);
+    const R tt = use_inv ? div_rcp(num, den, inv) : num / den;
+    if (tt < tmin || tt > tmax) return false;
+    const R x = comp(r.o, ia) + tt * comp(r.d, ia);
+    const R y = comp(r.o, ib) + tt * comp(r.d, ib);
+    if (x < a0 || x > a1 || y < b0 || y > b1) return false;
+    t = tt;
+    return true;
+}
 template <class R>
 __device__ __forceinline__ bool hit_box(const BoxRec<R>& b, const Ray<R>& r, R tmin, R tmax, R& t, uint32_t& face) {
     bool any = false;  // hittable_list semantics over the six sides: closest wins, a later equal t replaces
     R closest = tmax;
+#if ART_BOX_RCP
+    // face pair p (0: xy, k on z; 1: xz, k on y; 2: yz, k on x) divides by d.z, d.y, d.x
+    R inv[3];
+    bool ok[3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+        const R den = comp(r.d, p == 0 ? 2 : (p == 1 ? 1 : 0));
+        const R mag = __builtin_fabs(den);
+        ok[p] = mag > R(0x1p-500) && mag < R(0x1p500);
+        inv[p] = R(1) / (ok[p] ? den : R(1));
+    }
+#endif
     for (int f = 0; f < 6; ++f) {
         int axis;
         R a0, a1, b0, b1, k, tt;
         box_face(b, f, axis, a0, a1, b0, b1, k);
-        if (hit_rect(axis, a0, a1, b0, b1, k, r, tmin, closest, tt)) {
+#if ART_BOX_RCP
+        const bool h = hit_rect_inv(axis, a0, a1, b0, b1, k, r, inv[axis], ok[axis], tmin, closest, tt);
+#else
+        const bool h = hit_rect(axis, a0, a1, b0, b1, k, r, tmin, closest, tt);
+#endif
+        if (h) {
             any = true;
             closest = tt;
             face = static_cast<uint32_t>(f);
@@ -1213,6 +1251,9 @@ __device__ __forceinline__ bool hit_object(const DevScene<R>& S, const uint8_t* 
 // ART_MEDIUM_FASTREJECT: hit_medium decides "no scatter" from an f32 log2 bound before the exact glibc log.  Exact
 // (the bound is far wider than v_log_f32's error) but measured -0.2 % (cow) to -1.2 % (dino) (r3k): a lane's
 // rejection skips nothing while any lane of its wave scatters, and nearly every wave has one.  Off.
+#ifndef ART_MEDIUM_RCP
+#define ART_MEDIUM_RCP 1  // hit_medium (sphere boundary): the two root divisions through one reciprocal
+#endif
 #ifndef ART_MEDIUM_FASTREJECT
 #define ART_MEDIUM_FASTREJECT 0
 #endif
@@ -1242,7 +1283,24 @@ __device__ __forceinline__ bool hit_medium(const DevScene<R>& S, const uint8_t* 
         const R disc = half_b * half_b - a * c;
         if (disc < R(0)) return false;
         const R sqrtd = sqrt_rn(disc);
+#if ART_MEDIUM_RCP
+        // both roots through one reciprocal (div_rcp: Markstein's correctly rounded quotient, the division's bits for
+        // normal a, numerator and quotient; a = |d|^2 lies in [2^-46, 2^20] for every traced ray, the guard keeps the
+        // division for anything else, e.g. the 2^-72-probability zero direction of an isotropic draw).  A -0
+        // numerator gives +0 here and -0 from the division: t1 <= 0 is raised to tmin and t2 <= 0 fails below, so
+        // the sign of a zero root never reaches a result.
+        R r_near, r_far;
+        if (a > R(0x1p-500) && a < R(0x1p500)) {
+            const R inv_a = R(1) / a;
+            r_near = div_rcp(-half_b - sqrtd, a, inv_a);
+            r_far = div_rcp(-half_b + sqrtd, a, inv_a);
+        } else {
+            r_near = (-half_b - sqrtd) / a;
+            r_far = (-half_b + sqrtd) / a;
+        }
+#else
         const R r_near = (-half_b - sqrtd) / a, r_far = (-half_b + sqrtd) / a;
+#endif
         t1 = r_near;  // first call, t in [-inf, inf]
         if (t1 < -inf || inf < t1) {
             t1 = r_far;

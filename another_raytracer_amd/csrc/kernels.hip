@@ -364,25 +364,28 @@ __device__ __forceinline__ void gen_ray(const PassGeom& g, const CameraRec<R>& c
 
 // material.h scatter() for one hit of material type M (compile time: one shade kernel per material type, so a wave
 // never carries another material's code or registers); returns false when the path ends here.
-// pre: the lane's random_in_unit_sphere() draw, already taken by the wave (coop_unit_sphere), or null.
+// Shared steps already taken for the whole wave (k_paths_g), or null:
+//   pre    the lane's random_in_unit_sphere() draw (coop_unit_sphere);
+//   unitv  unit_vector of that draw (lambertian) or of the ray direction (metal, dielectric);
+//   texc   the material's texture value at the hit (lambertian, isotropic).
 template <class R, uint32_t M, uint32_t TF>
 __device__ __forceinline__ bool scatter(const DevScene<R>& S, const MatRec<R>& m, const Surf<R>& s, PathState<R>& st, V3<R>& att, V3<R>& dir,
-                                        const V3<R>* pre = nullptr) {
+                                        const V3<R>* pre = nullptr, const V3<R>* unitv = nullptr, const V3<R>* texc = nullptr) {
     if (M == MAT_LAMBERTIAN) {  // material.h:20-43
-        const V3<R> rv = unit(pre ? *pre : in_unit_sphere<R>(st.rng));
+        const V3<R> rv = unitv ? *unitv : unit(pre ? *pre : in_unit_sphere<R>(st.rng));
         dir = s.n + rv;
         if (near_zero(dir)) dir = s.n;
-        att = tex_value<R, TF>(S, m.tex, s.u, s.v, s.p);
+        att = texc ? *texc : tex_value<R, TF>(S, m.tex, s.u, s.v, s.p);
         return true;
     } else if (M == MAT_METAL) {  // material.h:45-61
-        const V3<R> reflected = reflect(unit(st.ray.d), s.n);
+        const V3<R> reflected = reflect(unitv ? *unitv : unit(st.ray.d), s.n);
         dir = reflected + m.fuzz * (pre ? *pre : in_unit_sphere<R>(st.rng));
         att = ld3(m.albedo);
         return dot(dir, s.n) > R(0);
     } else if (M == MAT_DIELECTRIC) {  // material.h:63-99
         att = mk(R(1), R(1), R(1));
         const R ratio = s.ff ? (R(1) / m.ir) : m.ir;
-        const V3<R> ud = unit(st.ray.d);
+        const V3<R> ud = unitv ? *unitv : unit(st.ray.d);
         const R cos_theta = fmin(dot(-ud, s.n), R(1));
         const R sin_theta = sqrt_rn(R(1) - cos_theta * cos_theta);
         const bool cannot = ratio * sin_theta > R(1);
@@ -397,7 +400,7 @@ __device__ __forceinline__ bool scatter(const DevScene<R>& S, const MatRec<R>& m
         return true;
     } else if (M == MAT_ISOTROPIC) {  // material.h:120-135
         dir = pre ? *pre : in_unit_sphere<R>(st.rng);
-        att = tex_value<R, TF>(S, m.tex, s.u, s.v, s.p);
+        att = texc ? *texc : tex_value<R, TF>(S, m.tex, s.u, s.v, s.p);
         return true;
     }
     return false;  // diffuse_light (material.h:106-110)
@@ -929,6 +932,9 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S0, PassG
 #define ART_LDS_PARTIAL 1  // k_paths_g LM 2: the top BVH levels in LDS when the whole BVH does not fit
 #endif
 constexpr uint32_t kLdsPartialMinNodes = 64;
+#ifndef ART_SHARED_SHADE_G
+#define ART_SHARED_SHADE_G 1  // k_paths_g with noise/image textures: texture value and unit_vector once per wave
+#endif
 #ifndef ART_COOP_SPHERE_G
 // k_paths_g: the wave-cooperative random_in_unit_sphere of k_paths (coop_unit_sphere) for lambertian, metal and
 // isotropic hits: measured +0.8 % (cow), +1.3 % (Next-Week final), +2.4 % (dino 4096^2) (r3k)
@@ -1186,16 +1192,32 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
                            static_cast<int>(s.mat), h.prim, h.obj);
 #endif
                 const MatRec<R>& mat = S.mats[s.mat];
+                // ART_SHARED_SHADE_G, in kernels with noise or image textures (where a texture value is costly): the
+                // steps several materials take, once for the wave instead of once per material branch present -- the
+                // texture value (diffuse_light, lambertian, isotropic: no draws) and one unit_vector (of the sphere
+                // draw for lambertian, of the ray direction for metal and dielectric).  Measured +1.3 % on the
+                // Next-Week final; with solid / checker textures only (cow, dino) the longer live ranges cost 1.5-2 %.
+                constexpr bool kShared = ART_SHARED_SHADE_G && ART_COOP_SPHERE_G && (TF & (TF_NOISE | TF_IMAGE)) != 0;
+                V3<R> texc = mk(R(0), R(0), R(0)), uv = mk(R(0), R(0), R(0));
+                if constexpr (kShared) {
+                    const bool scat = depth + 1 < max_depth;
+                    if (mat.type == MAT_LIGHT || (scat && (mat.type == MAT_LAMBERTIAN || mat.type == MAT_ISOTROPIC)))
+                        texc = tex_value<R, TF>(S, mat.tex, s.u, s.v, s.p);
+                    if (scat && (mat.type == MAT_LAMBERTIAN || mat.type == MAT_METAL || mat.type == MAT_DIELECTRIC))
+                        uv = unit(mat.type == MAT_LAMBERTIAN ? *pre : st.ray.d);
+                }
+                const V3<R>* texp = kShared ? &texc : nullptr;
+                const V3<R>* uvp = kShared ? &uv : nullptr;
                 if (mat.type == MAT_LIGHT) {  // material.h:114-116; diffuse_light never scatters
-                    st.L = st.L + st.T * tex_value<R, TF>(S, mat.tex, s.u, s.v, s.p);
+                    st.L = st.L + st.T * (texp ? *texp : tex_value<R, TF>(S, mat.tex, s.u, s.v, s.p));
                 } else if (depth + 1 < max_depth) {
                     V3<R> att, dir;
                     bool sc = false;
                     switch (mat.type) {
-                        case MAT_LAMBERTIAN: sc = scatter<R, MAT_LAMBERTIAN, TF>(S, mat, s, st, att, dir, pre); break;
-                        case MAT_METAL: sc = scatter<R, MAT_METAL, TF>(S, mat, s, st, att, dir, pre); break;
-                        case MAT_DIELECTRIC: sc = scatter<R, MAT_DIELECTRIC, TF>(S, mat, s, st, att, dir); break;
-                        case MAT_ISOTROPIC: sc = scatter<R, MAT_ISOTROPIC, TF>(S, mat, s, st, att, dir, pre); break;
+                        case MAT_LAMBERTIAN: sc = scatter<R, MAT_LAMBERTIAN, TF>(S, mat, s, st, att, dir, pre, uvp, texp); break;
+                        case MAT_METAL: sc = scatter<R, MAT_METAL, TF>(S, mat, s, st, att, dir, pre, uvp); break;
+                        case MAT_DIELECTRIC: sc = scatter<R, MAT_DIELECTRIC, TF>(S, mat, s, st, att, dir, nullptr, uvp); break;
+                        case MAT_ISOTROPIC: sc = scatter<R, MAT_ISOTROPIC, TF>(S, mat, s, st, att, dir, pre, nullptr, texp); break;
                         default: break;
                     }
                     if (sc) {
