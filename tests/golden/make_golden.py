@@ -12,8 +12,8 @@ fixtures pin:
                        scene build incl. BVH-build draws) and the sha256 of the canonical scene dump
   * render_<scene>.npz reference renders (engine_mode::single semantics): RGB8, f64 per-pixel sums and the
                        exact segment count (world.hit calls)
-  * render_stat_<scene>_384x216x<spp>.npz  the headline scene (alias 1, 16 spp), the cow mesh scene (16 spp) and the
-                       Next-Week final (alias 8, 32 spp) rendered by the reference twice with independent sample
+  * render_stat_<scene>_384x216x<spp>.npz  the headline scene (alias 1, 16 spp), the cow and dino mesh scenes (16 spp)
+                       and the Next-Week final (alias 8, 32 spp) rendered by the reference twice with independent sample
                        sequences -- engine_mode::single, and parallel_stripes with 4 threads (its shared global RNG)
                        -- for the statistical parity test of the f64 GPU path (SURVEY.md §8(d) tolerance 3: the
                        pair's RMSE is the noise floor); `make_golden.py stat [scene ...]` makes only these
@@ -88,7 +88,7 @@ def images_mode_fixtures():
         print("images", sc, info)
 
 
-STAT = [("1", 384, 216, 16), ("cow", 384, 216, 16), ("8", 384, 216, 32)]
+STAT = [("1", 384, 216, 16), ("cow", 384, 216, 16), ("8", 384, 216, 32), ("dino", 384, 216, 16)]
 
 
 def stat_fixtures(only=None):

@@ -157,7 +157,8 @@ def _rmse(a, b):
     return float(np.sqrt(np.mean((a.astype(np.float64) - b.astype(np.float64)) ** 2)))
 
 
-STAT = {"1": "render_stat_1_384x216x16.npz", "cow": "render_stat_cow_384x216x16.npz", "8": "render_stat_8_384x216x32.npz"}
+STAT = {"1": "render_stat_1_384x216x16.npz", "cow": "render_stat_cow_384x216x16.npz", "8": "render_stat_8_384x216x32.npz",
+        "dino": "render_stat_dino_384x216x16.npz"}
 
 
 @pytest.mark.parametrize("seed", [0, 1])

@@ -158,7 +158,7 @@ def _rmse(a, b):
 
 
 @pytest.mark.parametrize("scene,fixture", [("1", "render_stat_1_384x216x16.npz"), ("cow", "render_stat_cow_384x216x16.npz"),
-                                           ("8", "render_stat_8_384x216x32.npz")])
+                                           ("8", "render_stat_8_384x216x32.npz"), ("dino", "render_stat_dino_384x216x16.npz")])
 def test_pcg_mode_is_statistically_the_reference(scene, fixture):
     """The pcg mode (the GPU's RNG contract; the GPU equals it bit for bit) against the reference program's own
     renders with independent sample sequences (its single and 4-thread stripes renders): the same SURVEY §8(d)
