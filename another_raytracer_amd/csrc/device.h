@@ -386,8 +386,10 @@ __device__ __forceinline__ void box_face(const BoxRec<R>& b, int f, int& axis, R
 // div_rcp (Markstein: the division's bits for a normal divisor away from the extremes).  A component outside
 // [2^-500, 2^500] in magnitude -- in particular the +-0 of an axis-parallel ray, whose division gives +-inf or, for
 // k == o, the NaN the reference also carries (aarect.cpp) -- keeps the true division.
+// Measured (r3j, A/B with ART_MEDIUM_RCP on the same build): the two reciprocal variants together cost cow 1.9 % and
+// the Next-Week final 0.3 % (the guarded reciprocal's extra compare/select and registers outweigh the divisions): off.
 #ifndef ART_BOX_RCP
-#define ART_BOX_RCP 1
+#define ART_BOX_RCP 0
 #endif
 template <class R>
 __device__ __forceinline__ bool hit_rect_inv(int axis, R a0, R a1, R b0, R b1, R k, const Ray<R>& r, R inv, bool use_inv, R tmin, R tmax, R& t) {
@@ -1252,7 +1254,7 @@ __device__ __forceinline__ bool hit_object(const DevScene<R>& S, const uint8_t* 
 // (the bound is far wider than v_log_f32's error) but measured -0.2 % (cow) to -1.2 % (dino) (r3k): a lane's
 // rejection skips nothing while any lane of its wave scatters, and nearly every wave has one.  Off.
 #ifndef ART_MEDIUM_RCP
-#define ART_MEDIUM_RCP 1  // hit_medium (sphere boundary): the two root divisions through one reciprocal
+#define ART_MEDIUM_RCP 0  // hit_medium (sphere boundary): the two root divisions through one reciprocal (r3j: off, see ART_BOX_RCP)
 #endif
 #ifndef ART_MEDIUM_FASTREJECT
 #define ART_MEDIUM_FASTREJECT 0

@@ -4,6 +4,7 @@
 #   calib                       tools/valu_calib (VALU issue-cost calibration, plain run)
 #   uvcheck                     tools/uv_check (device vs glibc get_sphere_uv texel choice) -> gpurun_out/uv_check.json
 #   ab:LIB1,LIB2[:ARGS]         tools/ab_quick.sh over in-tree libart builds (bench.py ARGS, default --spp 256)
+#   abenv:ARGS:V1+V2+...        tools/ab_env.sh over LIB[@VAR=VAL,...] variants (bench.py ARGS)
 #   pmc:TAG:SCENE[:SPP]         tools/pmc.sh counter passes + kernel trace of the current libart (ART_LIB honoured)
 #   bench:TAG[:ARGS]            bench.py line -> gpurun_out/bench_TAG.log
 #   prof:TAG[:ARGS]             rocprofv3 --kernel-trace --stats of a bench run -> gpurun_out/prof_TAG
@@ -34,6 +35,8 @@ for step in "$@"; do
       cat gpurun_out/uv_check.json ;;
     ab)
       LIBS="${a//,/ }" ARGS="${b:---spp 256}" bash tools/ab_quick.sh || exit 1 ;;
+    abenv)
+      ARGS="$a" bash tools/ab_env.sh ${b//+/ } || exit 1 ;;
     pmc)
       spp=${c:-64}
       PMC_GROUPS="$PMC_ALL" TAG=$a SCENE=$b SPP=$spp bash tools/pmc.sh || exit 1
