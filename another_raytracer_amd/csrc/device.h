@@ -671,6 +671,9 @@ __device__ __forceinline__ void stat_lane(int k) { atomicAdd(&g_art_stats[k], 1u
 #ifndef ART_PARK_PREFETCH
 #define ART_PARK_PREFETCH 0  // 1: the node loop reads the entry under the stack top with the top (-1.4 %)
 #endif
+#ifndef ART_SORT_PARTIAL
+#define ART_SORT_PARTIAL 0  // LDS variant: 4-key sorting network without its last exchange (2 fewer VALU per visit)
+#endif
 #ifndef ART_LEAFSEL_BRANCHLESS
 #define ART_LEAFSEL_BRANCHLESS 1  // LDS variant, leaf-phase entry: one stack read up front, selects instead of branches
 #endif
@@ -975,7 +978,9 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                 ucas(q2, q3);
                 ucas(q0, q2);
                 ucas(q1, q3);
-                ucas(q1, q2);
+                // ART_SORT_PARTIAL: without the last exchange q1 / q2 (the 2nd and 3rd nearest) may be pushed in either
+                // order; q0 (the next node) and q3 (the farthest) are exact
+                if (!ART_SORT_PARTIAL) ucas(q1, q2);
                 if (q0 >= kKeyMiss) ART_STAT_LANE(12);  // a dead visit: no child box is entered before tmax
                 st.push(static_cast<int32_t>(q3), q3 < kKeyMiss);
                 st.push(static_cast<int32_t>(q2), q2 < kKeyMiss);

@@ -670,7 +670,14 @@ constexpr uint32_t kPathChunk = 256;
 #ifndef ART_RAY_POOL_G
 #define ART_RAY_POOL_G 0  // the same ring in k_paths_g: measured -1 % to -4 % (cow, final, dino, capsule, scene 7)
 #endif
-constexpr uint32_t kPoolRing = 128;  // two batches of 64
+// ART_POOL_RING: ring entries per wave.  128: two batches of 64, refilled when a batch's worth is free, so a round's
+// takers always find entries; 96 (a 25 % smaller ring footprint in L2): refilled when at most 32 are left, so a round
+// with more takers than entries leaves the rest idle for that round.
+#ifndef ART_POOL_RING
+#define ART_POOL_RING 128
+#endif
+constexpr uint32_t kPoolRing = ART_POOL_RING;
+static_assert(kPoolRing >= 96 && kPoolRing <= 128, "a ring holds the unread part of one batch and a whole new one");
 constexpr uint32_t kPoolWavesPerCu = 32;  // rings allocated per CU: the most waves a CU holds
 struct PoolRay {
     double ox, oy, oz, dx;
@@ -723,7 +730,8 @@ struct RayRing {
     __device__ __forceinline__ int take(uint32_t rank, uint32_t P, PathState<double>& st, uint32_t& q) const {
         const uint32_t pos = head + rank;
         const uint32_t slot = (((pos / 64u) & 1u) ? base1 : base0) + pos % 64u;
-        if (pos >= tail || slot >= P) return 2;
+        if (pos >= tail) return exhausted ? 2 : 0;  // 0: the ring ran dry this round (kPoolRing < 128 only)
+        if (slot >= P) return 2;
         const PoolRay& e = ring[pos % kPoolRing];
         const double tm = e.tm;
         if (tm != tm) return 0;
@@ -740,11 +748,11 @@ struct RayRing {
     // least one round after its stores (ordered by the s_waitcnt vmcnt(0) the path loops place after the trace)
     __device__ __forceinline__ void advance(uint32_t n, const PassGeom& sg, const CameraRec<double>& sc, uint32_t* next_slot, uint32_t lane) {
         head = min(head + n, tail);
-        if (!exhausted && tail - head <= 64u) refill(sg, sc, next_slot, lane);
+        if (!exhausted && tail - head <= kPoolRing - 64u) refill(sg, sc, next_slot, lane);
     }
     __device__ __forceinline__ void start(const PassGeom& sg, const CameraRec<double>& sc, uint32_t* next_slot, uint32_t lane) {
         refill(sg, sc, next_slot, lane);
-        if (!exhausted) refill(sg, sc, next_slot, lane);
+        if (kPoolRing >= 128 && !exhausted) refill(sg, sc, next_slot, lane);
         __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
 };

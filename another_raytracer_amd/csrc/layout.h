@@ -103,7 +103,13 @@ constexpr int kMaxStackDepth = 64;   // per-lane LDS traversal stack entries (si
 #ifndef ART_LDS_MOTION
 #define ART_LDS_MOTION 0
 #endif
-constexpr uint32_t kLdsNodeCap = 320;  // the random scene: 259 nodes (its SAH tree without the hoisted ground sphere)
+// LDS node capacity: the random scene's tree without the hoisted ground sphere has 259 nodes (greedy collapse, bvh.cpp;
+// 223 with ART_BVH_COLLAPSE=1).  Every plane stays a multiple of 256 B (bank 0); the 7.5 KiB saved against a 320 cap
+// leave room for deeper traversal stacks (the optimal collapse's tree needs 18 entries instead of 15)
+#ifndef ART_LDS_NODE_CAP
+#define ART_LDS_NODE_CAP 272
+#endif
+constexpr uint32_t kLdsNodeCap = ART_LDS_NODE_CAP;
 constexpr uint32_t kLdsNodePlanes = ART_LDS_MOTION ? 13 : 10;
 constexpr uint32_t kLdsNodePlaneChild = 9;
 constexpr uint32_t kLdsNodePlaneMotion = 10;  // dlo y, dhi y, dlo y
