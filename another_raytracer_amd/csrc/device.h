@@ -645,7 +645,7 @@ __device__ __forceinline__ bool hit_lds_slot(const uint8_t* lds, uint32_t slot, 
 // Divergence statistics (diagnostic builds only): [0] node-loop wave iterations, [1] node visits (lane sum), [2] leaf-
 // loop wave iterations, [3] leaf tests (lane sum), [4] outer-loop wave iterations, [5] outer iterations (lane sum),
 // [6] traversals, [7] hit_sphere tests with disc >= 0.
-__device__ unsigned long long g_art_stats[16];
+__device__ unsigned long long g_art_stats[24];
 __device__ __forceinline__ void stat_wave(int k) {
     const uint64_t m = __ballot(true);
     if (static_cast<int>(__lane_id()) == __ffsll(static_cast<long long>(m)) - 1) atomicAdd(&g_art_stats[k], 1ull);
@@ -1172,6 +1172,15 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                     ref = S.primrefs[slot];
                     h = hit_prim<R, F>(S, ref, r, tmin, tmax, tt, fc);
                 }
+#ifdef ART_STATS
+                {  // leaf tests by primitive type: lane tests [15/17/19/21], wave iterations running that type [16/18/20/22]
+                    const uint32_t ty = primref_type(ref);
+                    if (ty == PRIM_BOX) { ART_STAT_WAVE(16); ART_STAT_LANE(15); }
+                    else if (ty == PRIM_SPHERE) { ART_STAT_WAVE(18); ART_STAT_LANE(17); }
+                    else if (ty == PRIM_TRIANGLE) { ART_STAT_WAVE(20); ART_STAT_LANE(19); }
+                    else { ART_STAT_WAVE(22); ART_STAT_LANE(21); }
+                }
+#endif
             }
             if (h) {
                 ART_STAT_LANE(13);

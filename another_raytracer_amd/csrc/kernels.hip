@@ -671,13 +671,22 @@ constexpr uint32_t kPathChunk = 256;
 #define ART_RAY_POOL_G 0  // the same ring in k_paths_g: measured -1 % to -4 % (cow, final, dino, capsule, scene 7)
 #endif
 // ART_POOL_RING: ring entries per wave.  128: two batches of 64, refilled when a batch's worth is free, so a round's
-// takers always find entries; 96 (a 25 % smaller ring footprint in L2): refilled when at most 32 are left, so a round
-// with more takers than entries leaves the rest idle for that round.
+// takers always find entries; 96 (default): refilled when at most 32 are left, so a round with more takers than
+// entries leaves the rest idle for that round.  Measured (r3m, scene 1, PMC per segment; XCD-contiguous rings): HBM
+// reads 3.50 B (128) -> 0.10 B (96), writes 33.5 -> 27.9 B: the 3 MiB of rings per XCD stay in its 4 MiB L2 between a
+// refill and the takes (the writes left are the 8.9 B of radiance records and dirty ring lines evicted between
+// laps); Msamples/s +0.4 % (within the run-to-run spread).
 #ifndef ART_POOL_RING
-#define ART_POOL_RING 128
+#define ART_POOL_RING 96
 #endif
 constexpr uint32_t kPoolRing = ART_POOL_RING;
 static_assert(kPoolRing >= 96 && kPoolRing <= 128, "a ring holds the unread part of one batch and a whole new one");
+// ART_RING_XCD (default 1): measured (r3m, 128-entry rings) HBM reads 11.3 -> 3.5 B per segment against the
+// block-major layout, Msamples/s unchanged
+#ifndef ART_RING_XCD
+#define ART_RING_XCD 1
+#endif
+constexpr uint32_t kXcds = 8;  // MI355X
 constexpr uint32_t kPoolWavesPerCu = 32;  // rings allocated per CU: the most waves a CU holds
 struct PoolRay {
     double ox, oy, oz, dx;
@@ -692,7 +701,15 @@ struct RayRing {
     uint32_t base0, base1;  // first slot of the batch in ring half 0 / 1
     uint32_t cur, end;      // the wave's claimed slot chunk [cur, end)
     bool exhausted;         // every slot of the pass is in a batch
-    __device__ __forceinline__ void init(void* pool, uint32_t wave) {
+    // wave w of block b: the rings of one XCD's blocks are contiguous (ART_RING_XCD; blocks go to the 8 XCDs round
+    // robin, block b to XCD b % 8), so each XCD's rings spread over all of its L2's sets instead of every block's
+    // chunk landing on the same sets (block-major rings of one XCD lie 8 chunks apart: a power-of-two stride)
+    __device__ __forceinline__ void init(void* pool, uint32_t block, uint32_t nblocks, uint32_t waves_per_block, uint32_t w) {
+        uint32_t wave = block * waves_per_block + w;
+        if (ART_RING_XCD) {
+            const uint32_t per_xcd = (nblocks + kXcds - 1) / kXcds;
+            wave = ((block % kXcds) * per_xcd + block / kXcds) * waves_per_block + w;
+        }
         ring = static_cast<PoolRay*>(pool) + static_cast<size_t>(wave) * kPoolRing;
         head = tail = base0 = base1 = cur = end = 0;
         exhausted = false;
@@ -817,7 +834,7 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S0, PassG
 #endif
 #if ART_RAY_POOL
     RayRing rr;
-    rr.init(w.pool, blockIdx.x * (B / 64) + threadIdx.x / 64);
+    rr.init(w.pool, blockIdx.x, gridDim.x, B / 64, threadIdx.x / 64);
     rr.start(s_g, s_cam, next_slot, lane);
 #endif
     for (;;) {
@@ -1076,7 +1093,7 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
 #endif
 #if ART_RAY_POOL_G
     RayRing rr;
-    rr.init(w.pool, blockIdx.x * (B / 64) + threadIdx.x / 64);
+    rr.init(w.pool, blockIdx.x, gridDim.x, B / 64, threadIdx.x / 64);
     rr.start(s_g, s_cam, next_slot, lane);
 #endif
     for (;;) {
@@ -2179,7 +2196,8 @@ static int extend_variant(const DeviceScene<R>& ds, int flags) {
 }
 // The persistent kernels' waves index the camera-ray rings (kPoolWavesPerCu per CU allocated)
 static void check_ring_waves(int blocks, int block, int num_cu) {
-    if (static_cast<size_t>(blocks) * static_cast<size_t>(block / 64) > static_cast<size_t>(num_cu) * kPoolWavesPerCu)
+    const size_t padded = (static_cast<size_t>(blocks) + kXcds - 1) / kXcds * kXcds;  // RayRing::init's XCD-major index
+    if (padded * static_cast<size_t>(block / 64) > static_cast<size_t>(num_cu) * kPoolWavesPerCu)
         throw std::runtime_error("internal: persistent grid larger than the camera-ray rings");
 }
 template <uint32_t F, uint32_t TF>
@@ -2512,7 +2530,7 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     HIP_OK(hipGetLastError());
 #ifdef ART_STATS
     {
-        unsigned long long st[16] = {0};
+        unsigned long long st[24] = {0};
         HIP_OK(hipStreamSynchronize(stream));
         HIP_OK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_art_stats), sizeof st));
         std::fprintf(stderr, "ART_STATS node_w %llu node_l %llu (util %.3f) leaf_w %llu leaf_l %llu (util %.3f) outer_w %llu outer_l %llu (util %.3f) "
@@ -2522,6 +2540,9 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
         std::fprintf(stderr, "ART_STATS dead node visits (LDS scene) %llu (%.3f of visits), stale visits (box entered beyond tmax) %llu (%.3f), "
                      "leaf tests that shorten tmax %llu (%.3f of tests)\n",
                      st[12], double(st[12]) / st[1], st[14], double(st[14]) / st[1], st[13], double(st[13]) / st[3]);
+        if (st[15] + st[17] + st[19] + st[21] > 0)
+            std::fprintf(stderr, "ART_STATS leaf tests by type (lane tests, wave iterations running it): box %llu %llu sphere %llu %llu triangle %llu %llu rect %llu %llu\n",
+                         st[15], st[16], st[17], st[18], st[19], st[20], st[21], st[22]);
         const double tt = double(st[8] + st[9] + st[10] + st[11]);
         if (tt > 0) std::fprintf(stderr, "ART_STATS cycles: load/claim %.3f trace %.3f shade %.3f append/store %.3f\n", st[8] / tt, st[9] / tt, st[10] / tt, st[11] / tt);
         std::memset(st, 0, sizeof st);
