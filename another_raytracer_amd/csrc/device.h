@@ -443,8 +443,8 @@ __device__ __forceinline__ bool hit_box(const BoxRec<R>& b, const Ray<R>& r, R t
 // The test of a primitive given its record (a prim object's copy, DevScene::obj_prims): the same arithmetic as hit_prim.
 template <class R, uint32_t F>
 __device__ __forceinline__ bool hit_prim_rec(uint32_t type, const PrimRec80& rec, const Ray<R>& r, R tmin, R tmax, R& t, uint32_t& face) {
-    if ((F & F_SPHERE) && (F == F_SPHERE || type == PRIM_SPHERE)) return hit_sphere(reinterpret_cast<const SphereRec<R>&>(rec), r, tmin, tmax, t);
-    if ((F & F_TRI) && (F == F_TRI || type == PRIM_TRIANGLE)) return hit_tri(reinterpret_cast<const TriRec<R>&>(rec), r, tmin, tmax, t);
+    if ((F & F_SPHERE) && (fbase(F) == F_SPHERE || type == PRIM_SPHERE)) return hit_sphere(reinterpret_cast<const SphereRec<R>&>(rec), r, tmin, tmax, t);
+    if ((F & F_TRI) && (fbase(F) == F_TRI || type == PRIM_TRIANGLE)) return hit_tri(reinterpret_cast<const TriRec<R>&>(rec), r, tmin, tmax, t);
     if ((F & F_RECT) && type == PRIM_RECT) {
         const RectRec<R>& q = reinterpret_cast<const RectRec<R>&>(rec);
         return hit_rect(static_cast<int>(q.axis), q.a0, q.a1, q.b0, q.b1, q.k, r, tmin, tmax, t);
@@ -458,8 +458,8 @@ template <class R, uint32_t F>
 __device__ __forceinline__ bool hit_prim(const DevScene<R>& S, uint32_t ref, const Ray<R>& r, R tmin, R tmax, R& t, uint32_t& face) {
     const uint32_t idx = primref_index(ref);
     const uint32_t type = primref_type(ref);
-    if ((F & F_SPHERE) && (F == F_SPHERE || type == PRIM_SPHERE)) return hit_sphere(S.spheres[idx], r, tmin, tmax, t);
-    if ((F & F_TRI) && (F == F_TRI || type == PRIM_TRIANGLE)) return hit_tri(S.tris[idx], r, tmin, tmax, t);
+    if ((F & F_SPHERE) && (fbase(F) == F_SPHERE || type == PRIM_SPHERE)) return hit_sphere(S.spheres[idx], r, tmin, tmax, t);
+    if ((F & F_TRI) && (fbase(F) == F_TRI || type == PRIM_TRIANGLE)) return hit_tri(S.tris[idx], r, tmin, tmax, t);
     if ((F & F_RECT) && type == PRIM_RECT) {
         const RectRec<R>& q = S.rects[idx];
         return hit_rect(static_cast<int>(q.axis), q.a0, q.a1, q.b0, q.b1, q.k, r, tmin, tmax, t);
@@ -584,6 +584,24 @@ __device__ __forceinline__ void slab4_packed(const float4& lx, const float4& hx,
     q2 = slab_key_packed(x0b.x, x1b.x, y0b.x, y1b.x, z0b.x, z1b.x, ch.z, tminf, tmaxf);
     q3 = slab_key_packed<ART_CHILD16 != 0>(x0b.y, x1b.y, y0b.y, y1b.y, z0b.y, z1b.y, ch.w, tminf, tmaxf);
 }
+// The HBM-scene traversal's packed keys (PK): near/far planes as slab4_nf, keys as slab_key_packed (the 16-bit codes of
+// children 1 and 3 in the high halves of ch.y / ch.w, as the LDS image's)
+__device__ __forceinline__ void slab4_packed_nf(const float4& lx, const float4& hx, const float4& ly, const float4& hy, const float4& lz,
+                                                const float4& hz, const int4& ch, float ix, float iy, float iz, float oix, float oiy, float oiz,
+                                                float tminf, float tmaxf, uint32_t& q0, uint32_t& q1, uint32_t& q2, uint32_t& q3) {
+    const f2v vx = {ix, ix}, vy = {iy, iy}, vz = {iz, iz};
+    const f2v nx = {-oix, -oix}, ny = {-oiy, -oiy}, nz = {-oiz, -oiz};
+    const f2v x0a = __builtin_elementwise_fma(f2v{lx.x, lx.y}, vx, nx), x0b = __builtin_elementwise_fma(f2v{lx.z, lx.w}, vx, nx);
+    const f2v x1a = __builtin_elementwise_fma(f2v{hx.x, hx.y}, vx, nx), x1b = __builtin_elementwise_fma(f2v{hx.z, hx.w}, vx, nx);
+    const f2v y0a = __builtin_elementwise_fma(f2v{ly.x, ly.y}, vy, ny), y0b = __builtin_elementwise_fma(f2v{ly.z, ly.w}, vy, ny);
+    const f2v y1a = __builtin_elementwise_fma(f2v{hy.x, hy.y}, vy, ny), y1b = __builtin_elementwise_fma(f2v{hy.z, hy.w}, vy, ny);
+    const f2v z0a = __builtin_elementwise_fma(f2v{lz.x, lz.y}, vz, nz), z0b = __builtin_elementwise_fma(f2v{lz.z, lz.w}, vz, nz);
+    const f2v z1a = __builtin_elementwise_fma(f2v{hz.x, hz.y}, vz, nz), z1b = __builtin_elementwise_fma(f2v{hz.z, hz.w}, vz, nz);
+    q0 = slab_key_packed(x0a.x, x1a.x, y0a.x, y1a.x, z0a.x, z1a.x, ch.x, tminf, tmaxf);
+    q1 = slab_key_packed<true>(x0a.y, x1a.y, y0a.y, y1a.y, z0a.y, z1a.y, ch.y, tminf, tmaxf);
+    q2 = slab_key_packed(x0b.x, x1b.x, y0b.x, y1b.x, z0b.x, z1b.x, ch.z, tminf, tmaxf);
+    q3 = slab_key_packed<true>(x0b.y, x1b.y, y0b.y, y1b.y, z0b.y, z1b.y, ch.w, tminf, tmaxf);
+}
 __device__ __forceinline__ void ucas(uint32_t& a, uint32_t& b) {
     const uint32_t lo = a < b ? a : b;
     b = a < b ? b : a;
@@ -704,6 +722,11 @@ __device__ __forceinline__ float4 lds_f4(uint32_t addr) {
     const f4v v = *(__attribute__((address_space(3))) const f4v*)(size_t)addr;
     return make_float4(v.x, v.y, v.z, v.w);
 }
+__device__ __forceinline__ uint2 lds_u2(uint32_t addr) {
+    typedef unsigned u2v_t __attribute__((ext_vector_type(2)));
+    const u2v_t v = *(__attribute__((address_space(3))) const u2v_t*)(size_t)addr;
+    return make_uint2(v.x, v.y);
+}
 __device__ __forceinline__ int4 lds_i4(uint32_t addr) {
     const i4v v = *(__attribute__((address_space(3))) const i4v*)(size_t)addr;
     return make_int4(v.x, v.y, v.z, v.w);
@@ -735,6 +758,34 @@ struct LaneStack<B, true> {  // LDS-scene variant: 16-bit entries, tracked as th
     // the next walk starts from a fresh LaneStack.
     __device__ __forceinline__ void pop_if(bool c) { top -= c ? kRow : 0u; }
 };
+#ifndef ART_STACK_ADDR_G
+// 32-bit stacks tracked by the LDS byte address of their top entry, as LaneStack<B, true> (a push or pop is one
+// select + add instead of a 64-bit multiply-add of the depth for every access); 0: tracked by depth
+#define ART_STACK_ADDR_G 1
+#endif
+#if ART_STACK_ADDR_G
+template <int B>
+struct LaneStack<B, false> {  // 32-bit entries; `top` is the LDS byte address of the top entry (the sentinel when empty)
+    static constexpr uint32_t kRow = 4u * B;
+    uint32_t bottom, top;
+    __device__ __forceinline__ explicit LaneStack(int32_t* stk)
+        : bottom(static_cast<uint32_t>(reinterpret_cast<size_t>((__attribute__((address_space(3))) int32_t*)stk)) - kRow), top(bottom) {}
+    __device__ __forceinline__ void push(int32_t v, bool keep) {
+        *(__attribute__((address_space(3))) int32_t*)(size_t)(top + kRow) = v;
+        top += keep ? kRow : 0u;
+    }
+    __device__ __forceinline__ int32_t peek() const { return *(__attribute__((address_space(3))) const int32_t*)(size_t)top; }
+#if ART_POP_GUARD_G
+    __device__ __forceinline__ void pop_if(bool c) { top -= (c && top != bottom) ? kRow : 0u; }
+#else
+    // no empty-stack guard: a walk that pops the sentinel's kNodeEmpty ends without reading on
+    __device__ __forceinline__ void pop_if(bool c) { top -= c ? kRow : 0u; }
+#endif
+    // the resumable traversal (TravResume) keeps the top address: the stack stays in this lane's LDS column
+    __device__ __forceinline__ uint32_t save() const { return top; }
+    __device__ __forceinline__ void restore(uint32_t t) { top = t; }
+};
+#else
 template <int B>
 struct LaneStack<B, false> {  // 32-bit entries
     int32_t* stk;
@@ -751,7 +802,10 @@ struct LaneStack<B, false> {  // 32-bit entries
     // no empty-stack guard, as LaneStack<B, true>: a walk that pops the sentinel's kNodeEmpty ends without reading on
     __device__ __forceinline__ void pop_if(bool c) { sp -= c ? 1 : 0; }
 #endif
+    __device__ __forceinline__ uint32_t save() const { return static_cast<uint32_t>(sp); }
+    __device__ __forceinline__ void restore(uint32_t t) { sp = static_cast<int>(t); }
 };
+#endif
 // Traversal stack entry: node/leaf codes, 16 bits in the LDS-scene variant (layout.h lds_leaf), 32 bits otherwise.
 template <bool L> using StackT = typename std::conditional<L, int16_t, int32_t>::type;
 #ifndef ART_STACK_SWZ
@@ -784,7 +838,8 @@ __device__ __forceinline__ float f32_dir(double d) {
 #define ART_SUSPEND_LANES 24  // measured over 8-40 on cow and the capsule (24: +8 %; 8: +4 %; 40: +7 %)
 #endif
 struct TravResume {
-    int32_t node, parked, sp;
+    int32_t node, parked;
+    uint32_t sp;  // LaneStack::save(): the top entry's LDS address (ART_STACK_ADDR_G) or the depth
     int32_t lanes;  // suspend when fewer lanes of the wave are traversing
     bool fresh;     // no traversal in progress: start at the root
     bool allow;     // wave-uniform: suspending is allowed in this round (paths remain to be started)
@@ -833,6 +888,11 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
     // L: inner nodes are coded by their byte offset in a node plane (index * 16, layout.h), so a visit's plane
     // addresses are one add each
     static_assert(kLdsNodeCap * 16 <= 32767, "LDS inner-node codes are 16-bit stack entries");
+    // PK (k_paths_g instantiations with F_CODE16): the HBM-scene traversal sorts packed keys as the LDS variant does,
+    // with the node's 16-bit child codes (BvhNode::pad, layout.h make_leaf16) in the low half of each key; codes,
+    // stack entries and leaves are then in the 16-bit form throughout the walk
+    constexpr bool PK = !L && (F & F_CODE16) != 0;
+    static_assert(!PK || (F & F_MEDIA_G) == 0, "packed keys need tmin > 0: no medium boundary traversals");
     const int32_t root_code = L ? root * 16 : root;
     int32_t node = root_code;
 #ifdef ART_STATS
@@ -860,7 +920,7 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
     // (popped before any other push: no extra stack depth).
     [[maybe_unused]] bool skip_nodes = false;
     if (hoisted != kNodeEmpty && (!RES || rs->fresh)) {
-        const int32_t h = L ? lds_leaf(leaf_first(hoisted), leaf_count(hoisted)) : hoisted;
+        const int32_t h = L ? lds_leaf(leaf_first(hoisted), leaf_count(hoisted)) : PK ? make_leaf16(leaf_first(hoisted), leaf_count(hoisted)) : hoisted;
 #if ART_SPECULATIVE
         parked = h;
         skip_nodes = true;
@@ -873,7 +933,7 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
         if (!rs->fresh) {
             node = rs->node;
             parked = rs->parked;
-            st.sp = rs->sp;
+            st.restore(rs->sp);
         }
     }
     [[maybe_unused]] bool progressed = false;
@@ -883,7 +943,7 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
             if (rs->allow && progressed && __popcll(__ballot(true)) < rs->lanes) {
                 rs->node = node;
                 rs->parked = parked;
-                rs->sp = st.sp;
+                rs->sp = st.save();
                 rs->fresh = false;
                 rs->suspended = true;
                 return hit;
@@ -951,7 +1011,12 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                 } else {
                     lx = lds_f4(a); hx = lds_f4(a + 16); ly = lds_f4(a + 32); hy = lds_f4(a + 48); lz = lds_f4(a + 64); hz = lds_f4(a + 80);
                 }
-                ch = lds_i4(a + 96);
+                if constexpr (PK) {  // the four 16-bit codes (BvhNode::pad), codes 1 and 3 in the high halves
+                    const uint2 cw = lds_u2(a + 112);
+                    ch = make_int4(static_cast<int32_t>(cw.x), static_cast<int32_t>(cw.x), static_cast<int32_t>(cw.y), static_cast<int32_t>(cw.y));
+                } else {
+                    ch = lds_i4(a + 96);
+                }
             } else {
                 const float4* np = reinterpret_cast<const float4*>(S.nodes + node);
                 if (ART_NEAR_FAR_G) {
@@ -962,7 +1027,12 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                 } else {
                     lx = np[0]; hx = np[1]; ly = np[2]; hy = np[3]; lz = np[4]; hz = np[5];
                 }
-                ch = reinterpret_cast<const int4*>(np)[6];
+                if constexpr (PK) {
+                    const uint2 cw = reinterpret_cast<const uint2*>(np)[14];
+                    ch = make_int4(static_cast<int32_t>(cw.x), static_cast<int32_t>(cw.x), static_cast<int32_t>(cw.y), static_cast<int32_t>(cw.y));
+                } else {
+                    ch = reinterpret_cast<const int4*>(np)[6];
+                }
             }
             // branchless pushes (far to near) after a sorting network (ascending entry distance, misses last): every
             // write lands at or below the final top, which the stack's spare row covers; the pop reads the entry under
@@ -993,6 +1063,20 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
 #ifdef ART_STATS
                 if (near) cur_d = __uint_as_float(q0 & 0xFFFF0000u);
 #endif
+            } else if constexpr (PK) {
+                // as the LDS variant: 5 integer min/max pairs; each pushed code sign-extended from its key's low half
+                uint32_t q0, q1, q2, q3;
+                slab4_packed_nf(lx, hx, ly, hy, lz, hz, ch, ix, iy, iz, oix, oiy, oiz, tminf, tmaxf, q0, q1, q2, q3);
+                ucas(q0, q1);
+                ucas(q2, q3);
+                ucas(q0, q2);
+                ucas(q1, q3);
+                ucas(q1, q2);
+                st.push(static_cast<int16_t>(q3), q3 < kKeyMiss);
+                st.push(static_cast<int16_t>(q2), q2 < kKeyMiss);
+                st.push(static_cast<int16_t>(q1), q1 < kKeyMiss);
+                near = q0 < kKeyMiss;
+                near_child = static_cast<int16_t>(q0);
             } else {
                 float k0, k1, k2, k3;
                 if (ART_NEAR_FAR_G) slab4_nf(lx, hx, ly, hy, lz, hz, ix, iy, iz, oix, oiy, oiz, tminf, tmaxf, k0, k1, k2, k3);
@@ -1113,6 +1197,14 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
             first2 = (x2 & ((1u << kLdsLeafShift) - 1)) - cnt;  // slot of entry k >= cnt: first2 + k
             cnt12 = cnt + (x2 >> kLdsLeafShift);
 #endif
+        } else if constexpr (PK) {
+            first = leaf16_first(leaf);
+            cnt = leaf16_count(leaf);
+#if ART_SPECULATIVE
+            // leaf2 == kNodeEmpty decodes as an empty range (count 0)
+            first2 = leaf16_first(leaf2) - cnt;
+            cnt12 = cnt + leaf16_count(leaf2);
+#endif
         } else {
             first = leaf_first(leaf);
             cnt = leaf_count(leaf);
@@ -1154,7 +1246,7 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                     V3<R> p1 = ld3(lt.p), p2 = ld3(lt.p + 3), p3 = ld3(lt.p + 6);
                     ref = S.primrefs[slot];
                     __asm__ volatile("" : "+v"(p1.x), "+v"(p1.y), "+v"(p1.z), "+v"(p2.x), "+v"(p2.y), "+v"(p2.z), "+v"(p3.x), "+v"(p3.y), "+v"(p3.z));
-                    if (F == F_TRI || primref_type(ref) == PRIM_TRIANGLE) h = hit_tri_v(p1, p2, p3, r, tmin, tmax, tt);
+                    if (fbase(F) == F_TRI || primref_type(ref) == PRIM_TRIANGLE) h = hit_tri_v(p1, p2, p3, r, tmin, tmax, tt);
                     else h = hit_prim<R, F & ~F_TRI>(S, ref, r, tmin, tmax, tt, fc);
                 } else if constexpr ((F & F_TRI) == 0 && ART_LEAF_PRIMS_G) {
                     // the leaf-ordered record copy: its loads go out beside the primref's instead of behind it
@@ -1500,7 +1592,7 @@ __device__ __forceinline__ void rect_surface(Surf<R>& s, int axis, R a0, R a1, R
 template <class R, uint32_t F, bool UV = true>
 __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref, uint32_t face, const Ray<R>& r, R t, Surf<R>& s) {
     const uint32_t idx = primref_index(ref);
-    const uint32_t type = (F == F_SPHERE) ? PRIM_SPHERE : primref_type(ref);
+    const uint32_t type = (fbase(F) == F_SPHERE) ? PRIM_SPHERE : primref_type(ref);
     switch (type) {
         case PRIM_SPHERE: {  // sphere.h:57-63, :24-37
             const SphereRec<R>& sp = S.spheres[idx];

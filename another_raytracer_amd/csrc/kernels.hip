@@ -1582,6 +1582,7 @@ struct DeviceScene {
     bool tex_basic = false;                          // only solid and checker textures
     bool lds_scene = false;                          // view.lds_image holds the layout.h LDS scene image
     bool lds_shade = false;                          // ... including a complete shading table (fused variant)
+    bool codes16 = false;                            // every node's child codes fit BvhNode::pad's 16-bit form
     size_t bytes = 0;
 
     template <class T>
@@ -1981,7 +1982,32 @@ static void build_device_scene(const FlatScene& f, DeviceScene<R>& ds) {
         }
         ds.view.leaf_prims = ds.upload(lp);
     }
-    ds.view.nodes = ds.upload(f.nodes);
+    {  // BvhNode::pad: the 16-bit child codes (layout.h make_leaf16), derived here from the 32-bit ones (never read
+       // from a scene file); codes16 when every inner index, leaf and hoisted leaf fits them
+        std::vector<BvhNode> nodes = f.nodes;
+        bool ok = nodes.size() <= 32768u;
+        for (BvhNode& b : nodes) {
+            int32_t c16[4];
+            for (int c = 0; c < 4; ++c) {
+                const int32_t x = b.child[c];
+                if (x >= 0) {
+                    c16[c] = x;
+                } else if (x == kNodeEmpty) {
+                    c16[c] = kNodeEmpty;
+                } else {
+                    ok = ok && leaf16_ok(leaf_first(x), leaf_count(x));
+                    c16[c] = ok ? make_leaf16(leaf_first(x), leaf_count(x)) : kNodeEmpty;
+                }
+            }
+            b.pad[0] = static_cast<int32_t>((static_cast<uint32_t>(c16[1]) << 16) | (static_cast<uint32_t>(c16[0]) & 0xFFFFu));
+            b.pad[1] = static_cast<int32_t>((static_cast<uint32_t>(c16[3]) << 16) | (static_cast<uint32_t>(c16[2]) & 0xFFFFu));
+            b.pad[2] = b.pad[3] = 0;
+        }
+        for (const auto& o : f.objs)
+            if (o.kind == OBJ_BVH && o.b != kNodeEmpty) ok = ok && leaf16_ok(leaf_first(o.b), leaf_count(o.b));
+        ds.codes16 = ok;
+        ds.view.nodes = ds.upload(nodes);
+    }
     ds.view.objs = ds.upload(objs);
     {  // obj_prims[o]: prim object o's primitive record (device.h hit_object)
         std::vector<PrimRec80> op(objs.size());
@@ -2240,23 +2266,31 @@ static void launch_paths_g_ft(int num_cu, hipStream_t st, const DevScene<double>
     check_ring_waves(blocks, kBlock, num_cu);
     hipLaunchKernelGGL((k_paths_g<F, TF, 0>), dim3(blocks), dim3(kBlock), lds, st, S, g, cam, w, next_slot);
 }
-static void launch_paths_g(uint32_t feat, bool tex_basic, int num_cu, hipStream_t st, const DevScene<double>& S, const PassGeom& g,
+// ART_CODE16_G: k_paths_g instantiations without F_MEDIA_G sort packed keys over 16-bit child codes (F_CODE16); a scene
+// whose codes do not fit them (more than 32768 nodes or 8192 primitive references) takes the F_ALL kernel instead
+#ifndef ART_CODE16_G
+#define ART_CODE16_G 1
+#endif
+static void launch_paths_g(uint32_t feat, bool tex_basic, bool codes16, int num_cu, hipStream_t st, const DevScene<double>& S, const PassGeom& g,
                            const CameraRec<double>& cam, const Work<double>& w, uint32_t* next_slot) {
-    if ((feat & ~kFeatSpheres) == 0) {
-        if (tex_basic) launch_paths_g_ft<kFeatSpheres, kTexBasic>(num_cu, st, S, g, cam, w, next_slot);
-        else launch_paths_g_ft<kFeatSpheres, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
+    constexpr uint32_t C = ART_CODE16_G ? F_CODE16 : 0u;
+    if (C && !codes16 && (feat & F_MEDIA_G) == 0) {
+        launch_paths_g_ft<F_ALL, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
+    } else if ((feat & ~kFeatSpheres) == 0) {
+        if (tex_basic) launch_paths_g_ft<kFeatSpheres | C, kTexBasic>(num_cu, st, S, g, cam, w, next_slot);
+        else launch_paths_g_ft<kFeatSpheres | C, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
     } else if ((feat & ~kFeatMesh) == 0) {
         // the F_TRI bit of an instantiation <=> the scene has triangles (leaf_tris exists)
         if (feat & F_TRI) {
-            if (tex_basic) launch_paths_g_ft<kFeatMesh, kTexBasic>(num_cu, st, S, g, cam, w, next_slot);
-            else launch_paths_g_ft<kFeatMesh, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
+            if (tex_basic) launch_paths_g_ft<kFeatMesh | C, kTexBasic>(num_cu, st, S, g, cam, w, next_slot);
+            else launch_paths_g_ft<kFeatMesh | C, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
         } else {
-            if (tex_basic) launch_paths_g_ft<kFeatMesh & ~F_TRI, kTexBasic>(num_cu, st, S, g, cam, w, next_slot);
-            else launch_paths_g_ft<kFeatMesh & ~F_TRI, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
+            if (tex_basic) launch_paths_g_ft<(kFeatMesh & ~F_TRI) | C, kTexBasic>(num_cu, st, S, g, cam, w, next_slot);
+            else launch_paths_g_ft<(kFeatMesh & ~F_TRI) | C, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
         }
     } else if ((feat & F_TRI) == 0) {  // e.g. the Next-Week final: no triangle code in the kernel
         if (feat & F_MEDIA_G) launch_paths_g_ft<F_ALL & ~F_TRI, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
-        else launch_paths_g_ft<F_ALL & ~F_TRI & ~F_MEDIA_G, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
+        else launch_paths_g_ft<(F_ALL & ~F_TRI & ~F_MEDIA_G) | C, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
     } else {
         launch_paths_g_ft<F_ALL, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
     }
@@ -2454,7 +2488,7 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
                     if (p.max_depth > 0) {
                         if (prof) mark();
                         if (variant == EXT_MEGA) launch_paths(I.num_cu, stream, ds.view, g, cam, w, counter(w, 0, 0, 0));
-                        else launch_paths_g(ds.features, ds.tex_basic, I.num_cu, stream, ds.view, g, cam, w, counter(w, 0, 0, 0));
+                        else launch_paths_g(ds.features, ds.tex_basic, ds.codes16, I.num_cu, stream, ds.view, g, cam, w, counter(w, 0, 0, 0));
                         if (prof) { mark(); mark(); }
                         ++ext_launches;
                     }

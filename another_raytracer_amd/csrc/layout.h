@@ -79,6 +79,14 @@ constexpr int32_t kNodeEmpty = -1;
 ART_HD int32_t make_leaf(uint32_t first, uint32_t count) { return ~static_cast<int32_t>((count << 24) | first); }
 ART_HD uint32_t leaf_first(int32_t c) { return static_cast<uint32_t>(~c) & 0xFFFFFFu; }
 ART_HD uint32_t leaf_count(int32_t c) { return (static_cast<uint32_t>(~c) >> 24) & 0x7Fu; }
+// 16-bit child codes (BvhNode::pad, the packed-key traversal of k_paths_g kernels with F_CODE16): an inner node is its
+// index (< 32768), a leaf of 1..4 primitives starting at primitive reference `first` (< 8192) is
+// -2 - ((count - 1) << 13 | first), at most -2, so kNodeEmpty (-1) stays apart and `code < kNodeEmpty` marks a leaf.
+// leaf16_first / leaf16_count of kNodeEmpty give an empty range.
+ART_HD bool leaf16_ok(uint32_t first, uint32_t count) { return count >= 1u && count <= 4u && first < 8192u && (((count - 1u) << 13) | first) <= 32766u; }
+ART_HD int32_t make_leaf16(uint32_t first, uint32_t count) { return -2 - static_cast<int32_t>(((count - 1u) << 13) | first); }
+ART_HD uint32_t leaf16_first(int32_t c) { return static_cast<uint32_t>(-2 - c) & 0x1FFFu; }
+ART_HD uint32_t leaf16_count(int32_t c) { return static_cast<uint32_t>((-2 - c) >> 13) + 1u; }
 constexpr int kMaxLeafPrims = 4;
 constexpr int kMaxBvhDepth = 30;     // binary SAH tree depth cap
 constexpr int kMaxStackDepth = 64;   // per-lane LDS traversal stack entries (sized per scene: FlatScene::max_stack)
@@ -180,6 +188,11 @@ struct alignas(16) ObjBox {
 // F_MEDIA: constant_medium objects; F_MEDIA_G: one of them has a boundary that is not a sphere primitive (its two
 // boundary hits are whole object traversals; a sphere boundary is one quadratic, device.h hit_medium)
 enum Feature : uint32_t { F_SPHERE = 1u, F_TRI = 2u, F_RECT = 4u, F_BOX = 8u, F_XFORM = 16u, F_MEDIA = 32u, F_MEDIA_G = 64u, F_ALL = 127u };
+// Not a scene feature: an instantiation flag of k_paths_g -- its traversals read the 16-bit child codes and sort packed
+// keys (device.h traverse); the scene's codes must all fit (DeviceScene::codes16) and it has no F_MEDIA_G boundary
+// traversals (those start at t = -inf, which packed keys cannot order).
+constexpr uint32_t F_CODE16 = 128u;
+ART_HD constexpr uint32_t fbase(uint32_t f) { return f & F_ALL; }
 constexpr uint32_t kFeatSpheres = F_SPHERE;
 constexpr uint32_t kFeatMesh = F_SPHERE | F_TRI | F_RECT | F_MEDIA;
 
