@@ -757,6 +757,8 @@ struct LaneStack<B, true> {  // LDS-scene variant: 16-bit entries, tracked as th
     // it, but a walk whose node is kNodeEmpty ends without another peek or pop (traverse), so that row is never read;
     // the next walk starts from a fresh LaneStack.
     __device__ __forceinline__ void pop_if(bool c) { top -= c ? kRow : 0u; }
+    __device__ __forceinline__ uint32_t save() const { return top; }
+    __device__ __forceinline__ void restore(uint32_t t) { top = t; }
 };
 #ifndef ART_STACK_ADDR_G
 // 32-bit stacks tracked by the LDS byte address of their top entry, as LaneStack<B, true> (a push or pop is one
@@ -808,6 +810,8 @@ struct LaneStack<B, false> {  // 32-bit entries
 #endif
 // Traversal stack entry: node/leaf codes, 16 bits in the LDS-scene variant (layout.h lds_leaf), 32 bits otherwise.
 template <bool L> using StackT = typename std::conditional<L, int16_t, int32_t>::type;
+// k_paths_g instantiations with F_CODE16 keep 16-bit entries as well (the LDS variant's LaneStack and stack columns)
+template <bool L, uint32_t F> using StackF = StackT<L || (F & F_CODE16) != 0>;
 #ifndef ART_STACK_SWZ
 #define ART_STACK_SWZ 1
 #endif
@@ -849,7 +853,7 @@ struct TravResume {
 // RES: resumable (rs non-null), HBM-scene variant only.
 template <class R, uint32_t F, int B, bool L, bool PL = false, bool RES = false>
 __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* lds, int32_t root, const Ray<R>& r, R tmin, R tmax,
-                                         StackT<L>* stk, R& t, uint32_t& prim, uint32_t& face, uint32_t& mt, TravResume* rs = nullptr,
+                                         StackF<L, F>* stk, R& t, uint32_t& prim, uint32_t& face, uint32_t& mt, TravResume* rs = nullptr,
                                          int32_t hoisted = kNodeEmpty) {
     static_assert(!(L && (F & F_MEDIA)), "packed LDS keys need tmin > 0: no medium boundary tests in the LDS variant");
     static_assert(!RES || (!L && ART_SPECULATIVE), "resumable traversal: HBM-scene speculative variant only");
@@ -884,15 +888,15 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
     const R d_a = L ? len2(r.d) : R(0);
     const R d_inv_a = L ? R(1) / d_a : R(0);
     bool hit = false;
-    LaneStack<B, L> st(stk);
+    // PK (k_paths_g instantiations with F_CODE16): the HBM-scene traversal sorts packed keys as the LDS variant does,
+    // with the node's 16-bit child codes (BvhNode::pad, layout.h make_leaf16) in the low half of each key; codes,
+    // stack entries (16-bit, the LDS variant's LaneStack) and leaves are then in the 16-bit form throughout the walk
+    constexpr bool PK = !L && (F & F_CODE16) != 0;
+    static_assert(!PK || (F & F_MEDIA_G) == 0, "packed keys need tmin > 0: no medium boundary traversals");
+    LaneStack<B, L || PK> st(stk);
     // L: inner nodes are coded by their byte offset in a node plane (index * 16, layout.h), so a visit's plane
     // addresses are one add each
     static_assert(kLdsNodeCap * 16 <= 32767, "LDS inner-node codes are 16-bit stack entries");
-    // PK (k_paths_g instantiations with F_CODE16): the HBM-scene traversal sorts packed keys as the LDS variant does,
-    // with the node's 16-bit child codes (BvhNode::pad, layout.h make_leaf16) in the low half of each key; codes,
-    // stack entries and leaves are then in the 16-bit form throughout the walk
-    constexpr bool PK = !L && (F & F_CODE16) != 0;
-    static_assert(!PK || (F & F_MEDIA_G) == 0, "packed keys need tmin > 0: no medium boundary traversals");
     const int32_t root_code = L ? root * 16 : root;
     int32_t node = root_code;
 #ifdef ART_STATS
@@ -1325,7 +1329,7 @@ __device__ __forceinline__ bool cull_box_hit(const ObjBox& b, const Ray<R>& r, R
     return lo <= hi;
 }
 template <class R, uint32_t F, int B, bool L, bool PL = false, bool RES = false>
-__device__ __forceinline__ bool hit_object(const DevScene<R>& S, const uint8_t* lds, int32_t oi, Ray<R> r, R tmin, R tmax, StackT<L>* stk,
+__device__ __forceinline__ bool hit_object(const DevScene<R>& S, const uint8_t* lds, int32_t oi, Ray<R> r, R tmin, R tmax, StackF<L, F>* stk,
                                            R& t, uint32_t& prim, uint32_t& face, uint32_t& mt, TravResume* rs = nullptr) {
     if constexpr ((F & F_XFORM) != 0 && ART_XFORM_CULL) {
         // a resumed traversal passed the box when it started
@@ -1369,7 +1373,7 @@ static __device__ __noinline__ double glibc_log_call(double x) { return glibc_lo
 // constant_medium.h:37-82.  Consumes one uniform when the clamped interval is non-empty.
 template <class R, uint32_t F, int B, bool L, bool PL = false>
 __device__ __forceinline__ bool hit_medium(const DevScene<R>& S, const uint8_t* lds, const ObjRec<R>& m, const Ray<R>& r, R tmin, R tmax,
-                                           StackT<L>* stk, uint64_t& rng, R& t) {
+                                           StackF<L, F>* stk, uint64_t& rng, R& t) {
     const R inf = R(__builtin_inf());
     R t1, t2;
     const ObjRec<R>& bo = S.objs[m.a];
@@ -1463,7 +1467,7 @@ struct HitOut {
     uint32_t mt;         // material type when the hit came from the LDS scene image, else kMatUnknown
 };
 template <class R, uint32_t F, int B, bool L, bool PL = false>
-__device__ __forceinline__ bool trace_world(const DevScene<R>& S, const uint8_t* lds, const Ray<R>& r, StackT<L>* stk, uint64_t& rng, R& t,
+__device__ __forceinline__ bool trace_world(const DevScene<R>& S, const uint8_t* lds, const Ray<R>& r, StackF<L, F>* stk, uint64_t& rng, R& t,
                                             HitOut& h) {
     R closest = R(__builtin_inf());
     bool any = false;
@@ -1512,7 +1516,7 @@ struct TraceState {
     }
 };
 template <class R, uint32_t F, int B, bool PL>
-__device__ __forceinline__ bool trace_world_res(const DevScene<R>& S, const Ray<R>& r, StackT<false>* stk, uint64_t& rng, TraceState<R>& ts) {
+__device__ __forceinline__ bool trace_world_res(const DevScene<R>& S, const Ray<R>& r, StackF<false, F>* stk, uint64_t& rng, TraceState<R>& ts) {
     ts.tr.suspended = false;
     for (int32_t w = ts.w; w < S.nworld; ++w) {
         const int32_t oi = S.world[w];

@@ -982,9 +982,10 @@ __device__ long long g_trace_pixel = -1, g_trace_sample = -1;
 constexpr int kBlockM = 256 * ART_PATHS_G_WAVES;  // one LM block per CU at the kernel's occupancy
 constexpr size_t kPathsGLdsCap = 160 * 1024;
 __host__ __device__ constexpr size_t align16(size_t x) { return (x + 15u) & ~size_t(15); }
-__host__ __device__ constexpr size_t paths_g_stack_bytes(uint32_t stack, int block) { return sizeof(StackT<false>) * stack * block; }
-__host__ __device__ constexpr size_t paths_g_head_bytes(uint32_t stack, int block) {  // stack, camera, pass geometry, jumps
-    return align16(paths_g_stack_bytes(stack, block) + sizeof(CameraRec<double>) + sizeof(PassGeom)) + (ART_COOP_SPHERE_G ? kJumpBytes : 0);
+// s16: 16-bit stack entries (F_CODE16 instantiations, device.h StackF)
+__host__ __device__ constexpr size_t paths_g_stack_bytes(uint32_t stack, int block, bool s16) { return (s16 ? 2u : 4u) * stack * block; }
+__host__ __device__ constexpr size_t paths_g_head_bytes(uint32_t stack, int block, bool s16) {  // stack, camera, pass geometry, jumps
+    return align16(paths_g_stack_bytes(stack, block, s16) + sizeof(CameraRec<double>) + sizeof(PassGeom)) + (ART_COOP_SPHERE_G ? kJumpBytes : 0);
 }
 // LM kernels also hold the world list and the object records (a few KiB): every segment walks them, and a prim
 // object's test otherwise waits on three dependent L1 loads (world slot -> object -> primitive)
@@ -1003,18 +1004,20 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
     // primrefs, triangles] -- as in k_paths, the camera and pass geometry are read from LDS where a path starts (as
     // kernel arguments held in SGPRs for the whole loop they spilled ~100 SGPRs into VGPR lanes)
     extern __shared__ __align__(16) uint8_t smem[];
-    StackT<false>* stk = reinterpret_cast<StackT<false>*>(smem) + B + threadIdx.x;
-    CameraRec<double>& s_cam = *reinterpret_cast<CameraRec<double>*>(smem + paths_g_stack_bytes(g.stack, B));
-    PassGeom& s_g = *reinterpret_cast<PassGeom*>(smem + paths_g_stack_bytes(g.stack, B) + sizeof(CameraRec<double>));
-    stk[-B] = static_cast<StackT<false>>(kNodeEmpty);
+    constexpr bool S16 = (F & F_CODE16) != 0;
+    using ST = StackF<false, F>;
+    ST* stk = reinterpret_cast<ST*>(smem) + B + stack_column<S16>(threadIdx.x);
+    CameraRec<double>& s_cam = *reinterpret_cast<CameraRec<double>*>(smem + paths_g_stack_bytes(g.stack, B, S16));
+    PassGeom& s_g = *reinterpret_cast<PassGeom*>(smem + paths_g_stack_bytes(g.stack, B, S16) + sizeof(CameraRec<double>));
+    stk[-B] = static_cast<ST>(kNodeEmpty);
     if (threadIdx.x == 0) {
         s_cam = cam;
         s_g = g;
     }
-    [[maybe_unused]] JumpEntry* jt = reinterpret_cast<JumpEntry*>(smem + align16(paths_g_stack_bytes(g.stack, B) + sizeof(CameraRec<double>) + sizeof(PassGeom)));
+    [[maybe_unused]] JumpEntry* jt = reinterpret_cast<JumpEntry*>(smem + align16(paths_g_stack_bytes(g.stack, B, S16) + sizeof(CameraRec<double>) + sizeof(PassGeom)));
     if (ART_COOP_SPHERE_G && threadIdx.x < static_cast<uint32_t>(kJumpEntries)) jt[threadIdx.x] = pcg_jump(3u * threadIdx.x);
     DevScene<double> S = S0;
-    size_t lm_off = paths_g_head_bytes(g.stack, B);  // LM: world list and objects, then the BVH arrays
+    size_t lm_off = paths_g_head_bytes(g.stack, B, S16);  // LM: world list and objects, then the BVH arrays
     if constexpr (LM != 0) {
         uint8_t* wb = smem + lm_off;
         for (int32_t i = static_cast<int32_t>(threadIdx.x); i < S0.nworld; i += B) reinterpret_cast<int32_t*>(wb)[i] = S0.world[i];
@@ -2230,7 +2233,7 @@ template <uint32_t F, uint32_t TF>
 static void launch_paths_g_ft(int num_cu, hipStream_t st, const DevScene<double>& S, const PassGeom& g, const CameraRec<double>& cam,
                               const Work<double>& w, uint32_t* next_slot) {
     // g.stack = stack_rows: sentinel + entries + spare row
-    const size_t lm_head = paths_g_head_bytes(g.stack, kBlockM) + paths_g_world_bytes(S.nworld, S.n_objs);
+    const size_t lm_head = paths_g_head_bytes(g.stack, kBlockM, (F & F_CODE16) != 0) + paths_g_world_bytes(S.nworld, S.n_objs);
     const size_t lds_m = lm_head + paths_g_mesh_bytes(S.n_nodes, S.n_primrefs, (F & F_TRI) ? (ART_LEAF_TRIS ? S.n_primrefs : S.n_tris) : 0u);
 #if ART_LDS_MESH
     if (S.n_nodes > 0 && lds_m <= kPathsGLdsCap) {
@@ -2261,7 +2264,7 @@ static void launch_paths_g_ft(int num_cu, hipStream_t st, const DevScene<double>
         return;
     }
 #endif
-    const size_t lds = paths_g_head_bytes(g.stack, kBlock);
+    const size_t lds = paths_g_head_bytes(g.stack, kBlock, (F & F_CODE16) != 0);
     const int blocks = blocks_per_cu(reinterpret_cast<const void*>(k_paths_g<F, TF, 0>), kBlock, lds) * num_cu;
     check_ring_waves(blocks, kBlock, num_cu);
     hipLaunchKernelGGL((k_paths_g<F, TF, 0>), dim3(blocks), dim3(kBlock), lds, st, S, g, cam, w, next_slot);
