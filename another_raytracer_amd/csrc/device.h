@@ -710,6 +710,11 @@ __device__ __forceinline__ void stat_lane(int k) { atomicAdd(&g_art_stats[k], 1u
 #ifndef ART_LEAF_PRIMS_G
 #define ART_LEAF_PRIMS_G 1  // triangle-free HBM-scene kernels read leaf records from the leaf-ordered copy
 #endif
+#ifndef ART_NF_XOR
+// HBM-scene traversal: a node's near plane at base + sign * 16 and the far plane at (that) ^ 16, the axis offsets as
+// immediates (node arrays 128-aligned): 10 address VALU per visit instead of 15
+#define ART_NF_XOR 1
+#endif
 #ifndef ART_LEAF2_G
 #define ART_LEAF2_G 1  // the HBM-scene traversal also tests a lane's two pending leaves in one leaf phase
 #endif
@@ -851,7 +856,7 @@ struct TravResume {
 };
 // B: lanes per block (LDS stack stride).  L: nodes and leaf spheres come from the LDS scene image at `lds`.
 // RES: resumable (rs non-null), HBM-scene variant only.
-template <class R, uint32_t F, int B, bool L, bool PL = false, bool RES = false>
+template <class R, uint32_t F, int B, bool L, int PL = 0, bool RES = false>
 __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* lds, int32_t root, const Ray<R>& r, R tmin, R tmax,
                                          StackF<L, F>* stk, R& t, uint32_t& prim, uint32_t& face, uint32_t& mt, TravResume* rs = nullptr,
                                          int32_t hoisted = kNodeEmpty) {
@@ -1000,16 +1005,22 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                     __asm__ volatile("v_lshrrev_b32 %0, 31, %1" : "=v"(sy) : "v"(iy));
                     __asm__ volatile("v_lshrrev_b32 %0, 31, %1" : "=v"(sz) : "v"(iz));
                     nfx = sx << 4;
-                    nfy = 32u + (sy << 4);
-                    nfz = 64u + (sz << 4);
+                    nfy = (ART_NF_XOR ? 0u : 32u) + (sy << 4);
+                    nfz = (ART_NF_XOR ? 0u : 64u) + (sz << 4);
                 }
             }
             if constexpr (L) {
-            } else if (PL && static_cast<uint32_t>(node) < S.n_lds_nodes) {
+            } else if (PL == 2 || (PL == 1 && static_cast<uint32_t>(node) < S.n_lds_nodes)) {  // PL 2: every node in LDS
                 // the top levels, copied into LDS: explicit LDS loads (a generic pointer here would be merged with
                 // the global branch's into flat loads)
                 const uint32_t a = S.nodes_lds + static_cast<uint32_t>(node) * static_cast<uint32_t>(sizeof(BvhNode));
-                if (ART_NEAR_FAR_G) {  // lx/ly/lz: near planes, hx/hy/hz: far planes
+                if (ART_NEAR_FAR_G && ART_NF_XOR) {
+                    // node addresses are multiples of 32 (the LDS node array is 128-aligned): near plane = a + sign * 16,
+                    // far plane = near ^ 16, and the y / z planes' +32 / +64 ride in the loads' immediate offsets
+                    const uint32_t nx = a + nfx, ny = a + nfy, nz = a + nfz;
+                    lx = lds_f4(nx); hx = lds_f4(nx ^ 16u); ly = lds_f4(ny + 32u); hy = lds_f4((ny ^ 16u) + 32u);
+                    lz = lds_f4(nz + 64u); hz = lds_f4((nz ^ 16u) + 64u);
+                } else if (ART_NEAR_FAR_G) {  // lx/ly/lz: near planes, hx/hy/hz: far planes
                     lx = lds_f4(a + nfx); hx = lds_f4(a + (nfx ^ 16u)); ly = lds_f4(a + nfy); hy = lds_f4(a + (nfy ^ 16u));
                     lz = lds_f4(a + nfz); hz = lds_f4(a + (nfz ^ 16u));
                 } else {
@@ -1023,7 +1034,14 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                 }
             } else {
                 const float4* np = reinterpret_cast<const float4*>(S.nodes + node);
-                if (ART_NEAR_FAR_G) {
+                if (ART_NEAR_FAR_G && ART_NF_XOR) {  // 32-bit offsets from the node array's base, as above
+                    const char* nb = reinterpret_cast<const char*>(S.nodes);
+                    const uint32_t o = static_cast<uint32_t>(node) * static_cast<uint32_t>(sizeof(BvhNode));
+                    const uint32_t nx = o + nfx, ny = o + nfy, nz = o + nfz;
+                    lx = *reinterpret_cast<const float4*>(nb + nx); hx = *reinterpret_cast<const float4*>(nb + (nx ^ 16u));
+                    ly = *reinterpret_cast<const float4*>(nb + ny + 32u); hy = *reinterpret_cast<const float4*>(nb + ((ny ^ 16u) + 32u));
+                    lz = *reinterpret_cast<const float4*>(nb + nz + 64u); hz = *reinterpret_cast<const float4*>(nb + ((nz ^ 16u) + 64u));
+                } else if (ART_NEAR_FAR_G) {
                     const char* nb = reinterpret_cast<const char*>(np);
                     lx = *reinterpret_cast<const float4*>(nb + nfx); hx = *reinterpret_cast<const float4*>(nb + (nfx ^ 16u));
                     ly = *reinterpret_cast<const float4*>(nb + nfy); hy = *reinterpret_cast<const float4*>(nb + (nfy ^ 16u));
@@ -1328,7 +1346,7 @@ __device__ __forceinline__ bool cull_box_hit(const ObjBox& b, const Ray<R>& r, R
     const float hi = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), f_hi(tmax)));
     return lo <= hi;
 }
-template <class R, uint32_t F, int B, bool L, bool PL = false, bool RES = false>
+template <class R, uint32_t F, int B, bool L, int PL = 0, bool RES = false>
 __device__ __forceinline__ bool hit_object(const DevScene<R>& S, const uint8_t* lds, int32_t oi, Ray<R> r, R tmin, R tmax, StackF<L, F>* stk,
                                            R& t, uint32_t& prim, uint32_t& face, uint32_t& mt, TravResume* rs = nullptr) {
     if constexpr ((F & F_XFORM) != 0 && ART_XFORM_CULL) {
@@ -1371,7 +1389,7 @@ __device__ __forceinline__ bool hit_object(const DevScene<R>& S, const uint8_t* 
 #endif
 static __device__ __noinline__ double glibc_log_call(double x) { return glibc_log(x); }
 // constant_medium.h:37-82.  Consumes one uniform when the clamped interval is non-empty.
-template <class R, uint32_t F, int B, bool L, bool PL = false>
+template <class R, uint32_t F, int B, bool L, int PL = 0>
 __device__ __forceinline__ bool hit_medium(const DevScene<R>& S, const uint8_t* lds, const ObjRec<R>& m, const Ray<R>& r, R tmin, R tmax,
                                            StackF<L, F>* stk, uint64_t& rng, R& t) {
     const R inf = R(__builtin_inf());
@@ -1466,7 +1484,7 @@ struct HitOut {
     uint32_t prim, obj;  // obj: world slot | box face << 16
     uint32_t mt;         // material type when the hit came from the LDS scene image, else kMatUnknown
 };
-template <class R, uint32_t F, int B, bool L, bool PL = false>
+template <class R, uint32_t F, int B, bool L, int PL = 0>
 __device__ __forceinline__ bool trace_world(const DevScene<R>& S, const uint8_t* lds, const Ray<R>& r, StackF<L, F>* stk, uint64_t& rng, R& t,
                                             HitOut& h) {
     R closest = R(__builtin_inf());
@@ -1515,7 +1533,7 @@ struct TraceState {
         tr.fresh = true;
     }
 };
-template <class R, uint32_t F, int B, bool PL>
+template <class R, uint32_t F, int B, int PL>
 __device__ __forceinline__ bool trace_world_res(const DevScene<R>& S, const Ray<R>& r, StackF<false, F>* stk, uint64_t& rng, TraceState<R>& ts) {
     ts.tr.suspended = false;
     for (int32_t w = ts.w; w < S.nworld; ++w) {

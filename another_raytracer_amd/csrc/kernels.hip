@@ -965,6 +965,9 @@ constexpr uint32_t kLdsPartialMinNodes = 64;
 // isotropic hits: measured +0.8 % (cow), +1.3 % (Next-Week final), +2.4 % (dino 4096^2) (r3k)
 #define ART_COOP_SPHERE_G 1
 #endif
+#ifndef ART_LM1_PL
+#define ART_LM1_PL 1
+#endif
 #ifndef ART_PATHS_G_WAVES
 #define ART_PATHS_G_WAVES 3  // 3 waves per SIMD (<= 168 VGPRs): measured best over 2 and 4 (cow +22 %, final +18 %, dino +21 % over 2)
 #endif
@@ -982,6 +985,7 @@ __device__ long long g_trace_pixel = -1, g_trace_sample = -1;
 constexpr int kBlockM = 256 * ART_PATHS_G_WAVES;  // one LM block per CU at the kernel's occupancy
 constexpr size_t kPathsGLdsCap = 160 * 1024;
 __host__ __device__ constexpr size_t align16(size_t x) { return (x + 15u) & ~size_t(15); }
+__host__ __device__ constexpr size_t align128(size_t x) { return (x + 127u) & ~size_t(127); }
 // s16: 16-bit stack entries (F_CODE16 instantiations, device.h StackF)
 __host__ __device__ constexpr size_t paths_g_stack_bytes(uint32_t stack, int block, bool s16) { return (s16 ? 2u : 4u) * stack * block; }
 __host__ __device__ constexpr size_t paths_g_head_bytes(uint32_t stack, int block, bool s16) {  // stack, camera, pass geometry, jumps
@@ -999,6 +1003,9 @@ template <uint32_t F, uint32_t TF, int LM>
 __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) void k_paths_g(DevScene<double> S0, PassGeom g, CameraRec<double> cam,
                                                                                      Work<double> w, uint32_t* next_slot) {
     using R = double;
+    // explicit-LDS node reads (traverse's PL path): LM 2 for its LDS part; LM 1 for every node with ART_LM1_PL (the
+    // XOR near/far addressing needs the explicit LDS addresses; through the LDS-inferred pointer it costs more adds)
+    constexpr int kLdsNodesPL = LM == 2 ? 1 : (LM == 1 && ART_LM1_PL && ART_NF_XOR) ? 2 : 0;
     constexpr int B = LM ? kBlockM : kBlock;
     // dynamic LDS: [traversal stack: g.stack entries x B lanes (+ sentinel row)][camera][pass geometry][LM: nodes,
     // primrefs, triangles] -- as in k_paths, the camera and pass geometry are read from LDS where a path starts (as
@@ -1036,6 +1043,7 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
         S.obj_box = reinterpret_cast<const ObjBox*>(bb);
         lm_off += paths_g_world_bytes(S0.nworld, S0.n_objs);
     }
+    if constexpr (LM != 0) lm_off = align128(lm_off);  // node addresses multiples of 128 (device.h ART_NF_XOR)
     if constexpr (LM == 2) {  // the first n_lds_nodes nodes (the top levels of every BVH) into LDS
         BvhNode* m = reinterpret_cast<BvhNode*>(smem + lm_off);
         const uint4* s4 = reinterpret_cast<const uint4*>(S0.nodes);
@@ -1056,6 +1064,10 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
         // primrefs: 4-B entries, the tail of the last 16-B word comes from past the array's end -- copy word-wise
         for (uint32_t i = threadIdx.x; i < S0.n_primrefs; i += B) reinterpret_cast<uint32_t*>(m + nb)[i] = S0.primrefs[i];
         S.nodes = reinterpret_cast<const BvhNode*>(m);
+        if constexpr (kLdsNodesPL) {  // every node read through the explicit-LDS path (device.h traverse, PL)
+            S.nodes_lds = static_cast<uint32_t>(reinterpret_cast<size_t>((__attribute__((address_space(3))) uint8_t*)m));
+            S.n_lds_nodes = S0.n_nodes;
+        }
         S.primrefs = reinterpret_cast<const uint32_t*>(m + nb);
         if constexpr ((F & F_TRI) != 0) {
 #if ART_LEAF_TRIS
@@ -1182,12 +1194,12 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
             if constexpr (SUSP) {
                 ts.tr.allow = allow;
                 ts.tr.lanes = kSuspLanes;
-                in_trace = !trace_world_res<R, F, B, LM == 2>(S, st.ray, stk, st.rng, ts);
+                in_trace = !trace_world_res<R, F, B, kLdsNodesPL>(S, st.ray, stk, st.rng, ts);
                 hitw = ts.any;
                 t = ts.closest;
                 h = ts.h;
             } else {
-                hitw = trace_world<R, F, B, false, LM == 2>(S, nullptr, st.ray, stk, st.rng, t, h);
+                hitw = trace_world<R, F, B, false, kLdsNodesPL>(S, nullptr, st.ray, stk, st.rng, t, h);
             }
             susp = in_trace;  // suspended: nothing to shade this round
 #if ART_RAY_POOL_G
@@ -2234,7 +2246,7 @@ static void launch_paths_g_ft(int num_cu, hipStream_t st, const DevScene<double>
                               const Work<double>& w, uint32_t* next_slot) {
     // g.stack = stack_rows: sentinel + entries + spare row
     const size_t lm_head = paths_g_head_bytes(g.stack, kBlockM, (F & F_CODE16) != 0) + paths_g_world_bytes(S.nworld, S.n_objs);
-    const size_t lds_m = lm_head + paths_g_mesh_bytes(S.n_nodes, S.n_primrefs, (F & F_TRI) ? (ART_LEAF_TRIS ? S.n_primrefs : S.n_tris) : 0u);
+    const size_t lds_m = align128(lm_head) + paths_g_mesh_bytes(S.n_nodes, S.n_primrefs, (F & F_TRI) ? (ART_LEAF_TRIS ? S.n_primrefs : S.n_tris) : 0u);
 #if ART_LDS_MESH
     if (S.n_nodes > 0 && lds_m <= kPathsGLdsCap) {
         const int blocks = blocks_per_cu(reinterpret_cast<const void*>(k_paths_g<F, TF, 1>), kBlockM, lds_m) * num_cu;
@@ -2247,7 +2259,7 @@ static void launch_paths_g_ft(int num_cu, hipStream_t st, const DevScene<double>
 #endif
 #if ART_LDS_PARTIAL
     // too large for LM 1: as many of the first (top-level) nodes as fit beside the stacks
-    const size_t head = lm_head;
+    const size_t head = align128(lm_head);
     const uint32_t fit = head < kPathsGLdsCap ? static_cast<uint32_t>((kPathsGLdsCap - head) / sizeof(BvhNode)) : 0u;
     if (S.n_nodes > 0 && fit >= kLdsPartialMinNodes) {
         DevScene<double> SP = S;
