@@ -715,6 +715,9 @@ __device__ __forceinline__ void stat_lane(int k) { atomicAdd(&g_art_stats[k], 1u
 // immediates (node arrays 128-aligned): 10 address VALU per visit instead of 15
 #define ART_NF_XOR 1
 #endif
+#ifndef ART_NF_HOIST
+#define ART_NF_HOIST 1  // r3t: dino +0.8 % (its LM 1 kernel has the registers)
+#endif
 #ifndef ART_LEAF2_G
 #define ART_LEAF2_G 1  // the HBM-scene traversal also tests a lane's two pending leaves in one leaf phase
 #endif
@@ -899,6 +902,11 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
     constexpr bool PK = !L && (F & F_CODE16) != 0;
     static_assert(!PK || (F & F_MEDIA_G) == 0, "packed keys need tmin > 0: no medium boundary traversals");
     LaneStack<B, L || PK> st(stk);
+    // ART_NF_HOIST: the near-plane offsets computed once per traversal in kernels with every node in LDS (PL 2) and no
+    // instance transforms (the lighter register budgets: dino's LM 1 kernel), instead of 6 VALU per node visit
+    constexpr bool kNfHoist = !L && ART_NF_HOIST && ART_NF_XOR && PL == 2 && (F & F_XFORM) == 0;
+    [[maybe_unused]] const uint32_t nf_hx = (__float_as_uint(ix) >> 31) << 4, nf_hy = (__float_as_uint(iy) >> 31) << 4,
+                                    nf_hz = (__float_as_uint(iz) >> 31) << 4;
     // L: inner nodes are coded by their byte offset in a node plane (index * 16, layout.h), so a visit's plane
     // addresses are one add each
     static_assert(kLdsNodeCap * 16 <= 32767, "LDS inner-node codes are 16-bit stack entries");
@@ -999,7 +1007,11 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
             // visit from 1/d (live anyway; the empty asm keeps the compiler from hoisting three more loop-carried VGPRs)
             [[maybe_unused]] uint32_t nfx = 0, nfy = 0, nfz = 0;
             if constexpr (!L) {
-                if (ART_NEAR_FAR_G) {
+                if (ART_NEAR_FAR_G && kNfHoist) {  // the per-ray offsets, loop-invariant (3 VGPRs live over the walk)
+                    nfx = nf_hx;
+                    nfy = nf_hy;
+                    nfz = nf_hz;
+                } else if (ART_NEAR_FAR_G) {
                     uint32_t sx, sy, sz;  // sign bits of 1/d, extracted in the loop (volatile: not hoisted)
                     __asm__ volatile("v_lshrrev_b32 %0, 31, %1" : "=v"(sx) : "v"(ix));
                     __asm__ volatile("v_lshrrev_b32 %0, 31, %1" : "=v"(sy) : "v"(iy));
