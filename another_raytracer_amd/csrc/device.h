@@ -248,6 +248,7 @@ struct DevScene {
     const ImageRec* images;
     const uint8_t* texels;
     const TriRec<R>* leaf_tris;  // leaf_tris[slot] = tris[index of primrefs[slot]] for triangle refs, zeros otherwise
+    const TriRec112<R>* leaf_tris112;  // the same with each triangle's plane (n, dd), for the LM 1 kernels' LDS copy
     const PrimRec80* leaf_prims;  // leaf_prims[slot]: the record of primrefs[slot] of any type (triangle-free kernels)
     const PrimRec80* obj_prims;  // obj_prims[o] = the record of prim object o's primitive (indexed like objs)
     const ObjBox* obj_box;       // obj_box[o]: world-space cull box of instance o (indexed like objs)
@@ -341,6 +342,20 @@ __device__ __forceinline__ bool hit_tri_v(V3<R> p1, V3<R> p2, V3<R> p3, const Ra
     const R ndd = dot(N, r.d);
     if (fabs(ndd) < R(DBL_EPSILON)) return false;
     const R dd = -dot(N, p1);
+    const R tt = -(dot(N, r.o) + dd) / ndd;
+    if (tt < tmin || tmax < tt) return false;
+    const V3<R> p = r.o + tt * r.d;
+    if (dot(N, cross(p2 - p1, p - p1)) < R(0)) return false;
+    if (dot(N, cross(p3 - p2, p - p2)) < R(0)) return false;
+    if (dot(N, cross(p1 - p3, p - p3)) < R(0)) return false;
+    t = tt;
+    return true;
+}
+// hit_tri_v with the plane (N, dd) precomputed on the host by the same operations (TriRec112)
+template <class R>
+__device__ __forceinline__ bool hit_tri_pre(V3<R> p1, V3<R> p2, V3<R> p3, V3<R> N, R dd, const Ray<R>& r, R tmin, R tmax, R& t) {
+    const R ndd = dot(N, r.d);
+    if (fabs(ndd) < R(DBL_EPSILON)) return false;
     const R tt = -(dot(N, r.o) + dd) / ndd;
     if (tt < tmin || tmax < tt) return false;
     const V3<R> p = r.o + tt * r.d;
@@ -714,6 +729,9 @@ __device__ __forceinline__ void stat_lane(int k) { atomicAdd(&g_art_stats[k], 1u
 // HBM-scene traversal: a node's near plane at base + sign * 16 and the far plane at (that) ^ 16, the axis offsets as
 // immediates (node arrays 128-aligned): 10 address VALU per visit instead of 15
 #define ART_NF_XOR 1
+#endif
+#ifndef ART_TRI112
+#define ART_TRI112 1  // LM 1 (PL 2) kernels test leaf triangles from TriRec112 records (plane precomputed)
 #endif
 #ifndef ART_NF_HOIST
 #define ART_NF_HOIST 1  // r3t: dino +0.8 % (its LM 1 kernel has the registers)
@@ -1272,7 +1290,18 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
 #else
                 const uint32_t slot = first + k;
 #endif
-                if constexpr ((F & F_TRI) != 0 && ART_LEAF_TRIS) {
+                if constexpr ((F & F_TRI) != 0 && ART_LEAF_TRIS && ART_TRI112 && PL == 2) {
+                    // the LM 1 kernels' leaf triangles with their planes (TriRec112, in LDS): no cross product or
+                    // plane offset per test
+                    const TriRec112<R>& lt = S.leaf_tris112[slot];
+                    V3<R> p1 = ld3(lt.p), p2 = ld3(lt.p + 3), p3 = ld3(lt.p + 6), nn = ld3(lt.n);
+                    R pdd = lt.dd;
+                    ref = S.primrefs[slot];
+                    __asm__ volatile("" : "+v"(p1.x), "+v"(p1.y), "+v"(p1.z), "+v"(p2.x), "+v"(p2.y), "+v"(p2.z), "+v"(p3.x), "+v"(p3.y), "+v"(p3.z));
+                    __asm__ volatile("" : "+v"(nn.x), "+v"(nn.y), "+v"(nn.z), "+v"(pdd));
+                    if (fbase(F) == F_TRI || primref_type(ref) == PRIM_TRIANGLE) h = hit_tri_pre(p1, p2, p3, nn, pdd, r, tmin, tmax, tt);
+                    else h = hit_prim<R, F & ~F_TRI>(S, ref, r, tmin, tmax, tt, fc);
+                } else if constexpr ((F & F_TRI) != 0 && ART_LEAF_TRIS) {
                     // the leaf-ordered triangle copy: its address depends on the slot alone, so its loads go out
                     // beside the primref's instead of behind it (one L2 round trip per test instead of two); the
                     // empty asm keeps the compiler from sinking them under the type test

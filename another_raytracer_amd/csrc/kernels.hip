@@ -996,8 +996,12 @@ __host__ __device__ constexpr size_t paths_g_head_bytes(uint32_t stack, int bloc
 __host__ __device__ constexpr size_t paths_g_world_bytes(int32_t nworld, uint32_t n_objs) {
     return align16(sizeof(int32_t) * static_cast<uint32_t>(nworld)) + (sizeof(ObjRec<double>) + sizeof(PrimRec80) + sizeof(ObjBox)) * n_objs;
 }
+// LM 1's LDS copy of the triangle records: TriRec112 (ART_TRI112) or TriRec
+constexpr bool kLm1Pl = ART_LM1_PL && ART_NF_XOR;      // LM 1 reads its nodes through traverse's PL 2 path
+constexpr bool kLm1Tri112 = ART_TRI112 && kLm1Pl;        // ... and its leaf triangles from TriRec112 (traverse)
+constexpr size_t kLm1TriBytes = kLm1Tri112 ? sizeof(TriRec112<double>) : sizeof(TriRec<double>);
 __host__ __device__ constexpr size_t paths_g_mesh_bytes(uint32_t n_nodes, uint32_t n_primrefs, uint32_t n_tris) {  // n_tris: 0 unless F_TRI
-    return sizeof(BvhNode) * n_nodes + align16(sizeof(uint32_t) * n_primrefs) + sizeof(TriRec<double>) * n_tris;
+    return sizeof(BvhNode) * n_nodes + align16(sizeof(uint32_t) * n_primrefs) + kLm1TriBytes * n_tris;
 }
 template <uint32_t F, uint32_t TF, int LM>
 __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) void k_paths_g(DevScene<double> S0, PassGeom g, CameraRec<double> cam,
@@ -1005,7 +1009,7 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
     using R = double;
     // explicit-LDS node reads (traverse's PL path): LM 2 for its LDS part; LM 1 for every node with ART_LM1_PL (the
     // XOR near/far addressing needs the explicit LDS addresses; through the LDS-inferred pointer it costs more adds)
-    constexpr int kLdsNodesPL = LM == 2 ? 1 : (LM == 1 && ART_LM1_PL && ART_NF_XOR) ? 2 : 0;
+    constexpr int kLdsNodesPL = LM == 2 ? 1 : (LM == 1 && kLm1Pl) ? 2 : 0;
     constexpr int B = LM ? kBlockM : kBlock;
     // dynamic LDS: [traversal stack: g.stack entries x B lanes (+ sentinel row)][camera][pass geometry][LM: nodes,
     // primrefs, triangles] -- as in k_paths, the camera and pass geometry are read from LDS where a path starts (as
@@ -1054,7 +1058,7 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
     if constexpr (LM == 1) {
         uint8_t* m = smem + lm_off;
         const size_t nb = sizeof(BvhNode) * S0.n_nodes, pb = align16(sizeof(uint32_t) * S0.n_primrefs);
-        const size_t tb = (F & F_TRI) ? sizeof(TriRec<double>) * (ART_LEAF_TRIS ? S0.n_primrefs : S0.n_tris) : 0;
+        const size_t tb = (F & F_TRI) ? kLm1TriBytes * (ART_LEAF_TRIS ? S0.n_primrefs : S0.n_tris) : 0;
         auto copy = [&](uint8_t* dst, const void* src, size_t bytes) {
             const uint4* s4 = static_cast<const uint4*>(src);
             uint4* d4 = reinterpret_cast<uint4*>(dst);
@@ -1071,8 +1075,13 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
         S.primrefs = reinterpret_cast<const uint32_t*>(m + nb);
         if constexpr ((F & F_TRI) != 0) {
 #if ART_LEAF_TRIS
-            copy(m + nb + pb, S0.leaf_tris, tb);
-            S.leaf_tris = reinterpret_cast<const TriRec<double>*>(m + nb + pb);
+            if constexpr (kLm1Tri112) {
+                copy(m + nb + pb, S0.leaf_tris112, tb);
+                S.leaf_tris112 = reinterpret_cast<const TriRec112<double>*>(m + nb + pb);
+            } else {
+                copy(m + nb + pb, S0.leaf_tris, tb);
+                S.leaf_tris = reinterpret_cast<const TriRec<double>*>(m + nb + pb);
+            }
 #else
             copy(m + nb + pb, S0.tris, tb);
             S.tris = reinterpret_cast<const TriRec<double>*>(m + nb + pb);
@@ -1985,6 +1994,25 @@ static void build_device_scene(const FlatScene& f, DeviceScene<R>& ds) {
         for (size_t i = 0; i < lt.size(); ++i)
             if (primref_type(f.primrefs[i]) == PRIM_TRIANGLE) lt[i] = tri[primref_index(f.primrefs[i])];
         ds.view.leaf_tris = ds.upload(lt);
+        if constexpr (std::is_same<R, double>::value) {
+            // TriRec112: the plane of each leaf triangle by the device's operations in its order (device.h cross, dot;
+            // -ffp-contract=off on both sides): n = cross(p2 - p1, p3 - p1), dd = -dot(n, p1), bit for bit
+            std::vector<TriRec112<R>> l112(lt.size());
+            for (size_t i = 0; i < lt.size(); ++i) {
+                const R* q = lt[i].p;
+                const R ux = q[3] - q[0], uy = q[4] - q[1], uz = q[5] - q[2];
+                const R vx = q[6] - q[0], vy = q[7] - q[1], vz = q[8] - q[2];
+                const R nx = uy * vz - uz * vy, ny = uz * vx - ux * vz, nz = ux * vy - uy * vx;
+                for (int k = 0; k < 9; ++k) l112[i].p[k] = q[k];
+                l112[i].n[0] = nx;
+                l112[i].n[1] = ny;
+                l112[i].n[2] = nz;
+                l112[i].dd = -(nx * q[0] + ny * q[1] + nz * q[2]);
+                l112[i].mat = lt[i].mat;
+                l112[i].pad = 0;
+            }
+            ds.view.leaf_tris112 = ds.upload(l112);
+        }
         std::vector<PrimRec80> lp(f.primrefs.size());  // every primitive type in leaf order (triangle-free kernels)
         for (size_t i = 0; i < lp.size(); ++i) {
             const uint32_t ref = f.primrefs[i], idx = primref_index(ref);

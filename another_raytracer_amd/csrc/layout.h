@@ -44,6 +44,16 @@ struct TriRec {         // triangle.h: pt1, pt2, pt3
     uint32_t mat;
     uint32_t pad;
 };
+// A leaf triangle with its plane precomputed on the host by the device's own operations (ART_TRI112: the LM 1 kernels'
+// LDS copy): n = cross(pt2 - pt1, pt3 - pt1) and dd = -dot(n, pt1), triangle.h:30-41
+template <class R>
+struct TriRec112 {
+    R p[9];
+    R n[3];
+    R dd;
+    uint32_t mat;
+    uint32_t pad;
+};
 // One primitive record of any type (SphereRec, TriRec, RectRec, BoxRec are all <= 80 B): the device copy of a prim
 // object's primitive, indexed by object (DevScene::obj_prims)
 struct alignas(16) PrimRec80 {
