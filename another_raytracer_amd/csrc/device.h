@@ -730,6 +730,9 @@ __device__ __forceinline__ void stat_lane(int k) { atomicAdd(&g_art_stats[k], 1u
 // immediates (node arrays 128-aligned): 10 address VALU per visit instead of 15
 #define ART_NF_XOR 1
 #endif
+#ifndef ART_SPH_PRE_G
+#define ART_SPH_PRE_G 1  // r3w: Next-Week final +1.4 %, Cornell smoke +-0
+#endif
 #ifndef ART_TRI112
 #define ART_TRI112 1  // LM 1 (PL 2) kernels test leaf triangles from TriRec112 records (plane precomputed)
 #endif
@@ -911,8 +914,11 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
     // L: |d|^2 and its reciprocal for the leaf root divisions (div_rcp).  A traced direction is never zero (camera
     // rays point at the focus plane, scatter directions pass near_zero / dot(d, n) > 0) and its components are 0 or
     // differences of scene-scale doubles, so |d|^2 lies far inside div_rcp's range (> 2^-500, < 2^16).
-    const R d_a = L ? len2(r.d) : R(0);
-    const R d_inv_a = L ? R(1) / d_a : R(0);
+    // ART_SPH_PRE_G: the same for the HBM-scene traversal of triangle-free kernels (leaf spheres: the Next-Week final's
+    // cluster, the Cornell and two-sphere scenes); their directions are camera rays and scatter directions too
+    constexpr bool kSphPre = !L && ART_SPH_PRE_G && (F & F_SPHERE) != 0 && (F & F_TRI) == 0 && ART_LEAF_PRIMS_G;
+    const R d_a = (L || kSphPre) ? len2(r.d) : R(0);
+    const R d_inv_a = (L || kSphPre) ? R(1) / d_a : R(0);
     bool hit = false;
     // PK (k_paths_g instantiations with F_CODE16): the HBM-scene traversal sorts packed keys as the LDS variant does,
     // with the node's 16-bit child codes (BvhNode::pad, layout.h make_leaf16) in the low half of each key; codes,
@@ -1322,7 +1328,19 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                     PrimRec80 rec;
                     uint4* rp = reinterpret_cast<uint4*>(rec.b);
                     rp[0] = v0; rp[1] = v1; rp[2] = v2; rp[3] = v3; rp[4] = v4;
-                    h = hit_prim_rec<R, F>(primref_type(ref), rec, r, tmin, tmax, tt, fc);
+                    if constexpr (kSphPre) {
+                        // spheres with the ray's |d|^2 and its reciprocal (div_rcp roots), as the LDS variant
+                        if (primref_type(ref) == PRIM_SPHERE) {
+                            const SphereRec<R>& sr = reinterpret_cast<const SphereRec<R>&>(rec);
+                            V3<R> center = ld3(sr.c);
+                            if (sr.flags & SPH_MOVING) center = moving_center(center, ld3(sr.d), sr.t0, sr.dt, r.tm);
+                            h = sphere_root<R, true>(center, sr.r * sr.r, r, d_a, d_inv_a, tmin, tmax, tt);
+                        } else {
+                            h = hit_prim_rec<R, F & ~F_SPHERE>(primref_type(ref), rec, r, tmin, tmax, tt, fc);
+                        }
+                    } else {
+                        h = hit_prim_rec<R, F>(primref_type(ref), rec, r, tmin, tmax, tt, fc);
+                    }
                 } else {
                     ref = S.primrefs[slot];
                     h = hit_prim<R, F>(S, ref, r, tmin, tmax, tt, fc);
