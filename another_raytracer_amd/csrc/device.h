@@ -730,6 +730,10 @@ __device__ __forceinline__ void stat_lane(int k) { atomicAdd(&g_art_stats[k], 1u
 // immediates (node arrays 128-aligned): 10 address VALU per visit instead of 15
 #define ART_NF_XOR 1
 #endif
+#ifndef ART_LM2_COMPACT
+#define ART_LM2_COMPACT 0
+#endif
+constexpr uint32_t kLdsCompactNode = 112;  // LM 2 LDS node: 6 planes (96 B) + 16-bit codes (8 B) + 8 B pad
 #ifndef ART_SPH_PRE_G
 #define ART_SPH_PRE_G 1  // r3w: Next-Week final +1.4 %, Cornell smoke +-0
 #endif
@@ -1049,8 +1053,15 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
             } else if (PL == 2 || (PL == 1 && static_cast<uint32_t>(node) < S.n_lds_nodes)) {  // PL 2: every node in LDS
                 // the top levels, copied into LDS: explicit LDS loads (a generic pointer here would be merged with
                 // the global branch's into flat loads)
-                const uint32_t a = S.nodes_lds + static_cast<uint32_t>(node) * static_cast<uint32_t>(sizeof(BvhNode));
-                if (ART_NEAR_FAR_G && ART_NF_XOR) {
+                // kCompact (LM 2, ART_LM2_COMPACT): 112-B LDS nodes (the 96 B of planes, the 16-bit codes at +96), so
+                // ~15 % more of the tree fits; the far plane is at a - sign * 16 + 16 (a is only 16-aligned)
+                constexpr bool kCompact = PL == 1 && ART_LM2_COMPACT && PK && ART_NEAR_FAR_G;
+                const uint32_t a = S.nodes_lds + static_cast<uint32_t>(node) * (kCompact ? kLdsCompactNode : static_cast<uint32_t>(sizeof(BvhNode)));
+                if (kCompact) {
+                    const uint32_t nx = a + nfx, ny = a + nfy, nz = a + nfz, fx = a - nfx, fy = a - nfy, fz = a - nfz;
+                    lx = lds_f4(nx); hx = lds_f4(fx + 16u); ly = lds_f4(ny + 32u); hy = lds_f4(fy + 48u);
+                    lz = lds_f4(nz + 64u); hz = lds_f4(fz + 80u);
+                } else if (ART_NEAR_FAR_G && ART_NF_XOR) {
                     // node addresses are multiples of 32 (the LDS node array is 128-aligned): near plane = a + sign * 16,
                     // far plane = near ^ 16, and the y / z planes' +32 / +64 ride in the loads' immediate offsets
                     const uint32_t nx = a + nfx, ny = a + nfy, nz = a + nfz;
@@ -1063,7 +1074,7 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                     lx = lds_f4(a); hx = lds_f4(a + 16); ly = lds_f4(a + 32); hy = lds_f4(a + 48); lz = lds_f4(a + 64); hz = lds_f4(a + 80);
                 }
                 if constexpr (PK) {  // the four 16-bit codes (BvhNode::pad), codes 1 and 3 in the high halves
-                    const uint2 cw = lds_u2(a + 112);
+                    const uint2 cw = lds_u2(a + (kCompact ? 96u : 112u));
                     ch = make_int4(static_cast<int32_t>(cw.x), static_cast<int32_t>(cw.x), static_cast<int32_t>(cw.y), static_cast<int32_t>(cw.y));
                 } else {
                     ch = lds_i4(a + 96);

@@ -998,6 +998,7 @@ __host__ __device__ constexpr size_t paths_g_world_bytes(int32_t nworld, uint32_
 }
 // LM 1's LDS copy of the triangle records: TriRec112 (ART_TRI112) or TriRec
 constexpr bool kLm1Pl = ART_LM1_PL && ART_NF_XOR;      // LM 1 reads its nodes through traverse's PL 2 path
+template <uint32_t F> constexpr bool kLm2CompactF = ART_LM2_COMPACT && ART_NEAR_FAR_G && (F & F_CODE16) != 0;  // device.h kCompact
 constexpr bool kLm1Tri112 = ART_TRI112 && kLm1Pl;        // ... and its leaf triangles from TriRec112 (traverse)
 constexpr size_t kLm1TriBytes = kLm1Tri112 ? sizeof(TriRec112<double>) : sizeof(TriRec<double>);
 __host__ __device__ constexpr size_t paths_g_mesh_bytes(uint32_t n_nodes, uint32_t n_primrefs, uint32_t n_tris) {  // n_tris: 0 unless F_TRI
@@ -1010,6 +1011,7 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
     // explicit-LDS node reads (traverse's PL path): LM 2 for its LDS part; LM 1 for every node with ART_LM1_PL (the
     // XOR near/far addressing needs the explicit LDS addresses; through the LDS-inferred pointer it costs more adds)
     constexpr int kLdsNodesPL = LM == 2 ? 1 : (LM == 1 && kLm1Pl) ? 2 : 0;
+    constexpr bool kLm2Compact = LM == 2 && kLm2CompactF<F>;
     constexpr int B = LM ? kBlockM : kBlock;
     // dynamic LDS: [traversal stack: g.stack entries x B lanes (+ sentinel row)][camera][pass geometry][LM: nodes,
     // primrefs, triangles] -- as in k_paths, the camera and pass geometry are read from LDS where a path starts (as
@@ -1052,7 +1054,14 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
         BvhNode* m = reinterpret_cast<BvhNode*>(smem + lm_off);
         const uint4* s4 = reinterpret_cast<const uint4*>(S0.nodes);
         uint4* d4 = reinterpret_cast<uint4*>(m);
-        for (uint32_t i = threadIdx.x; i < S0.n_lds_nodes * (sizeof(BvhNode) / 16); i += B) d4[i] = s4[i];
+        if constexpr (kLm2Compact) {  // 112-B nodes: the six planes, then the 16-B word holding the 16-bit codes
+            for (uint32_t i = threadIdx.x; i < S0.n_lds_nodes * 7u; i += B) {
+                const uint32_t n = i / 7u, c = i - n * 7u;
+                d4[i] = s4[n * 8u + (c < 6u ? c : 7u)];
+            }
+        } else {
+            for (uint32_t i = threadIdx.x; i < S0.n_lds_nodes * (sizeof(BvhNode) / 16); i += B) d4[i] = s4[i];
+        }
         S.nodes_lds = static_cast<uint32_t>(reinterpret_cast<size_t>((__attribute__((address_space(3))) BvhNode*)m));
     }
     if constexpr (LM == 1) {
@@ -2288,7 +2297,8 @@ static void launch_paths_g_ft(int num_cu, hipStream_t st, const DevScene<double>
 #if ART_LDS_PARTIAL
     // too large for LM 1: as many of the first (top-level) nodes as fit beside the stacks
     const size_t head = align128(lm_head);
-    const uint32_t fit = head < kPathsGLdsCap ? static_cast<uint32_t>((kPathsGLdsCap - head) / sizeof(BvhNode)) : 0u;
+    const size_t node_bytes = kLm2CompactF<F> ? kLdsCompactNode : sizeof(BvhNode);
+    const uint32_t fit = head < kPathsGLdsCap ? static_cast<uint32_t>((kPathsGLdsCap - head) / node_bytes) : 0u;
     if (S.n_nodes > 0 && fit >= kLdsPartialMinNodes) {
         DevScene<double> SP = S;
         // ART_LDS_NODES_MAX (diagnostic): a cap on the LDS-resident nodes, to measure what each one is worth
@@ -2297,7 +2307,7 @@ static void launch_paths_g_ft(int num_cu, hipStream_t st, const DevScene<double>
             return e ? static_cast<uint32_t>(std::atoi(e)) : 0xFFFFFFFFu;
         }();
         SP.n_lds_nodes = std::min<uint32_t>(std::min<uint32_t>(fit, S.n_nodes), std::max<uint32_t>(cap, kLdsPartialMinNodes));
-        const size_t lds_p = head + sizeof(BvhNode) * SP.n_lds_nodes;
+        const size_t lds_p = head + node_bytes * SP.n_lds_nodes;
         const int blocks = blocks_per_cu(reinterpret_cast<const void*>(k_paths_g<F, TF, 2>), kBlockM, lds_p) * num_cu;
         check_ring_waves(blocks, kBlockM, num_cu);
         hipLaunchKernelGGL((k_paths_g<F, TF, 2>), dim3(blocks), dim3(kBlockM), lds_p, st, SP, g, cam, w, next_slot);
