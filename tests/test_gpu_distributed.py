@@ -40,3 +40,24 @@ def test_ranks_on_libart_rebuild_the_single_gpu_frame(gpu, world, tmp_path):
     eng.run(ref)
     assert np.array_equal(np.load(out), ref)
     assert BAND == 8
+
+
+@pytest.mark.parametrize("n", range(1, 9))
+def test_device_unpack_of_gathered_blocks(gpu, n):
+    """What rank 0 runs after the RCCL gather of bench.py --gpus N under torchrun (gather_frame): unpack_bands on CUDA
+    tensors (libart's unpack kernel on torch's stream) rebuilds the frame from the N padded blocks, padding rows ignored,
+    for heights that do not divide into band_rows x N and odd row byte counts."""
+    import torch
+    from another_raytracer_amd.distributed import band_rows_of, block_rows, unpack_bands
+    rng = np.random.default_rng(100 + n)
+    for H, W, band_rows in ((1080, 1920, 8), (1081, 37, 8), (37, 5, 1), (9, 64, 7)):
+        frame = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+        blk = block_rows(H, band_rows, n)
+        packed = np.full((n * blk, W, 3), 0xAB, np.uint8)
+        for r in range(n):
+            rows = band_rows_of(H, band_rows, n, r)
+            packed[r * blk: r * blk + len(rows)] = frame[rows]
+        out = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda:0")
+        unpack_bands(torch.from_numpy(packed).to("cuda:0"), out, H, band_rows, n)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), frame), (H, W, band_rows, n)
