@@ -668,7 +668,8 @@ constexpr uint32_t kPathChunk = 256;
 #define ART_RAY_POOL 1
 #endif
 #ifndef ART_RAY_POOL_G
-#define ART_RAY_POOL_G 0  // the same ring in k_paths_g: measured -1 % to -4 % (cow, final, dino, capsule, scene 7)
+#define ART_RAY_POOL_G 0  // the same ring in k_paths_g: measured -1 % to -4 % (cow, final, dino, capsule, scene 7); r3y
+                          // with the 96-entry XCD rings: cow -2.6 %, final -0.8 %, dino -0.9 %
 #endif
 // ART_POOL_RING: ring entries per wave.  128: two batches of 64, refilled when a batch's worth is free, so a round's
 // takers always find entries; 96 (default): refilled when at most 32 are left, so a round with more takers than
