@@ -43,7 +43,8 @@
 #endif
 
 // ART_SPLIT_PATHS (Makefile): unset = one translation unit; 1 = everything but k_paths and its launcher; 2 = only
-// k_paths and its launcher (kernels_paths.o, compiled with its own scheduler strategy, measured best for it alone).
+// k_paths and its launcher (kernels_paths.o, compiled with its own scheduler strategy, measured best for it alone);
+// 3 = only the k_paths_g instantiations ART_SPLIT_MESH moves out of the main object (kernels_mesh.o, likewise).
 #ifndef ART_SPLIT_PATHS
 #define ART_SPLIT_PATHS 0
 #endif
@@ -787,7 +788,7 @@ __host__ __device__ constexpr size_t paths_lds_head(uint32_t stack) {
     return ((kLdsImageBytes + paths_stack_bytes(stack) + kJumpBytes + sizeof(CameraRec<double>) + sizeof(PassGeom)) + 15u) & ~size_t(15);
 }
 __host__ __device__ constexpr size_t paths_lds_bytes(uint32_t stack) { return paths_lds_head(stack) + kPathsWorldBytes; }
-#if ART_SPLIT_PATHS != 1
+#if ART_SPLIT_PATHS == 0 || ART_SPLIT_PATHS == 2
 __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S0, PassGeom g, CameraRec<double> cam, Work<double> w, uint32_t* next_slot) {
     using R = double;
     constexpr int B = kBlockL;
@@ -943,7 +944,7 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S0, PassG
 #endif
 }
 
-#endif  // ART_SPLIT_PATHS != 1
+#endif  // ART_SPLIT_PATHS == 0 || ART_SPLIT_PATHS == 2
 
 // Persistent paths over the HBM scene (EXT_MEGA_G): the k_paths loop for every scene that does not fit the LDS
 // image (triangles, rects, boxes, transforms, media, noise/image textures).  A lane owns one path from its camera
@@ -1315,6 +1316,26 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
 #endif
 }
 
+// ART_CODE16_G: k_paths_g instantiations without F_MEDIA_G sort packed keys over 16-bit child codes (F_CODE16); a scene
+// whose codes do not fit them (more than 32768 nodes or 8192 primitive references) takes the F_ALL kernel instead
+#ifndef ART_CODE16_G
+#define ART_CODE16_G 1
+#endif
+// ART_SPLIT_MESH (Makefile, SPLIT=1): the instantiations for meshes with solid/checker textures whose BVH is not all in
+// LDS (LM 0 / 2: cow) are compiled in kernels_mesh.o (ART_SPLIT_PATHS=3) with LLVM's max-ilp scheduler (MESH_SCHED):
+// cow +1.1 %, while the other k_paths_g kernels lose 0.4-0.5 % under it (r3z2)
+#ifndef ART_SPLIT_MESH
+#define ART_SPLIT_MESH 0
+#endif
+constexpr uint32_t kMeshG = kFeatMesh | (ART_CODE16_G ? F_CODE16 : 0u);
+#if ART_SPLIT_PATHS == 3
+template __global__ void k_paths_g<kMeshG, kTexBasic, 0>(DevScene<double>, PassGeom, CameraRec<double>, Work<double>, uint32_t*);
+template __global__ void k_paths_g<kMeshG, kTexBasic, 2>(DevScene<double>, PassGeom, CameraRec<double>, Work<double>, uint32_t*);
+#elif ART_SPLIT_MESH
+extern template __global__ void k_paths_g<kMeshG, kTexBasic, 0>(DevScene<double>, PassGeom, CameraRec<double>, Work<double>, uint32_t*);
+extern template __global__ void k_paths_g<kMeshG, kTexBasic, 2>(DevScene<double>, PassGeom, CameraRec<double>, Work<double>, uint32_t*);
+#endif
+
 // Input: the kShards shards of material queue M at depth d (the extend stage sorted hits by material type).
 template <class R, uint32_t F, uint32_t M, uint32_t TF>
 __global__ __launch_bounds__(kBlock) void k_shade(DevScene<R> S, PassGeom g, Work<R> w, int d) {
@@ -1413,7 +1434,7 @@ __global__ __launch_bounds__(256) void k_accum_images(PassGeom g, Work<R> w, dou
     q[2] = qb;
 }
 
-#if ART_SPLIT_PATHS != 2
+#if ART_SPLIT_PATHS <= 1
 // Ray queries (rt_trace_rays): the world's closest hit (hittable_list::hit, hittable_list.cpp:5-19) of n caller-given
 // rays through the renderer's own traversal -- the LDS image (L) or the HBM scene -- and the surface normal
 // (hit_record::set_face_normal), so traversal edge cases (axis-parallel rays, origins on faces) can be checked one ray
@@ -1601,9 +1622,9 @@ __global__ void k_adapt_fill(int32_t* work, uint8_t* rgb, int W, int rows, int s
     for (int c = 0; c < 3; ++c) rgb[3 * static_cast<size_t>(p) + c] = static_cast<uint8_t>(o[c]);
 }
 
-#endif  // ART_SPLIT_PATHS != 2
+#endif  // ART_SPLIT_PATHS <= 1
 
-#if ART_SPLIT_PATHS != 2
+#if ART_SPLIT_PATHS <= 1
 // ------------------------------------------------------------------------------------------------ device scene
 template <class R>
 struct DeviceScene {
@@ -2210,7 +2231,7 @@ static int blocks_per_cu(const void* kernel, int block, size_t lds) {
     cache.emplace(key, per_cu);
     return per_cu;
 }
-#if ART_SPLIT_PATHS != 2
+#if ART_SPLIT_PATHS <= 1
 template <class R, uint32_t F, uint32_t M, uint32_t TF>
 static int shade_blocks(int num_cu) {
     return blocks_per_cu(reinterpret_cast<const void*>(k_shade<R, F, M, TF>), kBlock, 0) * num_cu;
@@ -2320,11 +2341,6 @@ static void launch_paths_g_ft(int num_cu, hipStream_t st, const DevScene<double>
     check_ring_waves(blocks, kBlock, num_cu);
     hipLaunchKernelGGL((k_paths_g<F, TF, 0>), dim3(blocks), dim3(kBlock), lds, st, S, g, cam, w, next_slot);
 }
-// ART_CODE16_G: k_paths_g instantiations without F_MEDIA_G sort packed keys over 16-bit child codes (F_CODE16); a scene
-// whose codes do not fit them (more than 32768 nodes or 8192 primitive references) takes the F_ALL kernel instead
-#ifndef ART_CODE16_G
-#define ART_CODE16_G 1
-#endif
 static void launch_paths_g(uint32_t feat, bool tex_basic, bool codes16, int num_cu, hipStream_t st, const DevScene<double>& S, const PassGeom& g,
                            const CameraRec<double>& cam, const Work<double>& w, uint32_t* next_slot) {
     constexpr uint32_t C = ART_CODE16_G ? F_CODE16 : 0u;
@@ -2355,7 +2371,7 @@ static void launch_paths_g(uint32_t feat, bool tex_basic, bool codes16, int num_
 #else
 #define ART_PATHS_LINKAGE
 #endif
-#if ART_SPLIT_PATHS != 1
+#if ART_SPLIT_PATHS == 0 || ART_SPLIT_PATHS == 2
 ART_PATHS_LINKAGE void launch_paths(int num_cu, hipStream_t st, const DevScene<double>& S, const PassGeom& g, const CameraRec<double>& cam,
                          const Work<double>& w, uint32_t* next_slot) {
     const size_t lds = paths_lds_bytes(g.stack);
@@ -2368,7 +2384,7 @@ ART_PATHS_LINKAGE void launch_paths(int num_cu, hipStream_t st, const DevScene<d
 void launch_paths(int num_cu, hipStream_t st, const DevScene<double>& S, const PassGeom& g, const CameraRec<double>& cam,
                   const Work<double>& w, uint32_t* next_slot);  // kernels_paths.o
 #endif
-#if ART_SPLIT_PATHS != 2
+#if ART_SPLIT_PATHS <= 1
 template <class R>
 static void bounce(const DeviceScene<R>& ds, int variant, int num_cu, hipStream_t st, const PassGeom& g, const CameraRec<R>& cam, const Work<R>& w,
                    int d, const std::function<void()>& mark) {
@@ -2713,10 +2729,10 @@ void Renderer::render(const CameraRec<double>& cam, const RenderParams& p, uint8
     render_impl<double>(*impl_, impl_->s64, cam, p, out_rgb, out_acc, stats);
 }
 
-#endif  // ART_SPLIT_PATHS != 2
+#endif  // ART_SPLIT_PATHS <= 1
 }  // namespace art
 
-#if ART_SPLIT_PATHS != 2
+#if ART_SPLIT_PATHS <= 1
 namespace art {
 int device_count() {
     int n = 0;
