@@ -1322,8 +1322,9 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
 #define ART_CODE16_G 1
 #endif
 // ART_SPLIT_MESH (Makefile, SPLIT=1): the instantiations for meshes with solid/checker textures whose BVH is not all in
-// LDS (LM 0 / 2: cow) are compiled in kernels_mesh.o (ART_SPLIT_PATHS=3) with LLVM's max-ilp scheduler (MESH_SCHED):
-// cow +1.1 %, while the other k_paths_g kernels lose 0.4-0.5 % under it (r3z2)
+// LDS (LM 0 / 2: cow) are compiled in kernels_mesh.o (ART_SPLIT_PATHS=3) with LLVM's iterative-maxocc scheduler
+// (MESH_SCHED): cow +1.3 % to +1.8 % over the default scheduler; dino's LM 1 kernel loses 0.9 % under it and the Next-Week
+// final's 4.6 % (its spills double), so they stay in kernels.o (r3z2)
 #ifndef ART_SPLIT_MESH
 #define ART_SPLIT_MESH 0
 #endif
