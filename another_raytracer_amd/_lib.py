@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("ART_LIB") or os.path.join(_HERE, "libart.so")  # ART_
 
 RT_OK = 0
 RT_FP64 = 0  # the only fp_mode since ABI 2 (include/art.h)
-RT_ABI_VERSION = 3
+RT_ABI_VERSION = 4
 RT_OUT_DEVICE, RT_PROFILE, RT_GLOBAL_SCENE, RT_SPLIT_SHADE, RT_ADAPTIVE, RT_WAVEFRONT, RT_PARALLEL_IMAGES = 1, 2, 4, 8, 16, 32, 64
 ERRORS = {-1: "RT_E_INVALID", -2: "RT_E_SCENE", -3: "RT_E_DEVICE", -4: "RT_E_INTERNAL"}
 
@@ -58,6 +58,15 @@ class rt_scene_info(ctypes.Structure):
                 ("max_bvh_depth", ctypes.c_int32), ("device_bytes_f64", ctypes.c_uint64)]
 
 
+class rt_multi_times(ctypes.Structure):
+    _fields_ = [("total_ms", ctypes.c_double), ("render_ms_max", ctypes.c_double), ("render_ms_min", ctypes.c_double),
+                ("gather_ms", ctypes.c_double), ("unpack_ms", ctypes.c_double), ("wait_ms", ctypes.c_double),
+                ("collectives", ctypes.c_uint64), ("slowest_device", ctypes.c_int32), ("ngpus", ctypes.c_int32)]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
 # rt_progress_fn (include/art.h): int (*)(void* user, int32_t samples_done, int32_t spp, const uint8_t*, const double*)
 rt_progress_fn = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p)
 
@@ -84,7 +93,7 @@ SIGNATURES = {
     "rt_image_free": (None, [ctypes.POINTER(ctypes.c_uint8)]),
     "rt_local_rows": (_I, [ctypes.POINTER(rt_params), ctypes.POINTER(ctypes.c_int32)]),
     "rt_band_block_rows": (_I, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
-    "rt_unpack_bands": (_I, [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P]),
+    "rt_unpack_bands": (_I, [_P, _S, _P, _S, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P]),
     "rt_multi_create": (_I, [ctypes.c_char_p, ctypes.c_char_p, _IP, _I, ctypes.POINTER(_P)]),
     "rt_multi_from_graph": (_I, [_P, _IP, _I, ctypes.POINTER(_P)]),
     "rt_multi_destroy": (None, [_P]),
@@ -92,6 +101,7 @@ SIGNATURES = {
     "rt_multi_ngpus": (_I, [_P]),
     "rt_multi_scene_info": (_I, [_P, ctypes.POINTER(rt_scene_info)]),
     "rt_multi_device_stats": (_I, [_P, _I, ctypes.POINTER(rt_stats)]),
+    "rt_multi_times_get": (_I, [_P, ctypes.POINTER(rt_multi_times)]),
     "rt_graph_new": (_P, []),
     "rt_graph_free": (None, [_P]),
     "rt_graph_random_double": (_I, [_P, _DP]),
@@ -157,25 +167,62 @@ def dvec(v):
     return (ctypes.c_double * 3)(*[float(x) for x in v])
 
 
-def kernel_build_id(path=None):
-    """Identity of the device code in libart.so: the first 16 hex digits of the SHA-256 of its `.hip_fatbin` ELF section
-    (the gfx950 code objects of every kernel; host-only rebuilds keep it).  PMC summaries (tools/pmc_summary.py) are
-    stamped with it, and bench.py uses a summary's per-segment counters only when the stamp equals the loaded build."""
-    import hashlib
+def _elf_sections(data):
+    """(name, type, offset, size) of every section of a little-endian ELF64 image."""
     import struct
-    with open(path or LIB_PATH, "rb") as f:
-        data = f.read()
     if data[:4] != b"\x7fELF" or data[4] != 2 or data[5] != 1:
         raise ValueError("not a little-endian ELF64 file")
     shoff, = struct.unpack_from("<Q", data, 0x28)
     shentsize, shnum, shstrndx = struct.unpack_from("<HHH", data, 0x3A)
-    def sec(i):
-        name, _typ, _flags, _addr, off, size = struct.unpack_from("<IIQQQQ", data, shoff + i * shentsize)
-        return name, off, size
-    _, stroff, _ = sec(shstrndx)
-    for i in range(shnum):
-        name, off, size = sec(i)
-        end = data.index(b"\0", stroff + name)
-        if data[stroff + name:end] == b".hip_fatbin":
-            return hashlib.sha256(data[off:off + size]).hexdigest()[:16]
-    raise ValueError("no .hip_fatbin section")
+    hdr = [struct.unpack_from("<IIQQQQ", data, shoff + i * shentsize) for i in range(shnum)]
+    stroff = hdr[shstrndx][4]
+    return [(data[stroff + h[0]:data.index(b"\0", stroff + h[0])].decode(), h[1], h[4], h[5]) for h in hdr]
+
+
+# the parts of a gfx950 code object that define what runs: kernel metadata (register and LDS use, arguments), kernel
+# descriptors and machine code -- not the symbol tables, which carry hipcc's path-derived __hip_cuid_* names
+_CODE_SECTIONS = (".note", ".rodata", ".text")
+
+
+def kernel_build_id(path=None):
+    """Identity of the device code in libart.so: the first 16 hex digits of a SHA-256 over the `.note`, `.rodata` and
+    `.text` sections of every gfx950 code object in its `.hip_fatbin` offload bundles, in bundle order.  It depends on
+    the kernels alone: host-only rebuilds, and rebuilds of the same sources at another path (whose `__hip_cuid_*` symbol
+    names differ), keep it.  PMC summaries (tools/pmc_summary.py) are stamped with it, and bench.py uses a summary's
+    per-segment counters only when the stamp equals the loaded build."""
+    import hashlib
+    import struct
+    with open(path or LIB_PATH, "rb") as f:
+        data = f.read()
+    fb = [s for s in _elf_sections(data) if s[0] == ".hip_fatbin"]
+    if not fb:
+        raise ValueError("no .hip_fatbin section")
+    _, _, off, size = fb[0]
+    fat = data[off:off + size]
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    h = hashlib.sha256()
+    pos, objects = 0, 0
+    while True:
+        b = fat.find(magic, pos)
+        if b < 0:
+            break
+        n, = struct.unpack_from("<Q", fat, b + len(magic))
+        p = b + len(magic) + 8
+        for _ in range(n):
+            eoff, esize, tlen = struct.unpack_from("<QQQ", fat, p)
+            triple = fat[p + 24:p + 24 + tlen]
+            p += 24 + tlen
+            if not triple.startswith(b"hipv4-amdgcn") or esize == 0:
+                continue
+            co = fat[b + eoff:b + eoff + esize]
+            if co[:4] != b"\x7fELF":
+                raise ValueError("compressed or unknown code object in the offload bundle")
+            h.update(triple)
+            for name, typ, soff, ssize in _elf_sections(co):
+                if name in _CODE_SECTIONS:
+                    h.update(name.encode() + struct.pack("<Q", ssize) + co[soff:soff + ssize])
+            objects += 1
+        pos = b + 1
+    if objects == 0:
+        raise ValueError("no gfx950 code object in .hip_fatbin")
+    return h.hexdigest()[:16]

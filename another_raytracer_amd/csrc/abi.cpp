@@ -241,11 +241,19 @@ int rt_band_block_rows(int32_t height, int32_t band_rows, int32_t n) {
     return art::band_block_rows(height, band_rows, n);
 }
 
-int rt_unpack_bands(const uint8_t* packed, uint8_t* frame, int32_t width, int32_t height, int32_t band_rows, int32_t n, int32_t flags,
-                    void* stream) {
+int rt_unpack_bands(const uint8_t* packed, size_t packed_bytes, uint8_t* frame, size_t frame_bytes, int32_t width, int32_t height,
+                    int32_t band_rows, int32_t n, int32_t flags, void* stream) {
     if (!packed || !frame) return fail(RT_E_INVALID, "packed and frame must be non-NULL");
     if (width < 1 || height < 1 || band_rows < 1 || n < 1) return fail(RT_E_INVALID, "width, height, band_rows and n must be >= 1");
     if (static_cast<int64_t>(width) * height > (int64_t(1) << 31)) return fail(RT_E_INVALID, "image too large");
+    const size_t row_bytes = static_cast<size_t>(width) * 3;
+    const size_t want_packed = static_cast<size_t>(n) * static_cast<size_t>(art::band_block_rows(height, band_rows, n)) * row_bytes;
+    const size_t want_frame = static_cast<size_t>(height) * row_bytes;
+    if (packed_bytes != want_packed)
+        return fail(RT_E_INVALID, "packed holds " + std::to_string(packed_bytes) + " bytes, the layout needs n * band_block_rows * width * 3 = " +
+                                      std::to_string(want_packed) + " (every rank's padded block)");
+    if (frame_bytes != want_frame)
+        return fail(RT_E_INVALID, "frame holds " + std::to_string(frame_bytes) + " bytes, height * width * 3 = " + std::to_string(want_frame));
     return guard(RT_E_DEVICE, [&] {
         art::unpack_bands(packed, frame, width, height, band_rows, n, (flags & RT_OUT_DEVICE) != 0, stream);
         return RT_OK;
@@ -374,6 +382,21 @@ int rt_multi_scene_info(const rt_multi* m, rt_scene_info* info) {
     view.aperture = m->graph.aperture;
     fill_info(view, m->flat, info);
     info->device_bytes_f64 = m->renderer->scene_bytes();
+    return RT_OK;
+}
+int rt_multi_times_get(const rt_multi* m, rt_multi_times* out) {
+    if (!m || !out) return fail(RT_E_INVALID, "multi and out must be non-NULL");
+    const art::MultiTimes& t = m->renderer->times();
+    std::memset(out, 0, sizeof *out);
+    out->total_ms = t.total_ms;
+    out->render_ms_max = t.render_ms_max;
+    out->render_ms_min = t.render_ms_min;
+    out->gather_ms = t.gather_ms;
+    out->unpack_ms = t.unpack_ms;
+    out->wait_ms = t.wait_ms;
+    out->collectives = t.collectives;
+    out->slowest_device = t.slowest_device;
+    out->ngpus = t.ngpus;
     return RT_OK;
 }
 int rt_multi_ngpus(const rt_multi* m) {

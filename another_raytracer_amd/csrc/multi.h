@@ -16,6 +16,13 @@
 
 namespace art {
 
+// Phases of the last render (include/art.h rt_multi_times).
+struct MultiTimes {
+    double total_ms = 0, render_ms_max = 0, render_ms_min = 0, gather_ms = 0, unpack_ms = 0, wait_ms = 0;
+    uint64_t collectives = 0;
+    int slowest_device = 0, ngpus = 0;
+};
+
 class MultiRenderer {
 public:
     struct Impl;
@@ -32,6 +39,7 @@ public:
     size_t scene_bytes() const;  // scene bytes on each device
     // Stats of device k (devices[k]) in the last render: its segments, its own kernel times and launches, its rows.
     bool device_stats(int k, RenderStats& out) const;
+    const MultiTimes& times() const;
 
 private:
     Impl* impl_;

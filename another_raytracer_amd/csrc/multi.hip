@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <memory>
@@ -99,6 +100,22 @@ struct DeviceBuf {
     }
 };
 
+// Every RCCL call of a non-blocking communicator may return ncclInProgress: the operation then completes in the
+// background and ncclCommGetAsyncError reports its state.
+static bool rccl_ok(ncclResult_t r) { return r == ncclSuccess || r == ncclInProgress; }
+#define RCCL_ISSUE(x)                                                                                          \
+    do {                                                                                                       \
+        ncclResult_t r_ = (x);                                                                                 \
+        if (!rccl_ok(r_)) throw std::runtime_error(std::string(#x) + ": " + ncclGetErrorString(r_));       \
+    } while (0)
+
+using Clock = std::chrono::steady_clock;
+static Clock::time_point deadline_from_now() {
+    const char* s = std::getenv("ART_MULTI_TIMEOUT_MS");
+    const double ms = (!s || !*s) ? 120000.0 : std::max(0.0, std::strtod(s, nullptr));
+    return Clock::now() + std::chrono::duration_cast<Clock::duration>(std::chrono::duration<double, std::milli>(ms));
+}
+
 struct MultiRenderer::Impl {
     std::vector<int> devices;
     std::vector<std::unique_ptr<Renderer>> renderers;  // one per device (the scene uploaded on each)
@@ -106,19 +123,82 @@ struct MultiRenderer::Impl {
     std::vector<hipStream_t> streams;                  // gather / unpack streams, one per device
     std::vector<DeviceBuf> send;                       // packed local rows, one per device
     DeviceBuf recv, frame;                             // on devices[0]
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};    // on devices[0]: gather start, gather end, unpack end
     std::vector<RenderStats> last;                     // per-device stats of the last render
+    MultiTimes times;
+    std::string broken;                                // why the communicators were aborted ("" = usable)
 
     ~Impl() {
-        for (auto c : comms)
-            if (c) (void)ncclCommDestroy(c);
+        for (size_t k = 0; k < comms.size(); ++k)
+            if (comms[k]) {
+                (void)hipSetDevice(devices[k]);
+                (void)ncclCommDestroy(comms[k]);
+            }
         for (size_t k = 0; k < streams.size(); ++k)
             if (streams[k]) {
                 (void)hipSetDevice(devices[k]);
                 (void)hipStreamDestroy(streams[k]);
             }
+        if (!devices.empty()) (void)hipSetDevice(devices[0]);
+        for (auto e : ev)
+            if (e) (void)hipEventDestroy(e);
         for (auto& b : send) b.release();
         recv.release();
         frame.release();
+    }
+    // Aborts every communicator (ncclCommAbort: returns without waiting for peers or pending operations); the
+    // MultiRenderer then refuses to render.  Throws the reason.
+    [[noreturn]] void abort_all(const std::string& why) {
+        for (size_t k = 0; k < comms.size(); ++k)
+            if (comms[k]) {
+                (void)hipSetDevice(devices[k]);
+                (void)ncclCommAbort(comms[k]);
+                comms[k] = nullptr;
+            }
+        broken = why;
+        throw std::runtime_error(why + " (RCCL communicators aborted; destroy and re-create the rt_multi)");
+    }
+    // Polls until every communicator's pending operation (init, group launch) is done, an error shows, or the deadline
+    // passes.
+    void wait_comms(const char* what, std::chrono::steady_clock::time_point deadline) {
+        for (;;) {
+            bool pending = false;
+            for (size_t k = 0; k < comms.size(); ++k) {
+                ncclResult_t st = ncclSuccess;
+                const ncclResult_t r = ncclCommGetAsyncError(comms[k], &st);
+                if (r != ncclSuccess) abort_all(std::string(what) + ": ncclCommGetAsyncError: " + ncclGetErrorString(r));
+                if (st == ncclInProgress) pending = true;
+                else if (st != ncclSuccess) abort_all(std::string(what) + " on device " + std::to_string(devices[k]) + ": " + ncclGetErrorString(st));
+            }
+            if (!pending) return;
+            if (std::chrono::steady_clock::now() >= deadline) abort_all(std::string(what) + ": timed out (ART_MULTI_TIMEOUT_MS)");
+            std::this_thread::sleep_for(std::chrono::microseconds(50));
+        }
+    }
+    // Polls the gather streams (hipStreamQuery) and the communicators' asynchronous errors until every stream has
+    // drained, or aborts at the deadline: a stuck collective ends the call with RT_E_DEVICE instead of hanging it.
+    void wait_streams(const char* what, std::chrono::steady_clock::time_point deadline) {
+        std::vector<bool> done(streams.size(), false);
+        for (;;) {
+            bool all = true;
+            for (size_t k = 0; k < streams.size(); ++k) {
+                if (done[k]) continue;
+                HIP_CHECK(hipSetDevice(devices[k]));
+                const hipError_t q = hipStreamQuery(streams[k]);
+                if (q == hipSuccess) {
+                    done[k] = true;
+                    continue;
+                }
+                if (q != hipErrorNotReady) abort_all(std::string(what) + ": hipStreamQuery: " + hipGetErrorString(q));
+                all = false;
+                ncclResult_t st = ncclSuccess;
+                if (ncclCommGetAsyncError(comms[k], &st) != ncclSuccess || (st != ncclSuccess && st != ncclInProgress))
+                    abort_all(std::string(what) + " on device " + std::to_string(devices[k]) + ": " + ncclGetErrorString(st));
+            }
+            if (all) return;
+            if (std::chrono::steady_clock::now() >= deadline) abort_all(std::string(what) + ": timed out (ART_MULTI_TIMEOUT_MS)");
+            std::this_thread::sleep_for(std::chrono::microseconds(20));
+        }
     }
 };
 
@@ -135,8 +215,6 @@ MultiRenderer::MultiRenderer(const FlatScene& flat, const std::vector<int>& devi
     const int n = static_cast<int>(devices.size());
     impl_->devices = devices;
     for (int k = 0; k < n; ++k) impl_->renderers.push_back(std::make_unique<Renderer>(flat, devices[k]));
-    impl_->comms.assign(n, nullptr);
-    RCCL_CHECK(ncclCommInitAll(impl_->comms.data(), n, devices.data()));
     impl_->streams.assign(n, nullptr);
     impl_->send.resize(n);
     for (int k = 0; k < n; ++k) {
@@ -144,7 +222,26 @@ MultiRenderer::MultiRenderer(const FlatScene& flat, const std::vector<int>& devi
         HIP_CHECK(hipStreamCreateWithFlags(&impl_->streams[k], hipStreamNonBlocking));
         impl_->send[k].device = devices[k];
     }
+    HIP_CHECK(hipSetDevice(devices[0]));
+    for (auto& e : impl_->ev) HIP_CHECK(hipEventCreate(&e));
     impl_->recv.device = impl_->frame.device = devices[0];
+    // one communicator per device, rank k = devices[k], created as one group (what ncclCommInitAll does) but
+    // non-blocking, so that a stuck bootstrap ends at the deadline instead of hanging the caller
+    ncclUniqueId id;
+    RCCL_CHECK(ncclGetUniqueId(&id));
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    const char* blk = std::getenv("ART_RCCL_BLOCKING");  // diagnosis: 1 = blocking communicators
+    cfg.blocking = (blk && std::atoi(blk) == 1) ? 1 : 0;
+    impl_->comms.assign(n, nullptr);
+    const auto deadline = deadline_from_now();
+    RCCL_ISSUE(ncclGroupStart());
+    for (int k = 0; k < n; ++k) {
+        HIP_CHECK(hipSetDevice(devices[k]));
+        RCCL_ISSUE(ncclCommInitRankConfig(&impl_->comms[k], n, id, k, &cfg));
+    }
+    RCCL_ISSUE(ncclGroupEnd());
+    impl_->wait_comms("RCCL communicator init", deadline);
+    impl_->times.ngpus = n;
     guard.release();
 }
 
@@ -156,9 +253,11 @@ bool MultiRenderer::device_stats(int k, RenderStats& out) const {
     out = impl_->last[k];
     return true;
 }
+const MultiTimes& MultiRenderer::times() const { return impl_->times; }
 
 void MultiRenderer::render(const CameraRec<double>& cam, const RenderParams& p, uint8_t* out_rgb, bool out_device, RenderStats& stats) {
     Impl& I = *impl_;
+    if (!I.broken.empty()) throw std::runtime_error("rt_multi unusable: " + I.broken + " (destroy and re-create it)");
     const int n = static_cast<int>(I.devices.size());
     const int W = p.width, H = p.height, band_rows = std::max(1, p.band_rows);
     const int max_rows = band_block_rows(H, band_rows, n);
@@ -166,15 +265,21 @@ void MultiRenderer::render(const CameraRec<double>& cam, const RenderParams& p, 
     for (int k = 0; k < n; ++k) I.send[k].ensure(std::max<size_t>(block, 1));
     I.recv.ensure(std::max<size_t>(block * n, 1));
     if (!out_device) I.frame.ensure(row_bytes * H);
+    MultiTimes tm;
+    tm.ngpus = n;
+    tm.collectives = I.times.collectives;
 
-    const auto t0 = std::chrono::steady_clock::now();
+    using clock = std::chrono::steady_clock;
+    const auto t0 = clock::now();
     // phase 1: every device renders its bands into its send buffer (one host thread each; Renderer::render blocks)
     std::vector<RenderStats> st(n);
+    std::vector<double> rms(n, 0.0);
     std::vector<std::exception_ptr> err(n);
     std::vector<std::thread> pool;
     for (int k = 0; k < n; ++k)
         pool.emplace_back([&, k]() {
             try {
+                const auto a = clock::now();
                 RenderParams pk = p;
                 pk.band_rows = band_rows;
                 pk.band_count = n;
@@ -182,30 +287,59 @@ void MultiRenderer::render(const CameraRec<double>& cam, const RenderParams& p, 
                 pk.flags |= RT_OUT_DEVICE;
                 pk.stream = nullptr;  // the renderer's own stream on its device
                 I.renderers[k]->render(cam, pk, static_cast<uint8_t*>(I.send[k].p), nullptr, st[k]);
+                rms[k] = std::chrono::duration<double, std::milli>(clock::now() - a).count();
             } catch (...) {
                 err[k] = std::current_exception();
             }
         });
     for (auto& t : pool) t.join();
     for (auto& e : err)
-        if (e) std::rethrow_exception(e);  // no collective was started: every rank stays consistent
+        if (e) {
+            I.times = tm;  // no collective was started: every rank stays consistent and the multi usable
+            std::rethrow_exception(e);
+        }
+    tm.render_ms_max = tm.render_ms_min = rms[0];
+    for (int k = 1; k < n; ++k) {
+        if (rms[k] > tm.render_ms_max) {
+            tm.render_ms_max = rms[k];
+            tm.slowest_device = k;
+        }
+        tm.render_ms_min = std::min(tm.render_ms_min, rms[k]);
+    }
     // phase 2: one gather of the equal-sized packed blocks to devices[0] (rows past a band's end are padding)
-    RCCL_CHECK(ncclGroupStart());
+    const auto deadline = deadline_from_now();
+    HIP_CHECK(hipSetDevice(I.devices[0]));
+    HIP_CHECK(hipEventRecord(I.ev[0], I.streams[0]));
+    RCCL_ISSUE(ncclGroupStart());
     for (int k = 0; k < n; ++k) {
         HIP_CHECK(hipSetDevice(I.devices[k]));
-        RCCL_CHECK(ncclGather(I.send[k].p, k == 0 ? I.recv.p : nullptr, block, ncclUint8, 0, I.comms[k], I.streams[k]));
+        RCCL_ISSUE(ncclGather(I.send[k].p, k == 0 ? I.recv.p : nullptr, block, ncclUint8, 0, I.comms[k], I.streams[k]));
     }
-    RCCL_CHECK(ncclGroupEnd());
+    RCCL_ISSUE(ncclGroupEnd());
+    ++I.times.collectives;
+    tm.collectives = I.times.collectives;
+    I.times = tm;
+    // fault injection (tests): the collective fails while in flight, as a peer error or an expired deadline would
+    if (std::getenv("ART_FAULT_GATHER_ABORT")) I.abort_all("ncclGather: injected failure (ART_FAULT_GATHER_ABORT)");
+    const auto tw = clock::now();
+    I.wait_comms("ncclGather launch", deadline);  // non-blocking group: the gathers are enqueued once this returns
+    HIP_CHECK(hipSetDevice(I.devices[0]));
+    HIP_CHECK(hipEventRecord(I.ev[1], I.streams[0]));
+    I.wait_streams("ncclGather", deadline);
+    tm.wait_ms = std::chrono::duration<double, std::milli>(clock::now() - tw).count();
     // phase 3: the root places every row and hands the frame over
     HIP_CHECK(hipSetDevice(I.devices[0]));
     uint8_t* dst = out_device ? out_rgb : static_cast<uint8_t*>(I.frame.p);
     launch_unpack(static_cast<const uint8_t*>(I.recv.p), dst, W, H, band_rows, n, max_rows, I.streams[0]);
     if (!out_device) HIP_CHECK(hipMemcpyAsync(out_rgb, I.frame.p, row_bytes * H, hipMemcpyDeviceToHost, I.streams[0]));
-    for (int k = 0; k < n; ++k) {
-        HIP_CHECK(hipSetDevice(I.devices[k]));
-        HIP_CHECK(hipStreamSynchronize(I.streams[k]));
-    }
-    const auto t1 = std::chrono::steady_clock::now();
+    HIP_CHECK(hipEventRecord(I.ev[2], I.streams[0]));
+    HIP_CHECK(hipStreamSynchronize(I.streams[0]));
+    const auto t1 = clock::now();
+    float g_ms = 0.f, u_ms = 0.f;
+    HIP_CHECK(hipEventElapsedTime(&g_ms, I.ev[0], I.ev[1]));
+    HIP_CHECK(hipEventElapsedTime(&u_ms, I.ev[1], I.ev[2]));
+    tm.gather_ms = g_ms;
+    tm.unpack_ms = u_ms;
 
     I.last = st;
     stats = RenderStats{};
@@ -222,6 +356,8 @@ void MultiRenderer::render(const CameraRec<double>& cam, const RenderParams& p, 
     stats.samples_per_pass = st[0].samples_per_pass;
     stats.local_rows = H;
     stats.extend_variant = st[0].extend_variant;
+    tm.total_ms = stats.ms;
+    I.times = tm;
 }
 
 }  // namespace art

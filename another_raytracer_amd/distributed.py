@@ -9,7 +9,7 @@
 The reference splits an image into 4 contiguous row stripes on 4 threads (engine.h:335-376).  Here rank r of N
 renders every global row y with (y // band_rows) % N == r (band_rows = 8: sky rows are cheap and object rows
 expensive, so interleaving balances the load; 8-row bands keep the kernels' 8x8 pixel tiles on 8 consecutive image
-rows, and split 1080 rows over 8 GPUs as 136/135 rows where 16-row bands gave 144/128), packs its rows contiguously, and rank 0 gathers the packed RGB8
+rows, and split 1080 rows over 8 GPUs as seven ranks of 136 rows and one of 128, where 16-row bands gave 144/128), packs its rows contiguously, and rank 0 gathers the packed RGB8
 blocks (RCCL over xGMI; the only collective of the path) and un-interleaves them.  Every pixel's RNG stream is keyed
 by (seed, global pixel, sample), so the gathered image is bit-identical to a single-GPU render (tests/).
 """
@@ -19,7 +19,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from ._lib import RT_OUT_DEVICE, RT_PROFILE, check, lib, rt_params, rt_stats
+from ._lib import RT_OUT_DEVICE, RT_PROFILE, check, lib, rt_multi_times, rt_params, rt_stats
 
 DEFAULT_BAND_ROWS = 8
 
@@ -43,37 +43,52 @@ def block_rows(height, band_rows, world):
 def unpack_bands(packed, frame, height, band_rows, world, stream=None):
     """Places `world` concatenated band blocks (packed: [world * block_rows, W, 3] uint8) into frame [H, W, 3]: libart's
     rt_unpack_bands, the same code rt_render_multi runs after its ncclGather (a kernel on the tensors' device, on
-    `stream` or torch's current stream; numpy arrays are unpacked on the host)."""
+    `stream` or torch's current stream; numpy arrays are unpacked on the host).  Both shapes are checked against the
+    layout here, and rt_unpack_bands refuses buffers whose byte sizes do not match it."""
     width = int(frame.shape[1])
+    block = block_rows(height, band_rows, world)
+    if tuple(packed.shape) != (int(world) * block, width, 3):
+        raise ValueError(f"packed has shape {tuple(packed.shape)}, the {world}-way layout needs ({int(world) * block}, {width}, 3)")
+    if tuple(frame.shape) != (int(height), width, 3):
+        raise ValueError(f"frame has shape {tuple(frame.shape)}, expected ({int(height)}, {width}, 3)")
+    nbytes = lambda a: a.numel() * a.element_size() if isinstance(a, torch.Tensor) else a.nbytes
+    pbytes, fbytes = nbytes(packed), nbytes(frame)
     if isinstance(packed, torch.Tensor):
         assert packed.is_contiguous() and frame.is_contiguous() and packed.dtype == torch.uint8 and frame.dtype == torch.uint8
         if packed.is_cuda:
             assert frame.is_cuda and frame.device == packed.device, "packed and frame must be on one device"
             st = stream if stream is not None else torch.cuda.current_stream(packed.device).cuda_stream
-            check(lib.rt_unpack_bands(ctypes.c_void_p(packed.data_ptr()), ctypes.c_void_p(frame.data_ptr()), width, int(height),
-                                      int(band_rows), int(world), RT_OUT_DEVICE, ctypes.c_void_p(st)), "rt_unpack_bands")
+            check(lib.rt_unpack_bands(ctypes.c_void_p(packed.data_ptr()), pbytes, ctypes.c_void_p(frame.data_ptr()), fbytes, width,
+                                      int(height), int(band_rows), int(world), RT_OUT_DEVICE, ctypes.c_void_p(st)), "rt_unpack_bands")
             return frame
         packed, frame_np = packed.numpy(), frame.numpy()
     else:
         frame_np = frame
-    assert packed.flags.c_contiguous and frame_np.flags.c_contiguous
-    check(lib.rt_unpack_bands(packed.ctypes.data_as(ctypes.c_void_p), frame_np.ctypes.data_as(ctypes.c_void_p), width, int(height),
-                              int(band_rows), int(world), 0, None), "rt_unpack_bands")
+    assert packed.flags.c_contiguous and frame_np.flags.c_contiguous and packed.dtype == np.uint8 and frame_np.dtype == np.uint8
+    check(lib.rt_unpack_bands(packed.ctypes.data_as(ctypes.c_void_p), pbytes, frame_np.ctypes.data_as(ctypes.c_void_p), fbytes, width,
+                              int(height), int(band_rows), int(world), 0, None), "rt_unpack_bands")
     return frame
 
 
 def gather_frame(send, height, band_rows, group=None, dst=0, recv=None, frame=None):
     """Gathers every rank's padded block `send` ([block_rows, W, C]: its band rows first, as rendered in place by
     render_frame) to `dst` with one collective (RCCL on GPUs, gloo on CPU), then places the rows with rt_unpack_bands.
-    Returns the [H, W, C] frame on dst (None elsewhere)."""
+    Returns the [H, W, C] frame on dst (None elsewhere).  A `send` that is not exactly one padded block is refused on
+    every rank before the collective (the unpadded [rows_r, W, C] form of ABI 3 included)."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
+    block = block_rows(height, band_rows, world)
+    if send.dim() != 3 or send.shape[0] != block:
+        raise ValueError(f"send must be this rank's padded gather block of {block} rows (block_rows({height}, {band_rows}, {world})), "
+                         f"got shape {tuple(send.shape)}")
     if rank != dst:
         dist.gather(send, None, dst=dst, group=group)
         return None
     width, chans = send.shape[1], send.shape[2]
     if recv is None:
-        recv = torch.empty((world * send.shape[0], width, chans), dtype=send.dtype, device=send.device)
+        recv = torch.empty((world * block, width, chans), dtype=send.dtype, device=send.device)
+    if tuple(recv.shape) != (world * block, width, chans):
+        raise ValueError(f"recv must hold {world} blocks of {block} rows, got shape {tuple(recv.shape)}")
     dist.gather(send, list(recv.chunk(world)), dst=dst, group=group)  # views of one contiguous buffer
     if frame is None:
         frame = torch.empty((height, width, chans), dtype=send.dtype, device=send.device)
@@ -181,6 +196,12 @@ class multi_engine:
             check(lib.rt_multi_device_stats(self._m, k, ctypes.byref(st)), "rt_multi_device_stats")
             out.append(st.as_dict())
         return out
+
+    def times(self):
+        """rt_multi_times of the last run: renders (slowest / fastest device), gather, unpack, collectives issued."""
+        t = rt_multi_times()
+        check(lib.rt_multi_times_get(self._m, ctypes.byref(t)), "rt_multi_times_get")
+        return t.as_dict()
 
     def __del__(self):
         if getattr(self, "_m", None) and self._m.value and lib is not None:

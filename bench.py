@@ -29,6 +29,11 @@ Extra fields:
                 CPU-parallel mode (engine.h:335-376: 4 row stripes, 4 threads, shared global RNG) on a bounded sample
                 of the same workload (same scene, full 1920x1080, reduced spp), median and spread of 5 runs, N = 1 only;
                 plus `all_cores`: the oracle's restatement on every host thread the job may use (median of 5).
+  parity        the timed frame itself checked per pixel, after the timed steps: a bounded set of full-spp rows of the
+                last timed step's RGB8 against the oracle's CPU restatement driven by the same PCG streams (rmse_lsb,
+                max_dlsb, within_1lsb, bit_exact; SURVEY.md §8(d) tolerance: RMSE <= 1.0 LSB).
+  config.phases where the step time goes: rt_multi_times (renders slowest/fastest device, ncclGather, unpack) with the
+                one-process driver; per-rank render and step times under torchrun.
 """
 import argparse
 import glob
@@ -93,6 +98,7 @@ def parse():
     ap.add_argument("--wavefront", action="store_true", help="one fused extend launch per depth (A/B vs persistent paths)")
     ap.add_argument("--cpu-baseline-spp", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true", help="skip the oracle check of the timed frame's rows")
     return ap.parse_args()
 
 
@@ -151,6 +157,32 @@ def cpu_baseline(args, repeats=5):
     except Exception as e:  # the port is optional evidence: report, do not fail the bench
         res["all_cores"] = {"error": str(e)[-300:]}
     return res
+
+
+def frame_parity(args, frame, budget_segments=2.5e8):
+    """Per-pixel parity of the timed frame (the last timed step's RGB8 on GPU 0) against the oracle's CPU restatement
+    driven by the same PCG streams (oracle/restate.cpp pcg mode, orc_render_rows: full spp, the same rows), outside the
+    timed region: RMSE and largest difference in 8-bit levels (LSB) over a bounded set of rows spread over the frame,
+    plus the rows through its middle (SURVEY.md §8(d) tolerance 2: RMSE <= 1.0 LSB, >= 99.5 % of pixels within 1 LSB;
+    the f64 path is bit-exact).  Test infrastructure as the checker only: the frame was produced by libart alone."""
+    import numpy as np
+    try:
+        from tests.oracle_lib import oracle_render_rows
+    except Exception as e:  # the checker is optional evidence: report, do not fail the bench
+        return {"error": str(e)[-300:]}
+    W, H, spp = args.width, args.height, args.spp
+    n = int(max(2, min(16, budget_segments // max(1, W * spp * 3))))
+    rows = sorted(set([int(round(i * (H - 1) / max(1, n - 2))) for i in range(n - 1)] + [H // 2]))
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    nt = int(env) if env.isdigit() and int(env) > 0 else (os.cpu_count() or 1)
+    t0 = time.perf_counter()
+    o = oracle_render_rows(args.scene, W, H, spp, rows, seed=0, threads=nt, max_depth=args.max_depth)
+    got = frame[rows].astype(np.int64)
+    d = got - o["rgb"].astype(np.int64)
+    return {"rows": rows, "pixels": int(d.shape[0] * d.shape[1]), "spp": spp, "rmse_lsb": float(np.sqrt(np.mean(d.astype(np.float64) ** 2))),
+            "max_dlsb": int(np.abs(d).max()), "within_1lsb": float(np.mean(np.all(np.abs(d) <= 1, axis=-1))),
+            "bit_exact": bool(np.array_equal(got, o["rgb"])), "tolerance": "RMSE <= 1.0 LSB and >= 99.5 % of pixels within 1 LSB (SURVEY 8(d) 2)",
+            "oracle": f"oracle/restate.cpp pcg mode, orc_render_rows over {nt} threads ({o['segments']} segments, {time.perf_counter() - t0:.1f} s)"}
 
 
 def latest_pmc(precision, scene, variant, build):
@@ -269,7 +301,11 @@ def main():
 
         def step():
             eng.run(frame, profile=profile)
+            times.append(eng.times())
             return eng.stats, eng.device_stats()
+
+        def last_frame():
+            return frame
 
         def sync():
             for d in devices:
@@ -294,8 +330,15 @@ def main():
         fr = frame_renderer(eng, band_rows=args.band_rows, device=dev)
 
         def step():
-            _, st = fr(profile=profile)
+            t = time.perf_counter()
+            out, st = fr(profile=profile)
+            sync()
+            last["frame"] = out
+            times.append({"total_ms": (time.perf_counter() - t) * 1e3, "render_ms": st["ms"]})
             return st, [st]
+
+        def last_frame():
+            return last["frame"]
 
         def sync():
             torch.cuda.synchronize(dev)
@@ -305,8 +348,10 @@ def main():
         parallelism = (f"row-bands({args.band_rows}) over {n} GPUs, one process per GPU (torchrun): dist.gather over RCCL "
                        f"to rank 0 + rt_unpack_bands")
 
+    times, last = [], {}
     for _ in range(args.warmup):
         step()
+    del times[:]
     if driver == "procs":
         dist.barrier()
     sync()
@@ -332,11 +377,13 @@ def main():
     if driver == "procs":
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    phase = None
     scene_bytes = scene_bytes_now()  # uploaded by the first render
     if driver == "procs":
         # max wall time over ranks; all ranks' segments; every rank's per-device totals for the roofline
         mine = torch.tensor([elapsed, float(segs), float(primary_segs), float(variant), acc[0]["segments"], acc[0]["primary"],
-                             acc[0]["extend_ms"], acc[0]["extend_launches"], acc[0]["local_rows"], acc[0]["steps"]],
+                             acc[0]["extend_ms"], acc[0]["extend_launches"], acc[0]["local_rows"], acc[0]["steps"],
+                             sum(t["render_ms"] for t in times) / max(len(times), 1), sum(t["total_ms"] for t in times) / max(len(times), 1)],
                             dtype=torch.float64, device=dev)
         allr = [torch.empty_like(mine) for _ in range(n)]
         dist.all_gather(allr, mine)
@@ -347,6 +394,9 @@ def main():
         variant = int(max(r[3] for r in rows))
         acc = [{"segments": r[4], "primary": r[5], "extend_ms": r[6], "extend_launches": r[7], "local_rows": int(r[8]), "steps": int(r[9])}
                for r in rows]
+        phase = {"render_ms_per_rank": [round(r[10], 3) for r in rows], "step_ms_per_rank": [round(r[11], 3) for r in rows],
+                 "note": "per step, averaged over the timed steps: render = rt_render of the rank's bands (kernels + finalize); "
+                         "step = render + dist.gather over RCCL + rt_unpack_bands on rank 0"}
     if rank == 0:
         value = segs / elapsed / 1e6
         primary = args.width * args.height * args.spp * args.steps
@@ -363,10 +413,21 @@ def main():
         }
         if n > 1:
             line["config"]["per_gpu_kernel_ms_per_step"] = [round(a["extend_ms"] / max(a["steps"], 1), 3) for a in acc]
+        if driver == "multi" and times:
+            avg = lambda k: round(sum(t[k] for t in times) / len(times), 4)
+            phase = {k: avg(k) for k in ("total_ms", "render_ms_max", "render_ms_min", "gather_ms", "unpack_ms", "wait_ms")}
+            phase["slowest_device"] = times[-1]["slowest_device"]
+            phase["note"] = ("rt_multi_times per step, averaged over the timed steps: render = each device's host thread "
+                             "(kernels + finalize), gather = ncclGather on GPU 0's stream (HIP events), unpack = k_unpack_bands")
+        if phase:
+            line["config"]["phases"] = phase
         if profile and acc and any(a["extend_ms"] > 0 for a in acc):
             line["roofline"] = roofline_of(acc, args.width, scene_bytes, variant, args.precision, args.scene, build)
         if n == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args)
+        if not args.no_parity:
+            f = last_frame()
+            line["parity"] = frame_parity(args, f.cpu().numpy() if hasattr(f, "cpu") else f)
         print(json.dumps(line), flush=True)
     if driver == "procs":
         dist.destroy_process_group()

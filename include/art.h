@@ -46,8 +46,11 @@ extern "C" {
 /* ABI 2: rt_params.fp_mode 0 = RT_FP64 (the only arithmetic: the reference's IEEE double), rt_scene_info's f32 byte count
  * dropped, rt_multi_* (multi-GPU render over RCCL), rt_render_progressive, rt_scene_save / rt_scene_load, rt_image_load.
  * ABI 3 (additive): rt_band_block_rows, rt_unpack_bands (the gather layout for callers that move the bands themselves,
- * e.g. one process per GPU over torch.distributed), rt_multi_ngpus, rt_multi_scene_info, rt_multi_device_stats. */
-#define RT_ABI_VERSION 3
+ * e.g. one process per GPU over torch.distributed), rt_multi_ngpus, rt_multi_scene_info, rt_multi_device_stats.
+ * ABI 4: rt_unpack_bands takes the byte sizes of both buffers and refuses a mismatch with the layout; rt_multi_times
+ * (per-phase timing of the last rt_render_multi: renders, gather, unpack); rt_render_multi bounds its wait on the
+ * collective (RT_E_DEVICE on an RCCL error or timeout, after which the rt_multi refuses further renders). */
+#define RT_ABI_VERSION 4
 
 /* return codes */
 #define RT_OK 0
@@ -183,11 +186,12 @@ int rt_local_rows(const rt_params* params, int32_t* rows_out);
  * rt_band_block_rows(height, band_rows, n) rows (the largest set's row count; a shorter set pads after its rows).
  * rt_unpack_bands places the n concatenated blocks (packed: n * block_rows * width * 3 bytes, block r = set r's rows in
  * local order) into the height-row frame (row 0 = top): device pointers and a kernel on `stream` (hipStream_t, NULL =
- * default) with RT_OUT_DEVICE, else host memory.  Replaces the reference's in-place stripe writes into one frame
- * (engine.h:343-355). */
+ * default) with RT_OUT_DEVICE, else host memory.  packed_bytes / frame_bytes are the sizes of the two buffers: unless
+ * they are exactly n * block_rows * width * 3 and height * width * 3 the call is refused (RT_E_INVALID) before any byte
+ * moves.  Replaces the reference's in-place stripe writes into one frame (engine.h:343-355). */
 int rt_band_block_rows(int32_t height, int32_t band_rows, int32_t n);
-int rt_unpack_bands(const uint8_t* packed, uint8_t* frame, int32_t width, int32_t height, int32_t band_rows, int32_t n, int32_t flags,
-                    void* stream);
+int rt_unpack_bands(const uint8_t* packed, size_t packed_bytes, uint8_t* frame, size_t frame_bytes, int32_t width, int32_t height,
+                    int32_t band_rows, int32_t n, int32_t flags, void* stream);
 
 /* ---- images (imageio::load_image, imageio.cpp:11-15: stbi_load(path, &w, &h, &c, 0) of stb_image v2.27) ----
  * Decodes a JPEG (baseline or progressive) or PNG file to 8-bit samples, native channel count, row 0 = top, the bytes
@@ -206,7 +210,12 @@ void rt_image_free(uint8_t* pixels);
  * kernel writes the rows in image order.  out_rgb8: W*H*3 bytes, row 0 = top; host memory, or device memory on
  * devices[0] with RT_OUT_DEVICE.  The image is bit-identical to rt_render's for any device count (the RNG is keyed by
  * (seed, global pixel, sample)).  stats: segments/primary summed over the devices, ms = host wall time of the call.
- * Threading: one rt_multi per process at a time per device set; calls are blocking. */
+ * Threading: one rt_multi per process at a time per device set; calls are blocking.
+ * Failure behaviour: a device whose render fails makes the call return that error before any collective starts (the
+ * rt_multi stays usable).  The communicators are non-blocking (ncclConfig_t.blocking = 0); their creation and the
+ * gather are polled (ncclCommGetAsyncError, hipStreamQuery) against a deadline of ART_MULTI_TIMEOUT_MS milliseconds
+ * (environment, default 120000).  An RCCL error or an expired deadline aborts every communicator (ncclCommAbort) and
+ * returns RT_E_DEVICE; the rt_multi then refuses renders until it is destroyed and created again. */
 typedef struct rt_multi rt_multi;
 int rt_multi_create(const char* name, const char* asset_dir, const int* devices, int ngpus, rt_multi** out);
 int rt_multi_from_graph(rt_graph* g, const int* devices, int ngpus, rt_multi** out);
@@ -218,6 +227,21 @@ int rt_multi_scene_info(const rt_multi* m, rt_scene_info* info);
 /* Stats of devices[k] alone in the last rt_render_multi: its segments, primaries, rows and (RT_PROFILE) its own kernel
  * times and launches; ms = that device's render time (before the gather). */
 int rt_multi_device_stats(const rt_multi* m, int k, rt_stats* stats);
+/* Phases of the last rt_render_multi, so a scaling shortfall can be attributed: every device's render (host wall time of
+ * its thread: kernels + its own finalize), the gather (HIP events around the ncclGather on devices[0]'s stream) and the
+ * unpack (k_unpack_bands + the host copy when out_rgb8 is host memory). */
+typedef struct rt_multi_times {
+    double total_ms;            /* the whole call (== rt_stats.ms) */
+    double render_ms_max;       /* slowest device's render */
+    double render_ms_min;       /* fastest device's render */
+    double gather_ms;           /* ncclGather, as devices[0]'s stream sees it */
+    double unpack_ms;           /* unpack kernel (+ device-to-host copy) */
+    double wait_ms;             /* host time spent polling the gather */
+    uint64_t collectives;       /* gathers this rt_multi has issued so far (failed renders issue none) */
+    int32_t slowest_device;     /* index k (devices[k]) of render_ms_max */
+    int32_t ngpus;
+} rt_multi_times;
+int rt_multi_times_get(const rt_multi* m, rt_multi_times* out);
 
 /* ---- scene graph builder (one call per reference constructor; returns an id >= 0 or a negative code) ----
  * Scene-build randomness (noise textures' perlin tables, rt_graph_bvh's node draws) comes from the graph's own

@@ -27,7 +27,7 @@ def test_every_declared_symbol_is_exported_and_bound():
     exported = set(re.findall(r" T (rt_\w+)", nm))
     assert set(decl) <= exported, set(decl) - exported
     assert set(decl) == set(_lib.SIGNATURES), set(decl) ^ set(_lib.SIGNATURES)
-    assert _lib.lib.rt_abi_version() == _lib.RT_ABI_VERSION == 3
+    assert _lib.lib.rt_abi_version() == _lib.RT_ABI_VERSION == 4
 
 
 def test_struct_layouts_match_the_header(tmp_path):
@@ -147,6 +147,7 @@ def test_multi_entry_points_validate_without_a_gpu():
         assert _lib.lib.rt_multi_create(b"c1", b"assets", devs, 1, ctypes.byref(m)) == -3
         assert m.value is None
     assert _lib.lib.rt_render_multi(None, None, None, None, None) == -1
+    assert _lib.lib.rt_multi_times_get(None, None) == -1
 
 
 def torch_has_gpu():

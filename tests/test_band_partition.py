@@ -48,14 +48,34 @@ def test_unpack_rebuilds_the_frame(n):
 
 
 def test_1080p_over_8_gpus_is_balanced():
-    # 8-row bands split 1080 rows over 8 GPUs as 136 / 135 rows
+    # 8-row bands split 1080 rows (135 bands) over 8 GPUs as seven ranks of 136 rows and one of 128
     sizes = [len(band_rows_of(1080, 8, 8, r)) for r in range(8)]
-    assert max(sizes) - min(sizes) <= 8 and sum(sizes) == 1080
+    assert sizes == [136] * 7 + [128] and sum(sizes) == 1080
     assert block_rows(1080, 8, 8) == max(sizes) == 136
 
 
 def test_bad_arguments_are_refused():
     assert _lib.lib.rt_band_block_rows(0, 8, 2) == -1 and _lib.lib.rt_band_block_rows(10, 0, 2) < 0 and _lib.lib.rt_band_block_rows(10, 8, 0) < 0
     buf = (ctypes.c_uint8 * 12)()
-    assert _lib.lib.rt_unpack_bands(None, buf, 2, 2, 1, 1, 0, None) < 0
-    assert _lib.lib.rt_unpack_bands(buf, buf, 2, 2, 0, 1, 0, None) < 0
+    assert _lib.lib.rt_unpack_bands(None, 12, buf, 12, 2, 2, 1, 1, 0, None) < 0
+    assert _lib.lib.rt_unpack_bands(buf, 12, buf, 12, 2, 2, 0, 1, 0, None) < 0
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 8])
+def test_unpack_refuses_buffers_that_do_not_match_the_layout(n):
+    # rt_unpack_bands reads n * block_rows rows of `packed` and writes H rows of `frame`: a buffer of any other size is
+    # refused (RT_E_INVALID) before a byte moves, so a caller passing ABI 3's unpadded block cannot over-read
+    H, W, band_rows = 37, 5, 4
+    blk = block_rows(H, band_rows, n)
+    packed = np.zeros((n * blk, W, 3), np.uint8)
+    frame = np.zeros((H, W, 3), np.uint8)
+    pp, fp = packed.ctypes.data_as(ctypes.c_void_p), frame.ctypes.data_as(ctypes.c_void_p)
+    assert _lib.lib.rt_unpack_bands(pp, packed.nbytes, fp, frame.nbytes, W, H, band_rows, n, 0, None) == 0
+    for pb, fb in ((packed.nbytes - W * 3, frame.nbytes), (packed.nbytes + 1, frame.nbytes), (packed.nbytes, frame.nbytes - 3),
+                   (0, frame.nbytes)):
+        assert _lib.lib.rt_unpack_bands(pp, pb, fp, fb, W, H, band_rows, n, 0, None) == -1
+        assert b"bytes" in _lib.lib.rt_last_error()
+    with pytest.raises(ValueError, match="layout needs"):
+        unpack_bands(packed[: n * blk - 1], frame, H, band_rows, n)
+    with pytest.raises(ValueError, match="frame has shape"):
+        unpack_bands(packed, frame[:-1], H, band_rows, n)

@@ -33,6 +33,10 @@ def _worker(rank, world, port, q):
     send = torch.zeros((block_rows(H, BAND, world), W, 3), dtype=torch.uint8)  # the padded gather block
     if parts:
         send[: len(rows)] = torch.from_numpy(np.concatenate(parts))
+    # a block that is not exactly block_rows long (e.g. ABI 3's unpadded [rows_r, W, 3]) is refused on every rank before
+    # the collective, so no rank waits in a gather the others never join
+    with pytest.raises(ValueError, match="padded gather block"):
+        gather_frame(send[:-1], H, BAND)
     frame = gather_frame(send, H, BAND)
     if rank == 0:
         q.put(frame.numpy())

@@ -207,3 +207,65 @@ def test_loaded_scene_renders_bit_identically(gpu, name, tmp_path):
         e.run(img, accum=acc)
         frames.append((img, acc, e.stats["segments"]))
     assert np.array_equal(frames[0][0], frames[1][0]) and np.array_equal(frames[0][1], frames[1][1]) and frames[0][2] == frames[1][2]
+
+
+def _multi(scene="1", W=64, H=40, spp=4, band_rows=8):
+    from another_raytracer_amd.distributed import multi_engine
+    w = art.scene_manager().build(scene)
+    cam = art.camera(w.lookfrom, w.lookat, (0, 1, 0), w.vfov, W / H, w.aperture, 10.0, 0.0, 1.0)
+    return multi_engine(scene, [0], cam, W, H, spp, band_rows=band_rows, background=w.background)
+
+
+def test_render_multi_phase_times(gpu):
+    # rt_multi_times: the renders, the gather and the unpack of the last call, each timed, and the collectives counted
+    m = _multi()
+    img = torch.zeros((40, 64, 3), dtype=torch.uint8, device="cuda:0")
+    m.run(img)
+    t = m.times()
+    assert t["ngpus"] == 1 and t["collectives"] == 1 and t["slowest_device"] == 0
+    assert 0 < t["render_ms_min"] <= t["render_ms_max"] <= t["total_ms"]
+    assert t["gather_ms"] >= 0 and t["unpack_ms"] > 0 and t["wait_ms"] >= 0
+    assert t["render_ms_max"] + t["gather_ms"] + t["unpack_ms"] <= t["total_ms"] * 1.05 + 0.5
+    assert abs(t["total_ms"] - m.stats["ms"]) < 1e-9
+    m.run(img)
+    assert m.times()["collectives"] == 2
+
+
+def test_render_multi_failed_render_starts_no_collective(gpu, monkeypatch):
+    # a device whose render fails (fault injection: its workspace growth is refused) ends rt_render_multi with RT_E_DEVICE
+    # before the gather -- no collective starts -- and the multi renders correctly afterwards
+    m = _multi()
+    first = np.zeros((40, 64, 3), np.uint8)
+    m.run(first)
+    assert m.times()["collectives"] == 1
+    m.width, m.height = 256, 160  # a larger frame: the renderer's workspace must grow
+    monkeypatch.setenv("ART_FAULT_WORKSPACE_BYTES", "1024")
+    with pytest.raises(art.RTError) as err:
+        m.run(np.zeros((160, 256, 3), np.uint8))
+    assert err.value.code == -3 and "ART_FAULT_WORKSPACE_BYTES" in str(err.value)
+    assert m.times()["collectives"] == 1
+    monkeypatch.delenv("ART_FAULT_WORKSPACE_BYTES")
+    m.width, m.height = 64, 40
+    again = np.zeros((40, 64, 3), np.uint8)
+    m.run(again)
+    assert np.array_equal(again, first) and m.times()["collectives"] == 2
+
+
+def test_render_multi_gather_failure_aborts_and_is_reported(gpu, monkeypatch):
+    # a collective that fails in flight (fault injection after ncclGroupEnd, as a peer error or an expired
+    # ART_MULTI_TIMEOUT_MS deadline would) aborts the communicators and returns RT_E_DEVICE; that rt_multi then refuses
+    # to render, and a new one works
+    m = _multi()
+    ref = np.zeros((40, 64, 3), np.uint8)
+    m.run(ref)
+    monkeypatch.setenv("ART_FAULT_GATHER_ABORT", "1")
+    with pytest.raises(art.RTError) as err:
+        m.run(np.zeros((40, 64, 3), np.uint8))
+    assert err.value.code == -3 and "injected" in str(err.value)
+    monkeypatch.delenv("ART_FAULT_GATHER_ABORT")
+    with pytest.raises(art.RTError, match="unusable"):
+        m.run(np.zeros((40, 64, 3), np.uint8))
+    del m
+    fresh = np.zeros((40, 64, 3), np.uint8)
+    _multi().run(fresh)
+    assert np.array_equal(fresh, ref)

@@ -10,7 +10,7 @@ if [ -z "$NOTESTS" ]; then
 fi
 for round in 1 2; do
 for lib in $LIBS; do
-  timeout -k 10 300 env ART_LIB=$PWD/another_raytracer_amd/$lib python bench.py --steps 2 --warmup 1 --no-cpu-baseline $ARGS > gpurun_out/ab_${lib}_$round.log 2>&1
+  timeout -k 10 300 env ART_LIB=$PWD/another_raytracer_amd/$lib python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-parity $ARGS > gpurun_out/ab_${lib}_$round.log 2>&1
   rc=$?; echo "$lib round $round rc=$rc $(grep -o '"value": [0-9.]*' gpurun_out/ab_${lib}_$round.log | head -1) $(grep -o '"extend_ms_total": [0-9.]*' gpurun_out/ab_${lib}_$round.log) $(grep -o "\"extend_variant\": [0-9]*" gpurun_out/ab_${lib}_$round.log) $(grep -o "\"segments_per_step\": [0-9]*" gpurun_out/ab_${lib}_$round.log)"
   [ $rc -eq 0 ] || { tail -5 gpurun_out/ab_${lib}_$round.log; exit $rc; }
 done
