@@ -1,6 +1,7 @@
 #!/bin/bash
 # One GPU-box session made of steps, each under its own time limit, stopping at the first failure:
 #   tests                       pytest -m gpu (tests/, one process)
+#   testk:EXPR                  pytest -m gpu -k EXPR (a subset first, under a shorter limit)
 #   calib                       tools/valu_calib (VALU issue-cost calibration, plain run)
 #   uvcheck                     tools/uv_check (device vs glibc get_sphere_uv texel choice) -> gpurun_out/uv_check.json
 #   ab:LIB1,LIB2[:ARGS]         tools/ab_quick.sh over in-tree libart builds (bench.py ARGS, default --spp 256)
@@ -27,6 +28,9 @@ for step in "$@"; do
     tests)
       run 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
       tail -1 gpurun_out/gpu_tests.log ;;
+    testk)
+      run 200 python -u -m pytest tests -m gpu -x -v --timeout 60 --timeout-method thread -k "$a" > gpurun_out/gpu_testk.log 2>&1
+      tail -1 gpurun_out/gpu_testk.log ;;
     calib)
       run 120 ./tools/valu_calib > gpurun_out/valu_calib.jsonl 2>&1
       cat gpurun_out/valu_calib.jsonl ;;
