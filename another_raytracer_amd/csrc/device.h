@@ -48,28 +48,7 @@ template <class R> __device__ __forceinline__ R len2(V3<R> v) { return v.x * v.x
 template <class R> __device__ __forceinline__ V3<R> cross(V3<R> u, V3<R> v) {
     return {u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x};
 }
-// 1 / x correctly rounded, as the compiler's f64 division expansion computes it when no operand needs scaling
-// (v_div_scale returns its inputs, v_div_fmas is a plain fma and v_div_fixup passes its input through for
-// 2^-1000 < x < 2^1000): hardware rcp, two Newton steps, the residual fma and the final fma -- the same operations on
-// the same values, without the scale, fmas and fixup instructions.  Other x (0, inf, NaN, extreme exponents) take
-// the division.
-#ifndef ART_RCP_RN
-#define ART_RCP_RN 0  // measured: k_paths -1.1 %, the Next-Week final +0.4 % (GPU parity exact either way)
-#endif
-__device__ __forceinline__ double rcp_rn(double x) {
-#if ART_RCP_RN
-    const double ax = __builtin_fabs(x);
-    if (!(ax > 0x1p-1000 && ax < 0x1p1000)) return 1.0 / x;
-    double r = __builtin_amdgcn_rcp(x);
-    r = fma(fma(-x, r, 1.0), r, r);
-    r = fma(fma(-x, r, 1.0), r, r);
-    return fma(fma(-x, r, 1.0), r, r);
-#else
-    return 1.0 / x;
-#endif
-}
-__device__ __forceinline__ float rcp_rn(float x) { return 1.0f / x; }
-template <class R> __device__ __forceinline__ V3<R> divs(V3<R> v, R t) { return rcp_rn(t) * v; }  // vec3.h:97-99: (1/t) * v
+template <class R> __device__ __forceinline__ V3<R> divs(V3<R> v, R t) { return (R(1) / t) * v; }  // vec3.h:97-99: (1/t) * v
 template <class R> __device__ __forceinline__ V3<R> unit(V3<R> v) { return divs(v, sqrt_rn(len2(v))); }
 template <class R> __device__ __forceinline__ bool near_zero(V3<R> v) {  // vec3.h:49-53
     const R s = R(1e-8);
@@ -251,7 +230,6 @@ struct DevScene {
     const TriRec112<R>* leaf_tris112;  // the same with each triangle's plane (n, dd), for the LM 1 kernels' LDS copy
     const PrimRec80* leaf_prims;  // leaf_prims[slot]: the record of primrefs[slot] of any type (triangle-free kernels)
     const PrimRec80* obj_prims;  // obj_prims[o] = the record of prim object o's primitive (indexed like objs)
-    const ObjBox* obj_box;       // obj_box[o]: world-space cull box of instance o (indexed like objs)
     const uint8_t* lds_image;   // layout.h LDS scene image (nullptr unless the scene qualifies)
     uint32_t n_nodes, n_primrefs, n_tris, n_objs;  // array lengths (k_paths_g's LDS copies)
     uint32_t nodes_lds;         // k_paths_g LM 2: LDS byte address of the copy of nodes [0, n_lds_nodes) (top levels)
@@ -397,54 +375,15 @@ __device__ __forceinline__ void box_face(const BoxRec<R>& b, int f, int& axis, R
     else if (pair == 1) { a0 = b.mn[0]; a1 = b.mx[0]; b0 = b.mn[2]; b1 = b.mx[2]; k = hi ? b.mx[1] : b.mn[1]; }
     else { a0 = b.mn[1]; a1 = b.mx[1]; b0 = b.mn[2]; b1 = b.mx[2]; k = hi ? b.mx[0] : b.mn[0]; }
 }
-// ART_BOX_RCP: a box's six plane distances (k - o) / d take one reciprocal per axis (two faces share it) and
-// div_rcp (Markstein: the division's bits for a normal divisor away from the extremes).  A component outside
-// [2^-500, 2^500] in magnitude -- in particular the +-0 of an axis-parallel ray, whose division gives +-inf or, for
-// k == o, the NaN the reference also carries (aarect.cpp) -- keeps the true division.
-// Measured (r3j, A/B with ART_MEDIUM_RCP on the same build): the two reciprocal variants together cost cow 1.9 % and
-// the Next-Week final 0.3 % (the guarded reciprocal's extra compare/select and registers outweigh the divisions): off.
-#ifndef ART_BOX_RCP
-#define ART_BOX_RCP 0
-#endif
-template <class R>
-__device__ __forceinline__ bool hit_rect_inv(int axis, R a0, R a1, R b0, R b1, R k, const Ray<R>& r, R inv, bool use_inv, R tmin, R tmax, R& t) {
-    const int ka = axis == 0 ? 2 : (axis == 1 ? 1 : 0);
-    const int ia = axis == 2 ? 1 : 0;
-    const int ib = axis == 0 ? 1 : 2;
-    const R num = k - comp(r.o, ka), den = comp(r.d, ka);
-    const R tt = use_inv ? div_rcp(num, den, inv) : num / den;
-    if (tt < tmin || tt > tmax) return false;
-    const R x = comp(r.o, ia) + tt * comp(r.d, ia);
-    const R y = comp(r.o, ib) + tt * comp(r.d, ib);
-    if (x < a0 || x > a1 || y < b0 || y > b1) return false;
-    t = tt;
-    return true;
-}
 template <class R>
 __device__ __forceinline__ bool hit_box(const BoxRec<R>& b, const Ray<R>& r, R tmin, R tmax, R& t, uint32_t& face) {
     bool any = false;  // hittable_list semantics over the six sides: closest wins, a later equal t replaces
     R closest = tmax;
-#if ART_BOX_RCP
-    // face pair p (0: xy, k on z; 1: xz, k on y; 2: yz, k on x) divides by d.z, d.y, d.x
-    R inv[3];
-    bool ok[3];
-#pragma unroll
-    for (int p = 0; p < 3; ++p) {
-        const R den = comp(r.d, p == 0 ? 2 : (p == 1 ? 1 : 0));
-        const R mag = __builtin_fabs(den);
-        ok[p] = mag > R(0x1p-500) && mag < R(0x1p500);
-        inv[p] = R(1) / (ok[p] ? den : R(1));
-    }
-#endif
     for (int f = 0; f < 6; ++f) {
         int axis;
         R a0, a1, b0, b1, k, tt;
         box_face(b, f, axis, a0, a1, b0, b1, k);
-#if ART_BOX_RCP
-        const bool h = hit_rect_inv(axis, a0, a1, b0, b1, k, r, inv[axis], ok[axis], tmin, closest, tt);
-#else
         const bool h = hit_rect(axis, a0, a1, b0, b1, k, r, tmin, closest, tt);
-#endif
         if (h) {
             any = true;
             closest = tt;
@@ -501,19 +440,11 @@ __device__ __forceinline__ float f_hi(float t) { return t * (1.0f + 2e-6f) + 1e-
 // distances are single-rounding FMAs fma(plane, 1/d, -o/d), two children per v_pk_fma_f32; one rounding is no worse
 // than the mul+sub the box padding was sized for, so the test stays conservative.
 typedef float f2v __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ float slab_key(float x0, float x1, float y0, float y1, float z0, float z1, int32_t child, float tminf, float tmaxf) {
-    const float lo = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), tminf));
-    const float hi = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), tmaxf));
-    return (lo <= hi && child != kNodeEmpty) ? lo : __builtin_inff();
-}
-// ART_NEAR_FAR_G: the HBM-scene traversal loads each axis' near and far planes by the direction's sign (as the LDS
+// The HBM-scene traversal loads each axis' near and far planes by the direction's sign (as the LDS
 // variant does), so a child's entry is max(x0, y0, z0, tmin) and its exit min(x1, y1, z1, tmax) without the per-axis
 // min/max.  For 1/d > 0, t(lo) <= t(hi) (the FMA rounding is monotone in the plane), so the selected planes give
 // exactly the values the min/max picked (and an empty slot's +-FLT_MAX box stays missed): same keys, 24 fewer VALU per
 // node visit.  Measured (r3c): cow +3.6 %, Next-Week final +5.6 %, dino 4096^2 +3.9 %.
-#ifndef ART_NEAR_FAR_G
-#define ART_NEAR_FAR_G 1
-#endif
 __device__ __forceinline__ float slab_key_nf(float x0, float x1, float y0, float y1, float z0, float z1, float tminf, float tmaxf) {
     const float lo = fmaxf(fmaxf(x0, y0), fmaxf(z0, tminf));
     const float hi = fminf(fminf(x1, y1), fminf(z1, tmaxf));
@@ -536,22 +467,6 @@ __device__ __forceinline__ void slab4_nf(const float4& lx, const float4& hx, con
     k2 = slab_key_nf(x0b.x, x1b.x, y0b.x, y1b.x, z0b.x, z1b.x, tminf, tmaxf);
     k3 = slab_key_nf(x0b.y, x1b.y, y0b.y, y1b.y, z0b.y, z1b.y, tminf, tmaxf);
 }
-__device__ __forceinline__ void slab4(const float4& lx, const float4& hx, const float4& ly, const float4& hy, const float4& lz, const float4& hz,
-                                      const int4& ch, float ix, float iy, float iz, float oix, float oiy, float oiz, float tminf, float tmaxf,
-                                      float& k0, float& k1, float& k2, float& k3) {
-    const f2v vx = {ix, ix}, vy = {iy, iy}, vz = {iz, iz};
-    const f2v nx = {-oix, -oix}, ny = {-oiy, -oiy}, nz = {-oiz, -oiz};
-    const f2v x0a = __builtin_elementwise_fma(f2v{lx.x, lx.y}, vx, nx), x0b = __builtin_elementwise_fma(f2v{lx.z, lx.w}, vx, nx);
-    const f2v x1a = __builtin_elementwise_fma(f2v{hx.x, hx.y}, vx, nx), x1b = __builtin_elementwise_fma(f2v{hx.z, hx.w}, vx, nx);
-    const f2v y0a = __builtin_elementwise_fma(f2v{ly.x, ly.y}, vy, ny), y0b = __builtin_elementwise_fma(f2v{ly.z, ly.w}, vy, ny);
-    const f2v y1a = __builtin_elementwise_fma(f2v{hy.x, hy.y}, vy, ny), y1b = __builtin_elementwise_fma(f2v{hy.z, hy.w}, vy, ny);
-    const f2v z0a = __builtin_elementwise_fma(f2v{lz.x, lz.y}, vz, nz), z0b = __builtin_elementwise_fma(f2v{lz.z, lz.w}, vz, nz);
-    const f2v z1a = __builtin_elementwise_fma(f2v{hz.x, hz.y}, vz, nz), z1b = __builtin_elementwise_fma(f2v{hz.z, hz.w}, vz, nz);
-    k0 = slab_key(x0a.x, x1a.x, y0a.x, y1a.x, z0a.x, z1a.x, ch.x, tminf, tmaxf);
-    k1 = slab_key(x0a.y, x1a.y, y0a.y, y1a.y, z0a.y, z1a.y, ch.y, tminf, tmaxf);
-    k2 = slab_key(x0b.x, x1b.x, y0b.x, y1b.x, z0b.x, z1b.x, ch.z, tminf, tmaxf);
-    k3 = slab_key(x0b.y, x1b.y, y0b.y, y1b.y, z0b.y, z1b.y, ch.w, tminf, tmaxf);
-}
 // Packed keys of the LDS variant: the entry distance's f32 bits with the low 16 bits replaced by the 16-bit child
 // code.  Entry distances are >= tminf > 0 there (world rays start at t = 0.001; the LDS variant has no media, whose
 // boundary tests start at -inf), so unsigned order is distance order to 2^-7 relative -- it only orders the pushes;
@@ -568,36 +483,26 @@ __device__ __forceinline__ uint32_t slab_key_packed(float x0, float x1, float y0
     float zt;
     __asm__("v_min_f32 %0, %1, %2" : "=v"(zt) : "v"(z1), "v"(tmaxf));
     const float hi = fminf(fminf(x1, y1), zt);
-    // HI: the code is the high half of `child` (ART_CHILD16): bytes 3, 2 of lo over bytes 3, 2 of child, one v_perm
+    // HI: the code is the high half of `child` (layout.h: child codes as int16): bytes 3, 2 of lo over bytes 3, 2 of child, one v_perm
     const uint32_t key = HI ? __builtin_amdgcn_perm(__float_as_uint(lo), static_cast<uint32_t>(child), 0x07060302u)
                             : (__float_as_uint(lo) & 0xFFFF0000u) | (static_cast<uint32_t>(child) & 0xFFFFu);
     return lo <= hi ? key : kKeyMiss;  // empty slots carry a box no ray enters (layout.h kLdsEmptyChild)
 }
-// dly / dhy: the y motion planes (near, far), tiy = tm * iy: the y plane distances are those of the boxes at the ray's
-// time, (plane0 + tm * dplane) * iy - oy * iy, as two single-rounding FMAs (the box padding covers the extra rounding)
-template <bool MOT>
 __device__ __forceinline__ void slab4_packed(const float4& lx, const float4& hx, const float4& ly, const float4& hy, const float4& lz,
-                                             const float4& hz, const float4& dly, const float4& dhy, const int4& ch, float ix, float iy,
-                                             float iz, float tiy, float oix, float oiy, float oiz, float tminf, float tmaxf, uint32_t& q0,
-                                             uint32_t& q1, uint32_t& q2, uint32_t& q3) {
-    const f2v vx = {ix, ix}, vy = {iy, iy}, vz = {iz, iz}, vty = {tiy, tiy};
+                                             const float4& hz, const int4& ch, float ix, float iy, float iz, float oix, float oiy, float oiz,
+                                             float tminf, float tmaxf, uint32_t& q0, uint32_t& q1, uint32_t& q2, uint32_t& q3) {
+    const f2v vx = {ix, ix}, vy = {iy, iy}, vz = {iz, iz};
     const f2v nx = {-oix, -oix}, ny = {-oiy, -oiy}, nz = {-oiz, -oiz};
     const f2v x0a = __builtin_elementwise_fma(f2v{lx.x, lx.y}, vx, nx), x0b = __builtin_elementwise_fma(f2v{lx.z, lx.w}, vx, nx);
     const f2v x1a = __builtin_elementwise_fma(f2v{hx.x, hx.y}, vx, nx), x1b = __builtin_elementwise_fma(f2v{hx.z, hx.w}, vx, nx);
-    f2v y0a = __builtin_elementwise_fma(f2v{ly.x, ly.y}, vy, ny), y0b = __builtin_elementwise_fma(f2v{ly.z, ly.w}, vy, ny);
-    f2v y1a = __builtin_elementwise_fma(f2v{hy.x, hy.y}, vy, ny), y1b = __builtin_elementwise_fma(f2v{hy.z, hy.w}, vy, ny);
-    if constexpr (MOT) {
-        y0a = __builtin_elementwise_fma(f2v{dly.x, dly.y}, vty, y0a);
-        y0b = __builtin_elementwise_fma(f2v{dly.z, dly.w}, vty, y0b);
-        y1a = __builtin_elementwise_fma(f2v{dhy.x, dhy.y}, vty, y1a);
-        y1b = __builtin_elementwise_fma(f2v{dhy.z, dhy.w}, vty, y1b);
-    }
+    const f2v y0a = __builtin_elementwise_fma(f2v{ly.x, ly.y}, vy, ny), y0b = __builtin_elementwise_fma(f2v{ly.z, ly.w}, vy, ny);
+    const f2v y1a = __builtin_elementwise_fma(f2v{hy.x, hy.y}, vy, ny), y1b = __builtin_elementwise_fma(f2v{hy.z, hy.w}, vy, ny);
     const f2v z0a = __builtin_elementwise_fma(f2v{lz.x, lz.y}, vz, nz), z0b = __builtin_elementwise_fma(f2v{lz.z, lz.w}, vz, nz);
     const f2v z1a = __builtin_elementwise_fma(f2v{hz.x, hz.y}, vz, nz), z1b = __builtin_elementwise_fma(f2v{hz.z, hz.w}, vz, nz);
     q0 = slab_key_packed(x0a.x, x1a.x, y0a.x, y1a.x, z0a.x, z1a.x, ch.x, tminf, tmaxf);
-    q1 = slab_key_packed<ART_CHILD16 != 0>(x0a.y, x1a.y, y0a.y, y1a.y, z0a.y, z1a.y, ch.y, tminf, tmaxf);
+    q1 = slab_key_packed<true>(x0a.y, x1a.y, y0a.y, y1a.y, z0a.y, z1a.y, ch.y, tminf, tmaxf);
     q2 = slab_key_packed(x0b.x, x1b.x, y0b.x, y1b.x, z0b.x, z1b.x, ch.z, tminf, tmaxf);
-    q3 = slab_key_packed<ART_CHILD16 != 0>(x0b.y, x1b.y, y0b.y, y1b.y, z0b.y, z1b.y, ch.w, tminf, tmaxf);
+    q3 = slab_key_packed<true>(x0b.y, x1b.y, y0b.y, y1b.y, z0b.y, z1b.y, ch.w, tminf, tmaxf);
 }
 // The HBM-scene traversal's packed keys (PK): near/far planes as slab4_nf, keys as slab_key_packed (the 16-bit codes of
 // children 1 and 3 in the high halves of ch.y / ch.w, as the LDS image's)
@@ -658,15 +563,8 @@ __device__ __forceinline__ bool hit_lds_slot(const uint8_t* lds, uint32_t slot, 
     const uint32_t code = lds_u1(kLdsOffRef + slot * 4u);
 #endif
     V3<double> center{a.x, a.y, b.x};
-#if ART_LDS_DY_SLOT
     // y motion only (lds_scene_image): c + tm * (+-0, dy, +-0) leaves x and z as they are; static slots hold dy = -0
     center.y = center.y + r.tm * lds_d1(kLdsOffMov + slot * 8u);
-#else
-    const uint32_t mv = (code >> kLdsRefMovShift) & ((1u << (kLdsRefMatShift - kLdsRefMovShift)) - 1);
-    if (mv) {  // y motion only (lds_scene_image): c + tm * (+0, dy, +0) leaves x and z exactly as they are
-        center.y = center.y + r.tm * lds_d1(kLdsOffMov + (mv - 1u) * 8u);
-    }
-#endif
 #if !ART_LDS_LEAF_NOREF
     prim = make_primref(PRIM_SPHERE, code & kLdsRefIndexMask);
     mt = code >> kLdsRefMatShift;
@@ -691,61 +589,6 @@ __device__ __forceinline__ void stat_lane(int k) { atomicAdd(&g_art_stats[k], 1u
 #define ART_STAT_LANE(k)
 #endif
 
-#ifndef ART_SPECULATIVE
-#define ART_SPECULATIVE 1
-#endif
-#ifndef ART_PARK_BRANCHLESS
-// LDS variant, node loop: parking reads the two top stack entries up front (no dependent read in a branch): -1.2 %
-#define ART_PARK_BRANCHLESS 0
-#endif
-#ifndef ART_PUSH_MASKED
-#define ART_PUSH_MASKED 0  // 1: store only kept stack entries (exec-masked ds_write): -0.9 %
-#endif
-#ifndef ART_PARK_PREFETCH
-#define ART_PARK_PREFETCH 0  // 1: the node loop reads the entry under the stack top with the top (-1.4 %)
-#endif
-#ifndef ART_SORT_PARTIAL
-#define ART_SORT_PARTIAL 0  // LDS variant: 4-key sorting network without its last exchange (2 fewer VALU per visit)
-#endif
-#ifndef ART_LEAFSEL_BRANCHLESS
-#define ART_LEAFSEL_BRANCHLESS 1  // LDS variant, leaf-phase entry: one stack read up front, selects instead of branches
-#endif
-#ifndef ART_LEAFSEL_BRANCHLESS_G
-#define ART_LEAFSEL_BRANCHLESS_G 1  // the same in the HBM-scene variant
-#endif
-#ifndef ART_POP_GUARD_G
-#define ART_POP_GUARD_G 0  // 1: HBM-scene variant stack pops keep the empty-stack guard
-#endif
-#ifndef ART_OBJ_PRIMS
-#define ART_OBJ_PRIMS 1  // prim objects test the per-object primitive copy (DevScene::obj_prims)
-#endif
-#ifndef ART_LEAF_TRIS
-#define ART_LEAF_TRIS 1  // triangle leaves read the leaf-ordered copy (DevScene::leaf_tris)
-#endif
-#ifndef ART_LEAF_PRIMS_G
-#define ART_LEAF_PRIMS_G 1  // triangle-free HBM-scene kernels read leaf records from the leaf-ordered copy
-#endif
-#ifndef ART_NF_XOR
-// HBM-scene traversal: a node's near plane at base + sign * 16 and the far plane at (that) ^ 16, the axis offsets as
-// immediates (node arrays 128-aligned): 10 address VALU per visit instead of 15
-#define ART_NF_XOR 1
-#endif
-#ifndef ART_LM2_COMPACT
-#define ART_LM2_COMPACT 0
-#endif
-constexpr uint32_t kLdsCompactNode = 112;  // LM 2 LDS node: 6 planes (96 B) + 16-bit codes (8 B) + 8 B pad
-#ifndef ART_SPH_PRE_G
-#define ART_SPH_PRE_G 1  // r3w: Next-Week final +1.4 %, Cornell smoke +-0
-#endif
-#ifndef ART_TRI112
-#define ART_TRI112 1  // LM 1 (PL 2) kernels test leaf triangles from TriRec112 records (plane precomputed)
-#endif
-#ifndef ART_NF_HOIST
-#define ART_NF_HOIST 1  // r3t: dino +0.8 % (its LM 1 kernel has the registers)
-#endif
-#ifndef ART_LEAF2_G
-#define ART_LEAF2_G 1  // the HBM-scene traversal also tests a lane's two pending leaves in one leaf phase
-#endif
 
 // The LDS scene image lives at LDS address 0 (k_extend and k_paths allocate LDS dynamically only), so node fetches
 // take a plain 32-bit LDS byte address: no base add per load.
@@ -774,12 +617,7 @@ struct LaneStack<B, true> {  // LDS-scene variant: 16-bit entries, tracked as th
     __device__ __forceinline__ explicit LaneStack(int16_t* stk)
         : bottom(static_cast<uint32_t>(reinterpret_cast<size_t>((__attribute__((address_space(3))) int16_t*)stk)) - kRow), top(bottom) {}
     __device__ __forceinline__ void push(int32_t v, bool keep) {
-#if ART_PUSH_MASKED
-        // the store of a kept entry only (an exec-masked ds_write; skipped by the wave when no lane keeps one)
-        if (keep) *(__attribute__((address_space(3))) int16_t*)(size_t)(top + kRow) = static_cast<int16_t>(v);
-#else
         *(__attribute__((address_space(3))) int16_t*)(size_t)(top + kRow) = static_cast<int16_t>(v);
-#endif
         top += keep ? kRow : 0u;
     }
     __device__ __forceinline__ int32_t peek() const { return *(__attribute__((address_space(3))) const int16_t*)(size_t)top; }
@@ -793,12 +631,6 @@ struct LaneStack<B, true> {  // LDS-scene variant: 16-bit entries, tracked as th
     __device__ __forceinline__ uint32_t save() const { return top; }
     __device__ __forceinline__ void restore(uint32_t t) { top = t; }
 };
-#ifndef ART_STACK_ADDR_G
-// 32-bit stacks tracked by the LDS byte address of their top entry, as LaneStack<B, true> (a push or pop is one
-// select + add instead of a 64-bit multiply-add of the depth for every access); 0: tracked by depth
-#define ART_STACK_ADDR_G 1
-#endif
-#if ART_STACK_ADDR_G
 template <int B>
 struct LaneStack<B, false> {  // 32-bit entries; `top` is the LDS byte address of the top entry (the sentinel when empty)
     static constexpr uint32_t kRow = 4u * B;
@@ -810,44 +642,16 @@ struct LaneStack<B, false> {  // 32-bit entries; `top` is the LDS byte address o
         top += keep ? kRow : 0u;
     }
     __device__ __forceinline__ int32_t peek() const { return *(__attribute__((address_space(3))) const int32_t*)(size_t)top; }
-#if ART_POP_GUARD_G
-    __device__ __forceinline__ void pop_if(bool c) { top -= (c && top != bottom) ? kRow : 0u; }
-#else
     // no empty-stack guard: a walk that pops the sentinel's kNodeEmpty ends without reading on
     __device__ __forceinline__ void pop_if(bool c) { top -= c ? kRow : 0u; }
-#endif
     // the resumable traversal (TravResume) keeps the top address: the stack stays in this lane's LDS column
     __device__ __forceinline__ uint32_t save() const { return top; }
     __device__ __forceinline__ void restore(uint32_t t) { top = t; }
 };
-#else
-template <int B>
-struct LaneStack<B, false> {  // 32-bit entries
-    int32_t* stk;
-    int sp = 0;
-    __device__ __forceinline__ explicit LaneStack(int32_t* s) : stk(s) {}
-    __device__ __forceinline__ void push(int32_t v, bool keep) {
-        stk[sp * B] = v;
-        sp += keep;
-    }
-    __device__ __forceinline__ int32_t peek() const { return stk[(sp - 1) * B]; }
-#if ART_POP_GUARD_G
-    __device__ __forceinline__ void pop_if(bool c) { sp -= (c && sp > 0) ? 1 : 0; }
-#else
-    // no empty-stack guard, as LaneStack<B, true>: a walk that pops the sentinel's kNodeEmpty ends without reading on
-    __device__ __forceinline__ void pop_if(bool c) { sp -= c ? 1 : 0; }
-#endif
-    __device__ __forceinline__ uint32_t save() const { return static_cast<uint32_t>(sp); }
-    __device__ __forceinline__ void restore(uint32_t t) { sp = static_cast<int>(t); }
-};
-#endif
 // Traversal stack entry: node/leaf codes, 16 bits in the LDS-scene variant (layout.h lds_leaf), 32 bits otherwise.
 template <bool L> using StackT = typename std::conditional<L, int16_t, int32_t>::type;
 // k_paths_g instantiations with F_CODE16 keep 16-bit entries as well (the LDS variant's LaneStack and stack columns)
 template <bool L, uint32_t F> using StackF = StackT<L || (F & F_CODE16) != 0>;
-#ifndef ART_STACK_SWZ
-#define ART_STACK_SWZ 1
-#endif
 // Column of lane t in a stack row.  16-bit entries pack two lanes per dword; a row holds a wave's 64 entries in 32
 // dwords.  Unswizzled, lanes 2i and 2i+1 share dword i, so a wave64 LDS access (serviced as lanes 0-31, then 32-63)
 // puts two lanes on one bank whenever their stack depths differ (a 2-way conflict on most pushes and pops of a
@@ -855,13 +659,10 @@ template <bool L, uint32_t F> using StackF = StackT<L || (F & F_CODE16) != 0>;
 // so do lanes 32-63, in every row (rows are 2 KiB = 512 dwords apart, a multiple of the 64 banks).
 template <bool L>
 __device__ __forceinline__ uint32_t stack_column(uint32_t t) {
-    if (!L || !ART_STACK_SWZ) return t;
+    if (!L) return t;
     return (t & ~63u) | ((t & 31u) << 1) | ((t >> 5) & 1u);
 }
 
-#ifndef ART_RCP_CLAMP
-#define ART_RCP_CLAMP 1
-#endif
 // f32 direction component for the slab reciprocals: magnitude at least 2^-64, sign of d (-0 stays negative).
 __device__ __forceinline__ float f32_dir(double d) {
     const float f = static_cast<float>(d);
@@ -876,7 +677,7 @@ __device__ __forceinline__ float f32_dir(double d) {
 #endif
 struct TravResume {
     int32_t node, parked;
-    uint32_t sp;  // LaneStack::save(): the top entry's LDS address (ART_STACK_ADDR_G) or the depth
+    uint32_t sp;  // LaneStack::save(): the top entry's LDS address
     int32_t lanes;  // suspend when fewer lanes of the wave are traversing
     bool fresh;     // no traversal in progress: start at the root
     bool allow;     // wave-uniform: suspending is allowed in this round (paths remain to be started)
@@ -889,22 +690,15 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                                          StackF<L, F>* stk, R& t, uint32_t& prim, uint32_t& face, uint32_t& mt, TravResume* rs = nullptr,
                                          int32_t hoisted = kNodeEmpty) {
     static_assert(!(L && (F & F_MEDIA)), "packed LDS keys need tmin > 0: no medium boundary tests in the LDS variant");
-    static_assert(!RES || (!L && ART_SPECULATIVE), "resumable traversal: HBM-scene speculative variant only");
+    static_assert(!RES || !L, "resumable traversal: HBM-scene variant only");
     const float ox = static_cast<float>(r.o.x), oy = static_cast<float>(r.o.y), oz = static_cast<float>(r.o.z);
     // hardware reciprocal (1 ulp): the box test is conservative by its 2e-6 relative padding, far above that
-#if ART_RCP_CLAMP
     // A direction component that is 0 (or tiny) would give 1/d = inf, and the plane distances fma(plane, 1/d, -o/d)
     // would mix +-inf and NaN (inf - inf): a ray parallel to an axis then missed boxes that hold it (tests/
     // test_gpu_rays.py).  The component is raised to +-2^-64 with its sign, so 1/d, o/d and plane/d stay finite for
     // any coordinate below 1e19 and the slab of a parallel ray holds its origin for t in (-huge, +huge) or for none.
     const float ix = __builtin_amdgcn_rcpf(f32_dir(r.d.x)), iy = __builtin_amdgcn_rcpf(f32_dir(r.d.y)), iz = __builtin_amdgcn_rcpf(f32_dir(r.d.z));
-#else
-    const float ix = __builtin_amdgcn_rcpf(static_cast<float>(r.d.x)), iy = __builtin_amdgcn_rcpf(static_cast<float>(r.d.y)),
-                iz = __builtin_amdgcn_rcpf(static_cast<float>(r.d.z));
-#endif
     const float oix = ox * ix, oiy = oy * iy, oiz = oz * iz;
-    // L: the y slabs move with the ray time (layout.h motion planes): plane(tm) * iy = plane0 * iy + dplane * (tm * iy)
-    const float tiy = (L && ART_LDS_MOTION) ? static_cast<float>(r.tm) * iy : 0.0f;
     // LDS variant: the near and far plane of each axis follow from the direction's sign, so the slab test reads them
     // directly (near plane offset per axis; the far plane is always the plane above it, one kLdsPlane away -- an
     // immediate DS offset -- since each axis stores lo, hi, lo) and needs no per-axis min/max
@@ -918,9 +712,9 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
     // L: |d|^2 and its reciprocal for the leaf root divisions (div_rcp).  A traced direction is never zero (camera
     // rays point at the focus plane, scatter directions pass near_zero / dot(d, n) > 0) and its components are 0 or
     // differences of scene-scale doubles, so |d|^2 lies far inside div_rcp's range (> 2^-500, < 2^16).
-    // ART_SPH_PRE_G: the same for the HBM-scene traversal of triangle-free kernels (leaf spheres: the Next-Week final's
+    // The same for the HBM-scene traversal of triangle-free kernels (leaf spheres: the Next-Week final's
     // cluster, the Cornell and two-sphere scenes); their directions are camera rays and scatter directions too
-    constexpr bool kSphPre = !L && ART_SPH_PRE_G && (F & F_SPHERE) != 0 && (F & F_TRI) == 0 && ART_LEAF_PRIMS_G;
+    constexpr bool kSphPre = !L && (F & F_SPHERE) != 0 && (F & F_TRI) == 0;
     const R d_a = (L || kSphPre) ? len2(r.d) : R(0);
     const R d_inv_a = (L || kSphPre) ? R(1) / d_a : R(0);
     bool hit = false;
@@ -930,9 +724,9 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
     constexpr bool PK = !L && (F & F_CODE16) != 0;
     static_assert(!PK || (F & F_MEDIA_G) == 0, "packed keys need tmin > 0: no medium boundary traversals");
     LaneStack<B, L || PK> st(stk);
-    // ART_NF_HOIST: the near-plane offsets computed once per traversal in kernels with every node in LDS (PL 2) and no
+    // kNfHoist: the near-plane offsets computed once per traversal in kernels with every node in LDS (PL 2) and no
     // instance transforms (the lighter register budgets: dino's LM 1 kernel), instead of 6 VALU per node visit
-    constexpr bool kNfHoist = !L && ART_NF_HOIST && ART_NF_XOR && PL == 2 && (F & F_XFORM) == 0;
+    constexpr bool kNfHoist = !L && PL == 2 && (F & F_XFORM) == 0;
     [[maybe_unused]] const uint32_t nf_hx = (__float_as_uint(ix) >> 31) << 4, nf_hy = (__float_as_uint(iy) >> 31) << 4,
                                     nf_hz = (__float_as_uint(iz) >> 31) << 4;
     // L: inner nodes are coded by their byte offset in a node plane (index * 16, layout.h), so a visit's plane
@@ -952,12 +746,10 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
 #define ART_DPUSH(q, keep) do { } while (0)
 #define ART_DPOP(c) do { } while (0)
 #endif
-#if ART_SPECULATIVE
     // Speculative while-while (Aila & Laine 2009): a lane that reaches a leaf parks it and keeps walking inner nodes
     // until every lane of the wave holds a leaf, so the node loop runs with more lanes active; parked leaves are then
     // tested together.  Nodes visited past a parked leaf used the older (larger) tmax: extra visits, same closest hit.
     int32_t parked = kNodeEmpty;
-#endif
     // hoisted (wave-uniform: the BVH object's leaf of hoisted primitives, ObjRec::b): every lane tests it in the first
     // leaf phase, at once and before any node visit, so the tree walk starts with its closest hit as tmax.  Speculative
     // walk: it is the parked leaf and the first node loop is skipped (a wave-uniform flag; pushing the root under it
@@ -966,13 +758,8 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
     [[maybe_unused]] bool skip_nodes = false;
     if (hoisted != kNodeEmpty && (!RES || rs->fresh)) {
         const int32_t h = L ? lds_leaf(leaf_first(hoisted), leaf_count(hoisted)) : PK ? make_leaf16(leaf_first(hoisted), leaf_count(hoisted)) : hoisted;
-#if ART_SPECULATIVE
         parked = h;
         skip_nodes = true;
-#else
-        st.push(root_code, true);
-        node = h;
-#endif
     }
     if constexpr (RES) {
         if (!rs->fresh) {
@@ -997,7 +784,7 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
         }
         ART_STAT_WAVE(4);
         ART_STAT_LANE(5);
-        while (node >= 0 && !skip_nodes) {  // skip_nodes: ART_SPECULATIVE only
+        while (node >= 0 && !skip_nodes) {
             ART_STAT_WAVE(0);
             ART_STAT_LANE(1);
 #ifdef ART_STATS
@@ -1005,7 +792,6 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
 #endif
             float4 lx, hx, ly, hy, lz, hz;  // L: near (lx, ly, lz) and far (hx, hy, hz) planes
             int4 ch;
-            [[maybe_unused]] float4 dly, dhy;  // L: near / far y motion planes
             if constexpr (L) {
                 const uint32_t n16 = static_cast<uint32_t>(node);  // index * 16
                 const uint32_t ax = n16 + off_nx, ay = n16 + off_ny, az = n16 + off_nz;
@@ -1015,86 +801,61 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                 hy = lds_f4(ay + kLdsPlane);
                 lz = lds_f4(az);
                 hz = lds_f4(az + kLdsPlane);
-#if ART_LDS_MOTION
-                dly = lds_f4(ay + (kLdsNodePlaneMotion - 3) * kLdsPlane);
-                dhy = lds_f4(ay + (kLdsNodePlaneMotion - 2) * kLdsPlane);
-#endif
-#if ART_CHILD16
                 {  // four 16-bit child codes in 8 bytes (layout.h): a ds_read_b64 instead of a ds_read_b128; codes 1
                    // and 3 stay in the high halves (slab4_packed builds their keys with one byte permute)
                     typedef unsigned u2v __attribute__((ext_vector_type(2)));
                     const u2v cw = *(__attribute__((address_space(3))) const u2v*)(size_t)(kLdsOffNodes + kLdsNodePlaneChild * kLdsPlane + n16);
                     ch = make_int4(static_cast<int32_t>(cw.x), static_cast<int32_t>(cw.x), static_cast<int32_t>(cw.y), static_cast<int32_t>(cw.y));
                 }
-#else
-                ch = lds_i4(kLdsOffNodes + kLdsNodePlaneChild * kLdsPlane + n16);
-#endif
             }
-            // !L (ART_NEAR_FAR_G): byte offsets of each axis' near plane in a BvhNode (lo x / y / z at 0 / 32 / 64, its hi
-            // plane 16 above), from the direction's sign; the far plane is the other one (offset ^ 16).  Recomputed per
-            // visit from 1/d (live anyway; the empty asm keeps the compiler from hoisting three more loop-carried VGPRs)
+            // !L: each axis' near plane in a BvhNode is at sign(1/d) * 16 from that axis' lo plane (lo x / y / z at 0 / 32 /
+            // 64, its hi plane 16 above) and the far plane is the other one (near ^ 16): the same keys as per-axis min/max
+            // (the FMA rounding is monotone in the plane; an empty slot's inverted +-FLT_MAX box stays missed), 24 fewer
+            // VALU per node visit.  Recomputed per visit from 1/d (live anyway; the empty asm keeps the compiler from
+            // hoisting three more loop-carried VGPRs) unless kNfHoist
             [[maybe_unused]] uint32_t nfx = 0, nfy = 0, nfz = 0;
             if constexpr (!L) {
-                if (ART_NEAR_FAR_G && kNfHoist) {  // the per-ray offsets, loop-invariant (3 VGPRs live over the walk)
+                if (kNfHoist) {  // the per-ray offsets, loop-invariant (3 VGPRs live over the walk)
                     nfx = nf_hx;
                     nfy = nf_hy;
                     nfz = nf_hz;
-                } else if (ART_NEAR_FAR_G) {
+                } else {
                     uint32_t sx, sy, sz;  // sign bits of 1/d, extracted in the loop (volatile: not hoisted)
                     __asm__ volatile("v_lshrrev_b32 %0, 31, %1" : "=v"(sx) : "v"(ix));
                     __asm__ volatile("v_lshrrev_b32 %0, 31, %1" : "=v"(sy) : "v"(iy));
                     __asm__ volatile("v_lshrrev_b32 %0, 31, %1" : "=v"(sz) : "v"(iz));
                     nfx = sx << 4;
-                    nfy = (ART_NF_XOR ? 0u : 32u) + (sy << 4);
-                    nfz = (ART_NF_XOR ? 0u : 64u) + (sz << 4);
+                    nfy = sy << 4;
+                    nfz = sz << 4;
                 }
             }
             if constexpr (L) {
             } else if (PL == 2 || (PL == 1 && static_cast<uint32_t>(node) < S.n_lds_nodes)) {  // PL 2: every node in LDS
                 // the top levels, copied into LDS: explicit LDS loads (a generic pointer here would be merged with
                 // the global branch's into flat loads)
-                // kCompact (LM 2, ART_LM2_COMPACT): 112-B LDS nodes (the 96 B of planes, the 16-bit codes at +96), so
-                // ~15 % more of the tree fits; the far plane is at a - sign * 16 + 16 (a is only 16-aligned)
-                constexpr bool kCompact = PL == 1 && ART_LM2_COMPACT && PK && ART_NEAR_FAR_G;
-                const uint32_t a = S.nodes_lds + static_cast<uint32_t>(node) * (kCompact ? kLdsCompactNode : static_cast<uint32_t>(sizeof(BvhNode)));
-                if (kCompact) {
-                    const uint32_t nx = a + nfx, ny = a + nfy, nz = a + nfz, fx = a - nfx, fy = a - nfy, fz = a - nfz;
-                    lx = lds_f4(nx); hx = lds_f4(fx + 16u); ly = lds_f4(ny + 32u); hy = lds_f4(fy + 48u);
-                    lz = lds_f4(nz + 64u); hz = lds_f4(fz + 80u);
-                } else if (ART_NEAR_FAR_G && ART_NF_XOR) {
+                const uint32_t a = S.nodes_lds + static_cast<uint32_t>(node) * static_cast<uint32_t>(sizeof(BvhNode));
+                {
                     // node addresses are multiples of 32 (the LDS node array is 128-aligned): near plane = a + sign * 16,
                     // far plane = near ^ 16, and the y / z planes' +32 / +64 ride in the loads' immediate offsets
                     const uint32_t nx = a + nfx, ny = a + nfy, nz = a + nfz;
                     lx = lds_f4(nx); hx = lds_f4(nx ^ 16u); ly = lds_f4(ny + 32u); hy = lds_f4((ny ^ 16u) + 32u);
                     lz = lds_f4(nz + 64u); hz = lds_f4((nz ^ 16u) + 64u);
-                } else if (ART_NEAR_FAR_G) {  // lx/ly/lz: near planes, hx/hy/hz: far planes
-                    lx = lds_f4(a + nfx); hx = lds_f4(a + (nfx ^ 16u)); ly = lds_f4(a + nfy); hy = lds_f4(a + (nfy ^ 16u));
-                    lz = lds_f4(a + nfz); hz = lds_f4(a + (nfz ^ 16u));
-                } else {
-                    lx = lds_f4(a); hx = lds_f4(a + 16); ly = lds_f4(a + 32); hy = lds_f4(a + 48); lz = lds_f4(a + 64); hz = lds_f4(a + 80);
                 }
                 if constexpr (PK) {  // the four 16-bit codes (BvhNode::pad), codes 1 and 3 in the high halves
-                    const uint2 cw = lds_u2(a + (kCompact ? 96u : 112u));
+                    const uint2 cw = lds_u2(a + 112u);
                     ch = make_int4(static_cast<int32_t>(cw.x), static_cast<int32_t>(cw.x), static_cast<int32_t>(cw.y), static_cast<int32_t>(cw.y));
                 } else {
                     ch = lds_i4(a + 96);
                 }
             } else {
                 const float4* np = reinterpret_cast<const float4*>(S.nodes + node);
-                if (ART_NEAR_FAR_G && ART_NF_XOR) {  // 32-bit offsets from the node array's base, as above
+                {  // 32-bit offsets from the node array's base, as above
                     const char* nb = reinterpret_cast<const char*>(S.nodes);
                     const uint32_t o = static_cast<uint32_t>(node) * static_cast<uint32_t>(sizeof(BvhNode));
                     const uint32_t nx = o + nfx, ny = o + nfy, nz = o + nfz;
                     lx = *reinterpret_cast<const float4*>(nb + nx); hx = *reinterpret_cast<const float4*>(nb + (nx ^ 16u));
                     ly = *reinterpret_cast<const float4*>(nb + ny + 32u); hy = *reinterpret_cast<const float4*>(nb + ((ny ^ 16u) + 32u));
                     lz = *reinterpret_cast<const float4*>(nb + nz + 64u); hz = *reinterpret_cast<const float4*>(nb + ((nz ^ 16u) + 64u));
-                } else if (ART_NEAR_FAR_G) {
-                    const char* nb = reinterpret_cast<const char*>(np);
-                    lx = *reinterpret_cast<const float4*>(nb + nfx); hx = *reinterpret_cast<const float4*>(nb + (nfx ^ 16u));
-                    ly = *reinterpret_cast<const float4*>(nb + nfy); hy = *reinterpret_cast<const float4*>(nb + (nfy ^ 16u));
-                    lz = *reinterpret_cast<const float4*>(nb + nfz); hz = *reinterpret_cast<const float4*>(nb + (nfz ^ 16u));
-                } else {
-                    lx = np[0]; hx = np[1]; ly = np[2]; hy = np[3]; lz = np[4]; hz = np[5];
                 }
                 if constexpr (PK) {
                     const uint2 cw = reinterpret_cast<const uint2*>(np)[14];
@@ -1112,14 +873,12 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                 // 16-bit child codes ride in the low half of the entry-distance keys: the network is 5 integer
                 // min/max pairs and each code comes back with one bit-field extract
                 uint32_t q0, q1, q2, q3;
-                slab4_packed<ART_LDS_MOTION != 0>(lx, hx, ly, hy, lz, hz, dly, dhy, ch, ix, iy, iz, tiy, oix, oiy, oiz, tminf, tmaxf, q0, q1, q2, q3);
+                slab4_packed(lx, hx, ly, hy, lz, hz, ch, ix, iy, iz, oix, oiy, oiz, tminf, tmaxf, q0, q1, q2, q3);
                 ucas(q0, q1);
                 ucas(q2, q3);
                 ucas(q0, q2);
                 ucas(q1, q3);
-                // ART_SORT_PARTIAL: without the last exchange q1 / q2 (the 2nd and 3rd nearest) may be pushed in either
-                // order; q0 (the next node) and q3 (the farthest) are exact
-                if (!ART_SORT_PARTIAL) ucas(q1, q2);
+                ucas(q1, q2);
                 if (q0 >= kKeyMiss) ART_STAT_LANE(12);  // a dead visit: no child box is entered before tmax
                 st.push(static_cast<int32_t>(q3), q3 < kKeyMiss);
                 st.push(static_cast<int32_t>(q2), q2 < kKeyMiss);
@@ -1148,8 +907,7 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                 near_child = static_cast<int16_t>(q0);
             } else {
                 float k0, k1, k2, k3;
-                if (ART_NEAR_FAR_G) slab4_nf(lx, hx, ly, hy, lz, hz, ix, iy, iz, oix, oiy, oiz, tminf, tmaxf, k0, k1, k2, k3);
-                else slab4(lx, hx, ly, hy, lz, hz, ch, ix, iy, iz, oix, oiy, oiz, tminf, tmaxf, k0, k1, k2, k3);
+                slab4_nf(lx, hx, ly, hy, lz, hz, ix, iy, iz, oix, oiy, oiz, tminf, tmaxf, k0, k1, k2, k3);
                 int32_t c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
                 cas(k0, c0, k1, c1);
                 cas(k2, c2, k3, c3);
@@ -1163,66 +921,33 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                 near = k0 < inf;
                 near_child = c0;
             }
-#if ART_SPECULATIVE && ART_PARK_BRANCHLESS
-            if constexpr (L) {
-                // the next node and the one under it, read together: a lane that parks a leaf takes the second without
-                // a dependent stack read inside a divergent branch
-                const int32_t t0 = st.peek(), t1 = st.peek_below();
-                const int32_t n0 = near ? near_child : t0;  // the next node
-                const int32_t n1 = near ? t0 : t1;          // the stack entry under it
-                const bool park = n0 < kNodeEmpty && parked == kNodeEmpty;  // a leaf and none parked yet: park it
-                parked = park ? n0 : parked;
-                node = park ? n1 : n0;
-                st.pop_if(!near);
-                st.pop_if(park);
-                ART_DPOP(!near);
-                ART_DPOP(park);
-            } else
-#endif
             {
                 const int32_t top = st.peek();
-#if ART_SPECULATIVE && ART_PARK_PREFETCH
-                // L: the entry under the top is read with it, so a lane that parks takes its next node without a
-                // dependent stack read inside the branch
-                [[maybe_unused]] int32_t below = 0;
-                if constexpr (L) below = st.peek_below();
-#endif
                 node = near ? near_child : top;
                 st.pop_if(!near);
                 ART_DPOP(!near);
-#if ART_SPECULATIVE
                 if (node < kNodeEmpty && parked == kNodeEmpty) {  // a leaf (codes below -1) and none parked yet: park it
                     parked = node;
-#if ART_PARK_PREFETCH
-                    if constexpr (L) node = near ? top : below;
-                    else node = st.peek();
-#else
                     node = st.peek();
-#endif
                     st.pop_if(true);
                     ART_DPOP(true);
                 }
-#endif
             }
-#if ART_SPECULATIVE
             if (!__any(parked == kNodeEmpty)) break;  // every lane still walking holds a leaf: test them together
-#endif
         }
-#if ART_SPECULATIVE
         // leaf phase: the parked leaf, else the current node when it is a leaf (a lane that left the node loop on the
-        // wave-wide break still has an inner node to return to)
-        // L: a lane that left the node loop holding a second leaf (parked + current) tests both in this phase, one
-        // leaf phase instead of two (the wave's leaf loop runs over the longer sum, once)
+        // wave-wide break still has an inner node to return to).  A lane that left the node loop holding a second leaf
+        // (parked + current) tests both in this phase, one leaf phase instead of two (the wave's leaf loop runs over
+        // the longer sum, once).  The stack is read once up front and the choices are selects (no dependent read in a
+        // divergent branch).
         skip_nodes = false;
         int32_t leaf = parked;
         int32_t leaf2 = kNodeEmpty;
-#if ART_LEAFSEL_BRANCHLESS
-        if constexpr (L || ART_LEAFSEL_BRANCHLESS_G) {
-            // the same choices as below, with the stack read once up front (no dependent read in a divergent branch)
+        {
             const bool has = parked != kNodeEmpty;
             if (!has && node == kNodeEmpty) break;
             const int32_t t0 = st.peek();
-            const bool take2 = has && (L || ART_LEAF2_G) && node < kNodeEmpty;  // a second leaf in hand: test both in this phase
+            const bool take2 = has && node < kNodeEmpty;  // a second leaf in hand: test both in this phase
             const bool pop = take2 || !has;
             leaf = has ? parked : node;
             leaf2 = take2 ? node : kNodeEmpty;
@@ -1230,84 +955,42 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
             st.pop_if(pop);
             ART_DPOP(pop);
             parked = kNodeEmpty;
-        } else
-#endif
-        if (leaf != kNodeEmpty) {
-            parked = kNodeEmpty;
-            if ((L || ART_LEAF2_G) && node < kNodeEmpty) {
-                leaf2 = node;
-                node = st.peek();
-                st.pop_if(true);
-                ART_DPOP(true);
-            }
-        } else {
-            if (node == kNodeEmpty) break;
-            leaf = node;
-            node = st.peek();
-            st.pop_if(true);
-            ART_DPOP(true);
         }
-#else
-        if (node == kNodeEmpty) break;
-        const int32_t leaf = node;
-        node = st.peek();
-        st.pop_if(true);
-#endif
         uint32_t first, cnt;
-#if ART_SPECULATIVE
         uint32_t first2 = 0, cnt12 = 0;
-#endif
         if constexpr (L) {
             const uint32_t x = ~static_cast<uint32_t>(leaf);
             first = x & ((1u << kLdsLeafShift) - 1);
             cnt = x >> kLdsLeafShift;
-#if ART_SPECULATIVE
             const uint32_t x2 = leaf2 == kNodeEmpty ? 0u : ~static_cast<uint32_t>(leaf2);
             first2 = (x2 & ((1u << kLdsLeafShift) - 1)) - cnt;  // slot of entry k >= cnt: first2 + k
             cnt12 = cnt + (x2 >> kLdsLeafShift);
-#endif
         } else if constexpr (PK) {
             first = leaf16_first(leaf);
             cnt = leaf16_count(leaf);
-#if ART_SPECULATIVE
             // leaf2 == kNodeEmpty decodes as an empty range (count 0)
             first2 = leaf16_first(leaf2) - cnt;
             cnt12 = cnt + leaf16_count(leaf2);
-#endif
         } else {
             first = leaf_first(leaf);
             cnt = leaf_count(leaf);
-#if ART_SPECULATIVE
             // leaf2 == kNodeEmpty decodes as an empty range (first 0, count 0)
             first2 = leaf_first(leaf2) - cnt;
             cnt12 = cnt + leaf_count(leaf2);
-#endif
         }
-#if ART_SPECULATIVE
         for (uint32_t k = 0; k < cnt12; ++k) {
-#else
-        for (uint32_t k = 0; k < cnt; ++k) {
-#endif
             ART_STAT_WAVE(2);
             ART_STAT_LANE(3);
             R tt;
             uint32_t fc = 0, ref, m = kMatUnknown;
             bool h;
             if constexpr (L) {
-#if ART_SPECULATIVE
                 const uint32_t slot = (k < cnt ? first : first2) + k;
-#else
-                const uint32_t slot = first + k;
-#endif
                 h = hit_lds_slot(lds, slot, r, d_a, d_inv_a, tmin, tmax, tt, ref, m);
                 fc = slot;  // the leaf slot travels in the face field (spheres have no face): LDS shading reads it
             } else {
-#if ART_SPECULATIVE
                 const uint32_t slot = (k < cnt ? first : first2) + k;
-#else
-                const uint32_t slot = first + k;
-#endif
-                if constexpr ((F & F_TRI) != 0 && ART_LEAF_TRIS && ART_TRI112 && PL == 2) {
+                if constexpr ((F & F_TRI) != 0 && PL == 2) {
                     // the LM 1 kernels' leaf triangles with their planes (TriRec112, in LDS): no cross product or
                     // plane offset per test
                     const TriRec112<R>& lt = S.leaf_tris112[slot];
@@ -1318,7 +1001,7 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                     __asm__ volatile("" : "+v"(nn.x), "+v"(nn.y), "+v"(nn.z), "+v"(pdd));
                     if (fbase(F) == F_TRI || primref_type(ref) == PRIM_TRIANGLE) h = hit_tri_pre(p1, p2, p3, nn, pdd, r, tmin, tmax, tt);
                     else h = hit_prim<R, F & ~F_TRI>(S, ref, r, tmin, tmax, tt, fc);
-                } else if constexpr ((F & F_TRI) != 0 && ART_LEAF_TRIS) {
+                } else if constexpr ((F & F_TRI) != 0) {
                     // the leaf-ordered triangle copy: its address depends on the slot alone, so its loads go out
                     // beside the primref's instead of behind it (one L2 round trip per test instead of two); the
                     // empty asm keeps the compiler from sinking them under the type test
@@ -1328,7 +1011,7 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                     __asm__ volatile("" : "+v"(p1.x), "+v"(p1.y), "+v"(p1.z), "+v"(p2.x), "+v"(p2.y), "+v"(p2.z), "+v"(p3.x), "+v"(p3.y), "+v"(p3.z));
                     if (fbase(F) == F_TRI || primref_type(ref) == PRIM_TRIANGLE) h = hit_tri_v(p1, p2, p3, r, tmin, tmax, tt);
                     else h = hit_prim<R, F & ~F_TRI>(S, ref, r, tmin, tmax, tt, fc);
-                } else if constexpr ((F & F_TRI) == 0 && ART_LEAF_PRIMS_G) {
+                } else {
                     // the leaf-ordered record copy: its loads go out beside the primref's instead of behind it
                     const uint4* lp = reinterpret_cast<const uint4*>(S.leaf_prims + slot);
                     uint4 v0 = lp[0], v1 = lp[1], v2 = lp[2], v3 = lp[3], v4 = lp[4];
@@ -1352,9 +1035,6 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                     } else {
                         h = hit_prim_rec<R, F>(primref_type(ref), rec, r, tmin, tmax, tt, fc);
                     }
-                } else {
-                    ref = S.primrefs[slot];
-                    h = hit_prim<R, F>(S, ref, r, tmin, tmax, tt, fc);
                 }
 #ifdef ART_STATS
                 {  // leaf tests by primitive type: lane tests [15/17/19/21], wave iterations running that type [16/18/20/22]
@@ -1398,34 +1078,9 @@ __device__ __forceinline__ Ray<R> xform_in(const ObjRec<R>& o, const Ray<R>& r) 
 }
 
 // Any non-medium object: prim, BVH, or a translate/rotate_y chain (<= kMaxXformChain) over one of them.
-// ART_XFORM_CULL: an instance is first tested against its world-space cull box (layout.h ObjBox) with the traversal's
-// own conservative f32 slab arithmetic; a miss skips the transform into object space and the whole object test.
-// Measured on the Next-Week final (its 1000-sphere cluster under translate(rotate_y)): -0.3 % (6 628 vs 6 650
-// Msamples/s at 256 spp): the root node's own test rejects the same rays, and every ray pays the box test.  Off.
-#ifndef ART_XFORM_CULL
-#define ART_XFORM_CULL 0
-#endif
-template <class R>
-__device__ __forceinline__ bool cull_box_hit(const ObjBox& b, const Ray<R>& r, R tmin, R tmax) {
-    const float ix = __builtin_amdgcn_rcpf(f32_dir(r.d.x)), iy = __builtin_amdgcn_rcpf(f32_dir(r.d.y)), iz = __builtin_amdgcn_rcpf(f32_dir(r.d.z));
-    const float oix = static_cast<float>(r.o.x) * ix, oiy = static_cast<float>(r.o.y) * iy, oiz = static_cast<float>(r.o.z) * iz;
-    const float x0 = fmaf(b.lo[0], ix, -oix), x1 = fmaf(b.hi[0], ix, -oix);
-    const float y0 = fmaf(b.lo[1], iy, -oiy), y1 = fmaf(b.hi[1], iy, -oiy);
-    const float z0 = fmaf(b.lo[2], iz, -oiz), z1 = fmaf(b.hi[2], iz, -oiz);
-    const float lo = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), f_lo(tmin)));
-    const float hi = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), f_hi(tmax)));
-    return lo <= hi;
-}
 template <class R, uint32_t F, int B, bool L, int PL = 0, bool RES = false>
 __device__ __forceinline__ bool hit_object(const DevScene<R>& S, const uint8_t* lds, int32_t oi, Ray<R> r, R tmin, R tmax, StackF<L, F>* stk,
                                            R& t, uint32_t& prim, uint32_t& face, uint32_t& mt, TravResume* rs = nullptr) {
-    if constexpr ((F & F_XFORM) != 0 && ART_XFORM_CULL) {
-        // a resumed traversal passed the box when it started
-        if (!RES || rs->fresh) {
-            const ObjBox& b = S.obj_box[oi];
-            if (b.valid && !cull_box_hit(b, r, tmin, tmax)) return false;
-        }
-    }
     if (F & F_XFORM) {
 #pragma unroll
         for (int c = 0; c < kMaxXformChain; ++c) {
@@ -1440,7 +1095,7 @@ __device__ __forceinline__ bool hit_object(const DevScene<R>& S, const uint8_t* 
         prim = static_cast<uint32_t>(o.a);
         mt = kMatUnknown;
         // HBM-scene kernels: the primitive's record from obj_prims[oi], whose address does not wait on the object
-        if constexpr (!L && ART_OBJ_PRIMS) return hit_prim_rec<R, F>(primref_type(prim), S.obj_prims[oi], r, tmin, tmax, t, face);
+        if constexpr (!L) return hit_prim_rec<R, F>(primref_type(prim), S.obj_prims[oi], r, tmin, tmax, t, face);
         else return hit_prim<R, F>(S, prim, r, tmin, tmax, t, face);
     }
     return traverse<R, F, B, L, PL, RES>(S, lds, o.a, r, tmin, tmax, stk, t, prim, face, mt, rs, o.b);
@@ -1448,15 +1103,6 @@ __device__ __forceinline__ bool hit_object(const DevScene<R>& S, const uint8_t* 
 
 // Out of line: measured +0.2 % (cow) to +1.8 % (Next-Week final) over the inlined body, which raised the register
 // pressure of the whole path loop for a function most segments do not reach.
-// ART_MEDIUM_FASTREJECT: hit_medium decides "no scatter" from an f32 log2 bound before the exact glibc log.  Exact
-// (the bound is far wider than v_log_f32's error) but measured -0.2 % (cow) to -1.2 % (dino) (r3k): a lane's
-// rejection skips nothing while any lane of its wave scatters, and nearly every wave has one.  Off.
-#ifndef ART_MEDIUM_RCP
-#define ART_MEDIUM_RCP 0  // hit_medium (sphere boundary): the two root divisions through one reciprocal (r3j: off, see ART_BOX_RCP)
-#endif
-#ifndef ART_MEDIUM_FASTREJECT
-#define ART_MEDIUM_FASTREJECT 0
-#endif
 static __device__ __noinline__ double glibc_log_call(double x) { return glibc_log(x); }
 // constant_medium.h:37-82.  Consumes one uniform when the clamped interval is non-empty.
 template <class R, uint32_t F, int B, bool L, int PL = 0>
@@ -1471,7 +1117,7 @@ __device__ __forceinline__ bool hit_medium(const DevScene<R>& S, const uint8_t* 
         // from the same ray and sphere, so both root selections (sphere.h:49-55) run on one quadratic: the same
         // values, half the arithmetic.
         const SphereRec<R>& sp = [&]() -> const SphereRec<R>& {
-            if constexpr (!L && ART_OBJ_PRIMS) return reinterpret_cast<const SphereRec<R>&>(S.obj_prims[m.a]);
+            if constexpr (!L) return reinterpret_cast<const SphereRec<R>&>(S.obj_prims[m.a]);
             else return S.spheres[primref_index(static_cast<uint32_t>(bo.a))];
         }();
         V3<R> center = ld3(sp.c);
@@ -1483,24 +1129,7 @@ __device__ __forceinline__ bool hit_medium(const DevScene<R>& S, const uint8_t* 
         const R disc = half_b * half_b - a * c;
         if (disc < R(0)) return false;
         const R sqrtd = sqrt_rn(disc);
-#if ART_MEDIUM_RCP
-        // both roots through one reciprocal (div_rcp: Markstein's correctly rounded quotient, the division's bits for
-        // normal a, numerator and quotient; a = |d|^2 lies in [2^-46, 2^20] for every traced ray, the guard keeps the
-        // division for anything else, e.g. the 2^-72-probability zero direction of an isotropic draw).  A -0
-        // numerator gives +0 here and -0 from the division: t1 <= 0 is raised to tmin and t2 <= 0 fails below, so
-        // the sign of a zero root never reaches a result.
-        R r_near, r_far;
-        if (a > R(0x1p-500) && a < R(0x1p500)) {
-            const R inv_a = R(1) / a;
-            r_near = div_rcp(-half_b - sqrtd, a, inv_a);
-            r_far = div_rcp(-half_b + sqrtd, a, inv_a);
-        } else {
-            r_near = (-half_b - sqrtd) / a;
-            r_far = (-half_b + sqrtd) / a;
-        }
-#else
         const R r_near = (-half_b - sqrtd) / a, r_far = (-half_b + sqrtd) / a;
-#endif
         t1 = r_near;  // first call, t in [-inf, inf]
         if (t1 < -inf || inf < t1) {
             t1 = r_far;
@@ -1530,19 +1159,6 @@ __device__ __forceinline__ bool hit_medium(const DevScene<R>& S, const uint8_t* 
     // scattering path's t and every sum after it.  glibc_log.h restates glibc's log operation by operation (equal for
     // every k * 2^-24); it replaced a 128 MiB table of glibc's values, whose random reads (an L2 miss per draw) cost 5-10 % on the medium scenes.
     const uint32_t k = uniform_k(rng);
-#if ART_MEDIUM_FASTREJECT
-    {
-        // decided without the exact log when hit_distance > inside by far more than the approximation's error: the
-        // uniform k * 2^-24 is exact in f32, v_log_f32 (log2) is within ~2^-21 relative + 2^-22 absolute, so
-        // |approx - hit_distance| < 2^-12 |approx| + 2^-16 |neg_inv_density| with a wide margin.  Most segments in the
-        // r = 5000 mist of the mesh scenes do not scatter (P(scatter) ~ 1 - e^-0.5), and they skip the out-of-line
-        // glibc log and its table load.  ξ = 0: log2(0) = -inf -> +inf > inside, as the exact path decides.
-        const double nid = static_cast<double>(m.p[0]);
-        const double approx = nid * (0.69314718055994531 * static_cast<double>(__builtin_amdgcn_logf(static_cast<float>(k) * 0x1p-24f)));
-        const double err = 0x1p-12 * __builtin_fabs(approx) + 0x1p-16 * __builtin_fabs(nid);
-        if (approx > static_cast<double>(inside) + err) return false;
-    }
-#endif
     const R hit_distance = m.p[0] * glibc_log_call(static_cast<double>(k) * 0x1p-24);
     if (hit_distance > inside) return false;
     t = t1 + hit_distance / ray_length;
@@ -1667,20 +1283,6 @@ __device__ __forceinline__ void rect_surface(Surf<R>& s, int axis, R a0, R a1, R
     set_face_normal(s, r, n);
     s.p = r.at(t);
 }
-// ART_SPHERE_UV_CALL: get_sphere_uv (sphere.h:24-37) out of line.  Inlined, the f64 polynomial constants of acos and
-// atan2 are hoisted out of the path loop (into VGPRs, 29 of them spilled to scratch at kernel start) in the
-// image-texture kernels; out of line the final-scene kernel drops from 168 VGPRs + 58 spilled to 151 and none, but the
-// call costs more than the reloads, which only earth-texture hits run: -1.0 % on the Next-Week final.  Off.
-#ifndef ART_SPHERE_UV_CALL
-#define ART_SPHERE_UV_CALL 0
-#endif
-[[maybe_unused]] static __device__ __noinline__ void sphere_uv_call(double ox, double oy, double oz, double& u, double& v) {
-    const double pi = 3.1415926535897932385;
-    const double theta = acos(-oy);
-    const double phi = atan2(-oz, ox) + pi;
-    u = phi / (2.0 * pi);
-    v = theta / pi;
-}
 template <class R, uint32_t F, bool UV = true>
 __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref, uint32_t face, const Ray<R>& r, R t, Surf<R>& s) {
     const uint32_t idx = primref_index(ref);
@@ -1696,15 +1298,11 @@ __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref,
             set_face_normal(s, r, outward);
             // u,v only feed image textures: acos/atan2 are skipped for materials that never sample them
             if (UV && !moving && (S.mats[sp.mat].flags & MATF_NEEDS_UV)) {
-#if ART_SPHERE_UV_CALL
-                sphere_uv_call(outward.x, outward.y, outward.z, s.u, s.v);
-#else
                 const R pi = R(3.1415926535897932385);
                 const R theta = acos(-outward.y);
                 const R phi = atan2(-outward.z, outward.x) + pi;
                 s.u = phi / (R(2) * pi);
                 s.v = theta / pi;
-#endif
             } else {
                 s.u = R(0);
                 s.v = R(0);

@@ -693,13 +693,22 @@ DecodedImage decode_png(const uint8_t* b, size_t n) {
     uint32_t W = 0, H = 0;
     int depth = 0, ctype = -1, interlace = 0;
     std::vector<uint8_t> idat, plte, trns;
-    bool end_seen = false;
+    // tRNS as stb_image v2.27 takes it (stbi__parse_png_file), chunk by chunk: a palette image's tRNS sets the alpha of
+    // its first entries (a later tRNS overwrites its own length of them; even an empty one makes the image 4-channel);
+    // a gray / RGB image's tRNS is a colour key of one 16-bit sample per channel; refused after image data, before the
+    // palette, or on a type with alpha
+    std::vector<uint8_t> pal_alpha;
+    bool pal_trns = false, key_trns = false;
+    bool end_seen = false, first = true;
     while (at + 8 <= n && !end_seen) {
         const uint32_t len = be32(b + at);
         const uint8_t* type = b + at + 4;
         if (n - at < 12 || n - at - 12 < len) pbad("truncated chunk");  // length + type + data + CRC must all be present
         const uint8_t* d = b + at + 8;
-        if (!std::memcmp(type, "IHDR", 4)) {
+        const bool ihdr = !std::memcmp(type, "IHDR", 4);
+        if (first && !ihdr) pbad("first not IHDR");
+        if (ihdr) {
+            if (!first) pbad("multiple IHDR");
             if (len != 13) pbad("bad IHDR");
             W = be32(d);
             H = be32(d + 4);
@@ -709,10 +718,25 @@ DecodedImage decode_png(const uint8_t* b, size_t n) {
             interlace = d[12];
             if (interlace > 1) pbad("bad interlace method");
         } else if (!std::memcmp(type, "PLTE", 4)) {
+            if (len > 256 * 3 || len % 3) pbad("invalid PLTE");
             plte.assign(d, d + len);
+            if (pal_alpha.size() < len / 3) pal_alpha.resize(len / 3, 255);
+            std::fill(pal_alpha.begin(), pal_alpha.begin() + len / 3, static_cast<uint8_t>(255));
         } else if (!std::memcmp(type, "tRNS", 4)) {
-            trns.assign(d, d + len);
+            if (!idat.empty()) pbad("tRNS after IDAT");
+            if (ctype == 3) {
+                if (plte.empty()) pbad("tRNS before PLTE");
+                if (len > plte.size() / 3) pbad("bad tRNS len");
+                std::copy(d, d + len, pal_alpha.begin());
+                pal_trns = true;
+            } else {
+                if (ctype == 4 || ctype == 6) pbad("tRNS with alpha");
+                if (len != static_cast<uint32_t>(ctype == 2 ? 6 : 2)) pbad("bad tRNS len");
+                trns.assign(d, d + len);
+                key_trns = true;
+            }
         } else if (!std::memcmp(type, "IDAT", 4)) {
+            if (ctype == 3 && plte.empty()) pbad("no PLTE");
             idat.insert(idat.end(), d, d + len);
         } else if (!std::memcmp(type, "IEND", 4)) {
             end_seen = true;
@@ -720,6 +744,7 @@ DecodedImage decode_png(const uint8_t* b, size_t n) {
             pbad(std::string("unknown critical chunk ") + std::string(reinterpret_cast<const char*>(type), 4));
         }
         at += 12 + len;
+        first = false;
     }
     if (W == 0 || H == 0 || W > (1u << 24) || H > (1u << 24)) pbad("bad image size");
     int chans;
@@ -736,13 +761,6 @@ DecodedImage decode_png(const uint8_t* b, size_t n) {
                           ((ctype == 2 || ctype == 4 || ctype == 6) && (depth == 8 || depth == 16));
     if (!depth_ok) pbad("bad bit depth for the color type");
     if (ctype == 3 && (plte.empty() || plte.size() % 3)) pbad("missing or bad palette");
-    // tRNS as stb_image v2.27 accepts it (stbi__parse_png_file): at most one alpha per palette entry; a colour key of
-    // exactly one 16-bit sample per channel for gray / RGB; none for the types that carry alpha
-    if (!trns.empty()) {
-        if (ctype == 3 && trns.size() > plte.size() / 3) pbad("bad tRNS len");
-        if ((ctype == 0 || ctype == 2) && trns.size() != static_cast<size_t>(2 * chans)) pbad("bad tRNS len");
-        if (ctype == 4 || ctype == 6) pbad("tRNS with alpha");
-    }
     // inflate
     std::vector<uint8_t> raw;
     {
@@ -818,7 +836,7 @@ DecodedImage decode_png(const uint8_t* b, size_t n) {
     img.h = static_cast<int>(H);
     const size_t npx = static_cast<size_t>(W) * H;
     if (ctype == 3) {
-        const bool alpha = !trns.empty();
+        const bool alpha = pal_trns;
         img.channels = alpha ? 4 : 3;
         img.data.resize(npx * img.channels);
         const size_t npal = plte.size() / 3;
@@ -826,23 +844,29 @@ DecodedImage decode_png(const uint8_t* b, size_t n) {
             const size_t k = samples[i];
             if (k >= npal) pbad("palette index out of range");
             for (int c = 0; c < 3; ++c) img.data[i * img.channels + c] = plte[3 * k + c];
-            if (alpha) img.data[i * 4 + 3] = k < trns.size() ? trns[k] : 255;
+            if (alpha) img.data[i * 4 + 3] = pal_alpha[k];
         }
         return img;
     }
-    const bool key = !trns.empty() && (ctype == 0 || ctype == 2);
+    const bool key = key_trns;
     img.channels = chans + (key ? 1 : 0);
     img.data.resize(npx * img.channels);
     static const int scale[9] = {0, 0xff, 0x55, 0, 0x11, 0, 0, 0, 0x01};
+    // the colour key as stb compares it: 16-bit samples as they are; below 16 bits the key's low byte times the depth
+    // scale, in 8 bits (stbi_uc), against the scaled 8-bit sample
+    uint16_t kv[3] = {0, 0, 0};
+    if (key)
+        for (int c = 0; c < chans; ++c) {
+            const uint16_t k16 = static_cast<uint16_t>((trns[2 * c] << 8) | trns[2 * c + 1]);
+            kv[c] = depth == 16 ? k16 : static_cast<uint8_t>((k16 & 255) * scale[depth]);
+        }
     for (size_t i = 0; i < npx; ++i) {
         bool transparent = key;
         for (int c = 0; c < chans; ++c) {
             const uint16_t s = samples[i * chans + c];
-            if (key) {
-                const uint16_t kv = static_cast<uint16_t>((trns[2 * c] << 8) | trns[2 * c + 1]);
-                if (s != kv) transparent = false;
-            }
-            img.data[i * img.channels + c] = depth == 16 ? static_cast<uint8_t>(s >> 8) : static_cast<uint8_t>(s * scale[depth]);
+            const uint8_t v8 = depth == 16 ? static_cast<uint8_t>(s >> 8) : static_cast<uint8_t>(s * scale[depth]);
+            if (key && (depth == 16 ? s : v8) != kv[c]) transparent = false;
+            img.data[i * img.channels + c] = v8;
         }
         if (key) img.data[i * img.channels + chans] = transparent ? 0 : 255;
     }

@@ -151,21 +151,12 @@ template <class R> struct ResRec;  // final per-slot radiance
 template <> struct ResRec<float> { float4 v; };
 template <> struct ResRec<double> { double x, y, z; };  // 24 B, unpadded: k_accum streams these at HBM rate
 __device__ __forceinline__ void store_res(ResRec<float>* res, uint32_t q, V3<float> L) { res[q].v = make_float4(L.x, L.y, L.z, 0.0f); }
-// ART_RES_NT: the radiance records stream out with non-temporal stores (read once, by k_accum after the pass), so they
+// The radiance records stream out with non-temporal stores (read once, by k_accum after the pass), so they
 // do not evict the L2-resident camera-ray rings of k_paths
-#ifndef ART_RES_NT
-#define ART_RES_NT 1
-#endif
 __device__ __forceinline__ void store_res(ResRec<double>* res, uint32_t q, V3<double> L) {
-#if ART_RES_NT
     __builtin_nontemporal_store(L.x, &res[q].x);
     __builtin_nontemporal_store(L.y, &res[q].y);
     __builtin_nontemporal_store(L.z, &res[q].z);
-#else
-    res[q].x = L.x;
-    res[q].y = L.y;
-    res[q].z = L.z;
-#endif
 }
 __device__ __forceinline__ void load_res(const ResRec<float>* res, uint32_t q, double& r, double& g, double& b) {
     const float4 v = res[q].v;
@@ -231,7 +222,7 @@ struct Work {
     uint32_t* counters;         // [(depth * kQueueKinds + kind) * kShards + shard] * kCounterStride
     unsigned long long* segments;
     double* acc;                // local pixels * 3
-    void* pool;                 // k_paths camera-ray rings (ART_RAY_POOL): kPoolRing PoolRays per wave
+    void* pool;                 // k_paths camera-ray rings: kPoolRing PoolRays per wave
 };
 template <class R>
 __host__ __device__ __forceinline__ uint32_t* counter(const Work<R>& w, int d, int kind, int s) {
@@ -426,16 +417,8 @@ __device__ __forceinline__ bool shade_hit_lds(const uint8_t* lds, uint32_t slot,
     const uint32_t code = reinterpret_cast<const uint32_t*>(lds + kLdsOffRef)[slot];
     const uint32_t mi = reinterpret_cast<const uint16_t*>(lds + kLdsOffMatIdx)[slot];
     V3<R> center{a.x, a.y, b.x};
-#if ART_LDS_DY_SLOT
     center.y = center.y + st.ray.tm * reinterpret_cast<const double*>(lds + kLdsOffMov)[slot];  // dy = -0: static
     (void)code;
-#else
-    const uint32_t mv = (code >> kLdsRefMovShift) & ((1u << (kLdsRefMatShift - kLdsRefMovShift)) - 1);
-    if (mv) {  // moving_sphere.h:72-74, as prim_surface; unit shutter, y motion (lds_scene_image): (tm - 0) / 1 == tm,
-               // and x + tm * (+0) == x, z + tm * (+0) == z
-        center.y = center.y + st.ray.tm * reinterpret_cast<const double*>(lds + kLdsOffMov)[mv - 1];
-    }
-#endif
     Surf<R> s;
     s.p = st.ray.at(t);
     set_face_normal(s, st.ray, reinterpret_cast<const double*>(lds + kLdsOffInvR)[slot] * (s.p - center));  // (p - c) / r
@@ -661,17 +644,10 @@ __global__ __launch_bounds__(L ? kBlockL : kBlock, L ? 1 : ART_EXTEND_MIN_WAVES)
 // below the ~88 M/s a single word sustains).  The bounce arithmetic and the RNG draws are those of the fused
 // k_extend, so images are bit-identical to the wavefront variants.
 constexpr uint32_t kPathChunk = 256;
-// Camera-ray pool (ART_RAY_POOL): a path start is run by the whole wave for however few lanes start a path (~a third
+// Camera-ray pool: a path start is run by the whole wave for however few lanes start a path (~a third
 // of them per round), so the camera rays are generated 64 at a time -- one per lane, converged -- into a per-wave ring
 // in global memory (L2-resident: 8 KiB per wave), and a starting lane loads the next ring entry instead.  Entry pos
 // holds the ray of slot base[(pos / 64) & 1] + pos % 64; tm = NaN marks a padding slot of a partial tile.
-#ifndef ART_RAY_POOL
-#define ART_RAY_POOL 1
-#endif
-#ifndef ART_RAY_POOL_G
-#define ART_RAY_POOL_G 0  // the same ring in k_paths_g: measured -1 % to -4 % (cow, final, dino, capsule, scene 7); r3y
-                          // with the 96-entry XCD rings: cow -2.6 %, final -0.8 %, dino -0.9 %
-#endif
 // ART_POOL_RING: ring entries per wave.  128: two batches of 64, refilled when a batch's worth is free, so a round's
 // takers always find entries; 96 (default): refilled when at most 32 are left, so a round with more takers than
 // entries leaves the rest idle for that round.  Measured (r3m, scene 1, PMC per segment; XCD-contiguous rings): HBM
@@ -683,11 +659,8 @@ constexpr uint32_t kPathChunk = 256;
 #endif
 constexpr uint32_t kPoolRing = ART_POOL_RING;
 static_assert(kPoolRing >= 96 && kPoolRing <= 128, "a ring holds the unread part of one batch and a whole new one");
-// ART_RING_XCD (default 1): measured (r3m, 128-entry rings) HBM reads 11.3 -> 3.5 B per segment against the
+// XCD-contiguous rings: measured (r3m, 128-entry rings) HBM reads 11.3 -> 3.5 B per segment against the
 // block-major layout, Msamples/s unchanged
-#ifndef ART_RING_XCD
-#define ART_RING_XCD 1
-#endif
 constexpr uint32_t kXcds = 8;  // MI355X
 constexpr uint32_t kPoolWavesPerCu = 32;  // rings allocated per CU: the most waves a CU holds
 struct PoolRay {
@@ -703,12 +676,12 @@ struct RayRing {
     uint32_t base0, base1;  // first slot of the batch in ring half 0 / 1
     uint32_t cur, end;      // the wave's claimed slot chunk [cur, end)
     bool exhausted;         // every slot of the pass is in a batch
-    // wave w of block b: the rings of one XCD's blocks are contiguous (ART_RING_XCD; blocks go to the 8 XCDs round
+    // wave w of block b: the rings of one XCD's blocks are contiguous (blocks go to the 8 XCDs round
     // robin, block b to XCD b % 8), so each XCD's rings spread over all of its L2's sets instead of every block's
     // chunk landing on the same sets (block-major rings of one XCD lie 8 chunks apart: a power-of-two stride)
     __device__ __forceinline__ void init(void* pool, uint32_t block, uint32_t nblocks, uint32_t waves_per_block, uint32_t w) {
         uint32_t wave = block * waves_per_block + w;
-        if (ART_RING_XCD) {
+        {
             const uint32_t per_xcd = (nblocks + kXcds - 1) / kXcds;
             wave = ((block % kXcds) * per_xcd + block / kXcds) * waves_per_block + w;
         }
@@ -823,9 +796,6 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S0, PassG
     const uint32_t lane = __lane_id();
     const uint64_t below = (1ull << lane) - 1ull;
     const V3<R> bg = mk(S.bg[0], S.bg[1], S.bg[2]);
-#if !ART_RAY_POOL
-    uint32_t cur = 0, end = 0;  // this wave's claimed slots [cur, end): wave-uniform
-#endif
     bool busy = false, drained = false;
     uint32_t q = 0;
     int depth = 0;
@@ -834,13 +804,10 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S0, PassG
 #ifdef ART_STATS
     unsigned long long tm_load = 0, tm_trace = 0, tm_shade = 0, tm_app = 0, tm_prev = __builtin_amdgcn_s_memtime();
 #endif
-#if ART_RAY_POOL
     RayRing rr;
     rr.init(w.pool, blockIdx.x, gridDim.x, B / 64, threadIdx.x / 64);
     rr.start(s_g, s_cam, next_slot, lane);
-#endif
     for (;;) {
-#if ART_RAY_POOL
         // every idle lane takes the next ring entry (a padding slot of a partial tile leaves it idle a round)
         const uint64_t idle = __ballot(!busy && !drained);
         if (idle) {
@@ -854,43 +821,6 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S0, PassG
             }
             rr.advance(n, s_g, s_cam, next_slot, lane);
         }
-#else
-        // every idle lane takes the next slot of the wave's chunk (padding slots of partial tiles stay idle a round)
-        const uint64_t idle = __ballot(!busy && !drained);
-        if (idle) {
-            const uint32_t n = static_cast<uint32_t>(__popcll(idle));
-            const uint32_t rank = static_cast<uint32_t>(__popcll(idle & below));
-            uint32_t slot;
-            if (cur + n > end) {
-                uint32_t nb = 0;
-                if (lane == 0) nb = atomicAdd(next_slot, kPathChunk);
-                nb = __shfl(nb, 0);
-                const uint32_t left = end - cur;
-                slot = rank < left ? cur + rank : nb + (rank - left);
-                cur = nb + (n - left);
-                end = nb + kPathChunk;
-            } else {
-                slot = cur + rank;
-                cur += n;
-            }
-            if (!busy && !drained) {
-                if (slot >= g.P) {
-                    drained = true;
-                } else {
-                    int lx, ly;
-                    q = slot;
-                    // compiler barrier: the LDS camera/geometry loads stay here instead of being hoisted out of
-                    // the loop into ~40 long-lived registers
-                    __asm__ volatile("" ::: "memory");
-                    if (slot_pixel(s_g, slot - s_g.fd_npix.div(slot) * s_g.npix_pad, lx, ly)) {
-                        gen_ray(s_g, s_cam, q, lx, ly, st);
-                        busy = true;
-                        depth = 0;
-                    }
-                }
-            }
-        }
-#endif
         ART_TICK(tm_load);
         if (__ballot(busy) == 0) {
             if (__ballot(!drained) == 0) break;
@@ -906,10 +836,8 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S0, PassG
             if (hitw) h.mt = reinterpret_cast<const uint32_t*>(lds + kLdsOffRef)[h.obj >> 16] >> kLdsRefMatShift;
 #endif
         }
-#if ART_RAY_POOL
         // the ring stores of this round's refill (issued before the trace) are complete before the next round's loads
         __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
         ART_TICK(tm_trace);
         // the whole wave draws random_in_unit_sphere for its lambertian and metal hits (material.h:33, :55), which
         // scatter with it first; lights and the max_depth bounce draw nothing
@@ -952,24 +880,7 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S0, PassG
 // the material's scatter (the k_shade arithmetic, one switch over the material type instead of one launch per type),
 // so the RNG draws and every f64 operation are those of the wavefront kernels and images are bit-identical to them.
 // F / TF: the scene's primitive and texture features (smallest instantiation that covers them).
-#ifndef ART_LDS_MESH
-#define ART_LDS_MESH 1  // k_paths_g with the mesh arrays in LDS when they fit (LM)
-#endif
-#ifndef ART_LDS_PARTIAL
-#define ART_LDS_PARTIAL 1  // k_paths_g LM 2: the top BVH levels in LDS when the whole BVH does not fit
-#endif
 constexpr uint32_t kLdsPartialMinNodes = 64;
-#ifndef ART_SHARED_SHADE_G
-#define ART_SHARED_SHADE_G 1  // k_paths_g with noise/image textures: texture value and unit_vector once per wave
-#endif
-#ifndef ART_COOP_SPHERE_G
-// k_paths_g: the wave-cooperative random_in_unit_sphere of k_paths (coop_unit_sphere) for lambertian, metal and
-// isotropic hits: measured +0.8 % (cow), +1.3 % (Next-Week final), +2.4 % (dino 4096^2) (r3k)
-#define ART_COOP_SPHERE_G 1
-#endif
-#ifndef ART_LM1_PL
-#define ART_LM1_PL 1
-#endif
 #ifndef ART_PATHS_G_WAVES
 #define ART_PATHS_G_WAVES 3  // 3 waves per SIMD (<= 168 VGPRs): measured best over 2 and 4 (cow +22 %, final +18 %, dino +21 % over 2)
 #endif
@@ -991,18 +902,15 @@ __host__ __device__ constexpr size_t align128(size_t x) { return (x + 127u) & ~s
 // s16: 16-bit stack entries (F_CODE16 instantiations, device.h StackF)
 __host__ __device__ constexpr size_t paths_g_stack_bytes(uint32_t stack, int block, bool s16) { return (s16 ? 2u : 4u) * stack * block; }
 __host__ __device__ constexpr size_t paths_g_head_bytes(uint32_t stack, int block, bool s16) {  // stack, camera, pass geometry, jumps
-    return align16(paths_g_stack_bytes(stack, block, s16) + sizeof(CameraRec<double>) + sizeof(PassGeom)) + (ART_COOP_SPHERE_G ? kJumpBytes : 0);
+    return align16(paths_g_stack_bytes(stack, block, s16) + sizeof(CameraRec<double>) + sizeof(PassGeom)) + kJumpBytes;
 }
 // LM kernels also hold the world list and the object records (a few KiB): every segment walks them, and a prim
 // object's test otherwise waits on three dependent L1 loads (world slot -> object -> primitive)
 __host__ __device__ constexpr size_t paths_g_world_bytes(int32_t nworld, uint32_t n_objs) {
-    return align16(sizeof(int32_t) * static_cast<uint32_t>(nworld)) + (sizeof(ObjRec<double>) + sizeof(PrimRec80) + sizeof(ObjBox)) * n_objs;
+    return align16(sizeof(int32_t) * static_cast<uint32_t>(nworld)) + (sizeof(ObjRec<double>) + sizeof(PrimRec80)) * n_objs;
 }
-// LM 1's LDS copy of the triangle records: TriRec112 (ART_TRI112) or TriRec
-constexpr bool kLm1Pl = ART_LM1_PL && ART_NF_XOR;      // LM 1 reads its nodes through traverse's PL 2 path
-template <uint32_t F> constexpr bool kLm2CompactF = ART_LM2_COMPACT && ART_NEAR_FAR_G && (F & F_CODE16) != 0;  // device.h kCompact
-constexpr bool kLm1Tri112 = ART_TRI112 && kLm1Pl;        // ... and its leaf triangles from TriRec112 (traverse)
-constexpr size_t kLm1TriBytes = kLm1Tri112 ? sizeof(TriRec112<double>) : sizeof(TriRec<double>);
+// LM 1's LDS copy of the leaf triangle records: TriRec112 (plane precomputed, traverse's PL 2 path)
+constexpr size_t kLm1TriBytes = sizeof(TriRec112<double>);
 __host__ __device__ constexpr size_t paths_g_mesh_bytes(uint32_t n_nodes, uint32_t n_primrefs, uint32_t n_tris) {  // n_tris: 0 unless F_TRI
     return sizeof(BvhNode) * n_nodes + align16(sizeof(uint32_t) * n_primrefs) + kLm1TriBytes * n_tris;
 }
@@ -1010,10 +918,9 @@ template <uint32_t F, uint32_t TF, int LM>
 __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) void k_paths_g(DevScene<double> S0, PassGeom g, CameraRec<double> cam,
                                                                                      Work<double> w, uint32_t* next_slot) {
     using R = double;
-    // explicit-LDS node reads (traverse's PL path): LM 2 for its LDS part; LM 1 for every node with ART_LM1_PL (the
-    // XOR near/far addressing needs the explicit LDS addresses; through the LDS-inferred pointer it costs more adds)
-    constexpr int kLdsNodesPL = LM == 2 ? 1 : (LM == 1 && kLm1Pl) ? 2 : 0;
-    constexpr bool kLm2Compact = LM == 2 && kLm2CompactF<F>;
+    // explicit-LDS node reads (traverse's PL path): LM 2 for its LDS part; LM 1 for every node (the XOR near/far
+    // addressing needs the explicit LDS addresses; through the LDS-inferred pointer it costs more adds)
+    constexpr int kLdsNodesPL = LM == 2 ? 1 : LM == 1 ? 2 : 0;
     constexpr int B = LM ? kBlockM : kBlock;
     // dynamic LDS: [traversal stack: g.stack entries x B lanes (+ sentinel row)][camera][pass geometry][LM: nodes,
     // primrefs, triangles] -- as in k_paths, the camera and pass geometry are read from LDS where a path starts (as
@@ -1030,7 +937,7 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
         s_g = g;
     }
     [[maybe_unused]] JumpEntry* jt = reinterpret_cast<JumpEntry*>(smem + align16(paths_g_stack_bytes(g.stack, B, S16) + sizeof(CameraRec<double>) + sizeof(PassGeom)));
-    if (ART_COOP_SPHERE_G && threadIdx.x < static_cast<uint32_t>(kJumpEntries)) jt[threadIdx.x] = pcg_jump(3u * threadIdx.x);
+    if (threadIdx.x < static_cast<uint32_t>(kJumpEntries)) jt[threadIdx.x] = pcg_jump(3u * threadIdx.x);
     DevScene<double> S = S0;
     size_t lm_off = paths_g_head_bytes(g.stack, B, S16);  // LM: world list and objects, then the BVH arrays
     if constexpr (LM != 0) {
@@ -1042,34 +949,23 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
         uint8_t* pb = ob + sizeof(ObjRec<double>) * S0.n_objs;
         const uint4* ps = reinterpret_cast<const uint4*>(S0.obj_prims);
         for (uint32_t i = threadIdx.x; i < S0.n_objs * (sizeof(PrimRec80) / 16); i += B) reinterpret_cast<uint4*>(pb)[i] = ps[i];
-        uint8_t* bb = pb + sizeof(PrimRec80) * S0.n_objs;
-        const uint4* bs = reinterpret_cast<const uint4*>(S0.obj_box);
-        for (uint32_t i = threadIdx.x; i < S0.n_objs * (sizeof(ObjBox) / 16); i += B) reinterpret_cast<uint4*>(bb)[i] = bs[i];
         S.world = reinterpret_cast<const int32_t*>(wb);
         S.objs = reinterpret_cast<const ObjRec<double>*>(ob);
         S.obj_prims = reinterpret_cast<const PrimRec80*>(pb);
-        S.obj_box = reinterpret_cast<const ObjBox*>(bb);
         lm_off += paths_g_world_bytes(S0.nworld, S0.n_objs);
     }
-    if constexpr (LM != 0) lm_off = align128(lm_off);  // node addresses multiples of 128 (device.h ART_NF_XOR)
+    if constexpr (LM != 0) lm_off = align128(lm_off);  // node addresses multiples of 128 (device.h traverse: near/far planes by XOR)
     if constexpr (LM == 2) {  // the first n_lds_nodes nodes (the top levels of every BVH) into LDS
         BvhNode* m = reinterpret_cast<BvhNode*>(smem + lm_off);
         const uint4* s4 = reinterpret_cast<const uint4*>(S0.nodes);
         uint4* d4 = reinterpret_cast<uint4*>(m);
-        if constexpr (kLm2Compact) {  // 112-B nodes: the six planes, then the 16-B word holding the 16-bit codes
-            for (uint32_t i = threadIdx.x; i < S0.n_lds_nodes * 7u; i += B) {
-                const uint32_t n = i / 7u, c = i - n * 7u;
-                d4[i] = s4[n * 8u + (c < 6u ? c : 7u)];
-            }
-        } else {
-            for (uint32_t i = threadIdx.x; i < S0.n_lds_nodes * (sizeof(BvhNode) / 16); i += B) d4[i] = s4[i];
-        }
+        for (uint32_t i = threadIdx.x; i < S0.n_lds_nodes * (sizeof(BvhNode) / 16); i += B) d4[i] = s4[i];
         S.nodes_lds = static_cast<uint32_t>(reinterpret_cast<size_t>((__attribute__((address_space(3))) BvhNode*)m));
     }
     if constexpr (LM == 1) {
         uint8_t* m = smem + lm_off;
         const size_t nb = sizeof(BvhNode) * S0.n_nodes, pb = align16(sizeof(uint32_t) * S0.n_primrefs);
-        const size_t tb = (F & F_TRI) ? kLm1TriBytes * (ART_LEAF_TRIS ? S0.n_primrefs : S0.n_tris) : 0;
+        const size_t tb = (F & F_TRI) ? kLm1TriBytes * S0.n_primrefs : 0;
         auto copy = [&](uint8_t* dst, const void* src, size_t bytes) {
             const uint4* s4 = static_cast<const uint4*>(src);
             uint4* d4 = reinterpret_cast<uint4*>(dst);
@@ -1085,18 +981,8 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
         }
         S.primrefs = reinterpret_cast<const uint32_t*>(m + nb);
         if constexpr ((F & F_TRI) != 0) {
-#if ART_LEAF_TRIS
-            if constexpr (kLm1Tri112) {
-                copy(m + nb + pb, S0.leaf_tris112, tb);
-                S.leaf_tris112 = reinterpret_cast<const TriRec112<double>*>(m + nb + pb);
-            } else {
-                copy(m + nb + pb, S0.leaf_tris, tb);
-                S.leaf_tris = reinterpret_cast<const TriRec<double>*>(m + nb + pb);
-            }
-#else
-            copy(m + nb + pb, S0.tris, tb);
-            S.tris = reinterpret_cast<const TriRec<double>*>(m + nb + pb);
-#endif
+            copy(m + nb + pb, S0.leaf_tris112, tb);
+            S.leaf_tris112 = reinterpret_cast<const TriRec112<double>*>(m + nb + pb);
         }
     }
     const uint32_t P = g.P;
@@ -1113,10 +999,8 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
     unsigned long long segs = 0;
     // suspendable BVH traversals (ART_SUSPEND_LANES) where node fetches go to L2 (LM 0, 2); with the whole BVH in LDS
     // (LM 1) a traversal is short and suspending only adds rounds
-#ifndef ART_SUSPEND_LANES_LM1
-#define ART_SUSPEND_LANES_LM1 0  // LM 1 (BVH in LDS): thresholds 4-40 measured -5 % to -22 % on dino and the final scene
-#endif
-    constexpr int kSuspLanes = LM == 1 ? ART_SUSPEND_LANES_LM1 : ART_SUSPEND_LANES;
+    // (LM 1, the BVH in LDS: thresholds 4-40 measured -5 % to -22 % on dino and the final scene)
+    constexpr int kSuspLanes = LM == 1 ? 0 : ART_SUSPEND_LANES;
     constexpr bool SUSP = kSuspLanes > 0;
     TraceState<R> ts;  // the lane's segment trace, possibly suspended in a BVH
     bool in_trace = false;
@@ -1126,32 +1010,8 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
 #ifdef ART_STATS
     unsigned long long tm_load = 0, tm_trace = 0, tm_shade = 0, tm_app = 0, tm_prev = __builtin_amdgcn_s_memtime();
 #endif
-#if ART_RAY_POOL_G
-    RayRing rr;
-    rr.init(w.pool, blockIdx.x, gridDim.x, B / 64, threadIdx.x / 64);
-    rr.start(s_g, s_cam, next_slot, lane);
-#endif
     for (;;) {
         const uint64_t idle = __ballot(!busy && !drained);
-#if ART_RAY_POOL_G
-        if (idle) {  // the camera-ray ring, as in k_paths
-            const uint32_t n = static_cast<uint32_t>(__popcll(idle));
-            const uint32_t rank = static_cast<uint32_t>(__popcll(idle & below));
-            if (!busy && !drained) {
-                const int got = rr.take(rank, P, st, q);
-                drained = got == 2;
-                busy = got == 1;
-                depth = 0;
-#ifdef ART_TRACE
-                int lx = 0, ly = 0;
-                if (busy) slot_pixel(s_g, q - s_g.fd_npix.div(q) * s_g.npix_pad, lx, ly);
-                tracing = busy && static_cast<long long>(global_row(s_g, ly)) * s_g.W + lx == g_trace_pixel &&
-                          static_cast<long long>(s_g.sample_base + s_g.fd_npix.div(q)) == g_trace_sample;
-#endif
-            }
-            rr.advance(n, s_g, s_cam, next_slot, lane);
-        }
-#else
         if (idle) {
             const uint32_t n = static_cast<uint32_t>(__popcll(idle));
             const uint32_t rank = static_cast<uint32_t>(__popcll(idle & below));
@@ -1187,7 +1047,6 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
                 }
             }
         }
-#endif
         ART_TICK(tm_load);
         if (__ballot(busy) == 0) {
             if (__ballot(!drained) == 0) break;
@@ -1222,25 +1081,18 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
                 hitw = trace_world<R, F, B, false, kLdsNodesPL>(S, nullptr, st.ray, stk, st.rng, t, h);
             }
             susp = in_trace;  // suspended: nothing to shade this round
-#if ART_RAY_POOL_G
-            __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring stores before the next round's loads
-#endif
             ART_TICK(tm_trace);
             if (!susp && hitw) {
                 world_surface<R, F, (TF & TF_IMAGE) != 0>(S, h, st.ray, t, s);
                 mtype = S.mats[s.mat].type;
             }
         }
-#if ART_COOP_SPHERE_G
         // the whole wave draws random_in_unit_sphere for its lambertian, metal and isotropic hits (material.h:33, :55,
         // :129: each scatters with it first; metal's unit_vector draws nothing), as k_paths does
         const bool need = busy && !susp && hitw && (mtype == MAT_LAMBERTIAN || mtype == MAT_METAL || mtype == MAT_ISOTROPIC) &&
                           depth + 1 < max_depth;
         const V3<R> ps = coop_unit_sphere<R>(need, st.rng, jt);
         const V3<R>* pre = &ps;
-#else
-        const V3<R>* pre = nullptr;
-#endif
         if (busy) {
             bool cont = false;
             if (susp) {
@@ -1252,12 +1104,12 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
                            static_cast<int>(s.mat), h.prim, h.obj);
 #endif
                 const MatRec<R>& mat = S.mats[s.mat];
-                // ART_SHARED_SHADE_G, in kernels with noise or image textures (where a texture value is costly): the
+                // In kernels with noise or image textures (where a texture value is costly): the
                 // steps several materials take, once for the wave instead of once per material branch present -- the
                 // texture value (diffuse_light, lambertian, isotropic: no draws) and one unit_vector (of the sphere
                 // draw for lambertian, of the ray direction for metal and dielectric).  Measured +1.3 % on the
                 // Next-Week final; with solid / checker textures only (cow, dino) the longer live ranges cost 1.5-2 %.
-                constexpr bool kShared = ART_SHARED_SHADE_G && ART_COOP_SPHERE_G && (TF & (TF_NOISE | TF_IMAGE)) != 0;
+                constexpr bool kShared = (TF & (TF_NOISE | TF_IMAGE)) != 0;
                 V3<R> texc = mk(R(0), R(0), R(0)), uv = mk(R(0), R(0), R(0));
                 if constexpr (kShared) {
                     const bool scat = depth + 1 < max_depth;
@@ -1316,11 +1168,8 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
 #endif
 }
 
-// ART_CODE16_G: k_paths_g instantiations without F_MEDIA_G sort packed keys over 16-bit child codes (F_CODE16); a scene
+// k_paths_g instantiations without F_MEDIA_G sort packed keys over 16-bit child codes (F_CODE16); a scene
 // whose codes do not fit them (more than 32768 nodes or 8192 primitive references) takes the F_ALL kernel instead
-#ifndef ART_CODE16_G
-#define ART_CODE16_G 1
-#endif
 // ART_SPLIT_MESH (Makefile, SPLIT=1): the instantiations for meshes with solid/checker textures whose BVH is not all in
 // LDS (LM 0 / 2: cow) are compiled in kernels_mesh.o (ART_SPLIT_PATHS=3) with LLVM's iterative-maxocc scheduler
 // (MESH_SCHED): cow +1.3 % to +1.8 % over the default scheduler; dino's LM 1 kernel loses 0.9 % under it and the Next-Week
@@ -1328,7 +1177,7 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
 #ifndef ART_SPLIT_MESH
 #define ART_SPLIT_MESH 0
 #endif
-constexpr uint32_t kMeshG = kFeatMesh | (ART_CODE16_G ? F_CODE16 : 0u);
+constexpr uint32_t kMeshG = kFeatMesh | F_CODE16;
 #if ART_SPLIT_PATHS == 3
 template __global__ void k_paths_g<kMeshG, kTexBasic, 0>(DevScene<double>, PassGeom, CameraRec<double>, Work<double>, uint32_t*);
 template __global__ void k_paths_g<kMeshG, kTexBasic, 2>(DevScene<double>, PassGeom, CameraRec<double>, Work<double>, uint32_t*);
@@ -1689,7 +1538,7 @@ static std::vector<uint8_t> lds_scene_image(const FlatScene& f, uint32_t& nmov, 
         if (sp.flags & SPH_MOVING) {
             // the image's moving spheres span the unit shutter (every moving_sphere of the reference scenes,
             // scene_manager.cpp:34-35, :201): their centre fraction is the ray time itself (hit_lds_slot); and they
-            // move along y only (scene_manager.cpp:33), so the node boxes carry y motion planes (layout.h)
+            // move along y only (scene_manager.cpp:33): the image keeps one dy per leaf slot (layout.h)
             if (sp.t0 != 0.0 || sp.dt != 1.0 || sp.d[0] != 0.0 || sp.d[2] != 0.0) return img;
             ++nmov;
         }
@@ -1698,61 +1547,11 @@ static std::vector<uint8_t> lds_scene_image(const FlatScene& f, uint32_t& nmov, 
     for (const BvhNode& b : f.nodes)
         for (int c = 0; c < 4; ++c)
             if (b.child[c] < 0 && b.child[c] != kNodeEmpty && leaf_count(b.child[c]) > kLdsLeafMaxCount) return img;
-    // y extent of every child at t = 0 and t = 1 (f64, exact sphere bounds; the centre at ray time tm is
-    // c.y + tm * dy, so the lerp of the two extents bounds it, and the lerp of a union bounds the union of lerps)
-    struct YSpan {
-        double lo0, hi0, lo1, hi1;
-        void grow(const YSpan& o) {
-            lo0 = std::min(lo0, o.lo0); hi0 = std::max(hi0, o.hi0);
-            lo1 = std::min(lo1, o.lo1); hi1 = std::max(hi1, o.hi1);
-        }
-    };
-    const double dinf = std::numeric_limits<double>::infinity();
-    const YSpan kNone{dinf, -dinf, dinf, -dinf};
-    std::vector<std::array<YSpan, 4>> cspan(f.nodes.size());
-    std::vector<uint8_t> state(f.nodes.size(), 0);
-    std::function<YSpan(int32_t)> node_span = [&](int32_t n) -> YSpan {
-        if (state[n] == 1) throw std::runtime_error("bvh node cycle");
-        YSpan all = kNone;
-        if (state[n] == 2) {
-            for (const YSpan& s : cspan[n]) all.grow(s);
-            return all;
-        }
-        state[n] = 1;
-        const BvhNode& b = f.nodes[n];
-        for (int c = 0; c < 4; ++c) {
-            YSpan s = kNone;
-            if (b.child[c] >= 0) {
-                s = node_span(b.child[c]);
-            } else if (b.child[c] != kNodeEmpty) {
-                for (uint32_t k = 0; k < leaf_count(b.child[c]); ++k) {
-                    const SphereRec<double>& sp = f.spheres[primref_index(f.primrefs[leaf_first(b.child[c]) + k])];
-                    const double y1 = (sp.flags & SPH_MOVING) ? sp.c[1] + sp.d[1] : sp.c[1];
-                    s.grow(YSpan{sp.c[1] - sp.r, sp.c[1] + sp.r, y1 - sp.r, y1 + sp.r});
-                }
-            }
-            cspan[n][c] = s;
-            all.grow(s);
-        }
-        state[n] = 2;
-        return all;
-    };
-    if (ART_LDS_MOTION)
-        for (size_t n = 0; n < f.nodes.size(); ++n) node_span(static_cast<int32_t>(n));
     img.assign(kLdsImageBytes, 0);
     auto put = [&](uint32_t off, const void* v, size_t n) { std::memcpy(img.data() + off, v, n); };
-    const float finf = std::numeric_limits<float>::infinity();
-    auto f32_down = [&](double x) {
-        float v = static_cast<float>(x);
-        return static_cast<double>(v) > x ? std::nextafter(v, -finf) : v;
-    };
-    auto f32_up = [&](double x) {
-        float v = static_cast<float>(x);
-        return static_cast<double>(v) < x ? std::nextafter(v, finf) : v;
-    };
     for (size_t n = 0; n < f.nodes.size(); ++n) {
         const BvhNode& b = f.nodes[n];
-        float planes[6][4], motion[2][4];
+        float planes[6][4];
         const float* src[6] = {b.lox, b.hix, b.loy, b.hiy, b.loz, b.hiz};
         int32_t child[4];
         for (int c = 0; c < 4; ++c) {
@@ -1760,36 +1559,16 @@ static std::vector<uint8_t> lds_scene_image(const FlatScene& f, uint32_t& nmov, 
             // a child check, and the astronomically rare ray whose three slab times coincide there finds no primitives
             const bool empty = b.child[c] == kNodeEmpty;
             for (int j = 0; j < 6; ++j) planes[j][c] = empty ? kLdsEmptyBox : src[j][c];
-            motion[0][c] = motion[1][c] = 0.0f;
-            if (ART_LDS_MOTION && !empty) {
-                // y slab at time tm: [lo0 + tm * dlo, hi0 + tm * dhi] in f32, rounded outward and padded as
-                // conservative_box pads (bvh.cpp), so it holds the f64 spheres at every tm in [0, 1]
-                const YSpan& s = cspan[n][c];
-                const double m = std::max({std::fabs(s.lo0), std::fabs(s.hi0), std::fabs(s.lo1), std::fabs(s.hi1), s.hi0 - s.lo0, s.hi1 - s.lo1});
-                const float pad = 1e-6f * static_cast<float>(m) + 1e-30f;
-                const float lo0 = f32_down(s.lo0) - pad, lo1 = f32_down(s.lo1) - pad;
-                const float hi0 = f32_up(s.hi0) + pad, hi1 = f32_up(s.hi1) + pad;
-                planes[2][c] = lo0;
-                planes[3][c] = hi0;
-                motion[0][c] = f32_down(static_cast<double>(lo1) - static_cast<double>(lo0));  // lo0 + dlo <= lo1
-                motion[1][c] = f32_up(static_cast<double>(hi1) - static_cast<double>(hi0));
-            }
             // inner nodes by their byte offset in a plane (index * 16: device.h traverse), leaves as lds_leaf codes
             child[c] = empty ? kLdsEmptyChild : b.child[c] >= 0 ? b.child[c] * 16 : lds_leaf(leaf_first(b.child[c]), leaf_count(b.child[c]));
         }
-        // per axis: lo, hi, lo (layout.h kLdsNodePlanes), the child codes, then y motion: dlo, dhi, dlo
+        // per axis: lo, hi, lo (layout.h kLdsNodePlanes), then the child codes as int16
         const int order[9] = {0, 1, 0, 2, 3, 2, 4, 5, 4};
         const uint32_t nn = static_cast<uint32_t>(n);
         for (uint32_t j = 0; j < 9; ++j) put(kLdsOffNodes + (j * kLdsNodeCap + nn) * 16, planes[order[j]], 16);
-        if (ART_CHILD16) {
-            const int16_t c16[8] = {static_cast<int16_t>(child[0]), static_cast<int16_t>(child[1]), static_cast<int16_t>(child[2]),
-                                    static_cast<int16_t>(child[3]), 0, 0, 0, 0};
-            put(kLdsOffNodes + (kLdsNodePlaneChild * kLdsNodeCap + nn) * 16, c16, 16);
-        } else {
-            put(kLdsOffNodes + (kLdsNodePlaneChild * kLdsNodeCap + nn) * 16, child, 16);
-        }
-        if (ART_LDS_MOTION)
-            for (uint32_t j = 0; j < 3; ++j) put(kLdsOffNodes + ((kLdsNodePlaneMotion + j) * kLdsNodeCap + nn) * 16, motion[j == 1 ? 1 : 0], 16);
+        const int16_t c16[8] = {static_cast<int16_t>(child[0]), static_cast<int16_t>(child[1]), static_cast<int16_t>(child[2]),
+                                static_cast<int16_t>(child[3]), 0, 0, 0, 0};
+        put(kLdsOffNodes + (kLdsNodePlaneChild * kLdsNodeCap + nn) * 16, c16, 16);
     }
     // shading table: one entry per material (two for a checker of solid colours); anything else keeps the scene off
     // the fused variant (shade_ok = false), which shades from the global scene records instead
@@ -1816,12 +1595,9 @@ static std::vector<uint8_t> lds_scene_image(const FlatScene& f, uint32_t& nmov, 
         put(kLdsOffSph + (kLdsSlotCap + sl) * 16, p1, 16);
         put(kLdsOffInvR + sl * 8, &inv_r, 8);
         uint32_t code = idx | (f.mats[sp.mat].type << kLdsRefMatShift);
-        if (ART_LDS_DY_SLOT) {
-            const double dy = moving ? sp.d[1] : -0.0;
-            put(kLdsOffMov + sl * 8, &dy, 8);
-        }
+        const double dy = moving ? sp.d[1] : -0.0;
+        put(kLdsOffMov + sl * 8, &dy, 8);
         if (moving) {
-            if (!ART_LDS_DY_SLOT) put(kLdsOffMov + m * 8, &sp.d[1], 8);
             code |= (m + 1) << kLdsRefMovShift;
             ++m;
         }
@@ -1860,116 +1636,6 @@ static std::vector<uint8_t> lds_scene_image(const FlatScene& f, uint32_t& nmov, 
     return img;
 }
 
-// World-space cull boxes of the instances (layout.h ObjBox; device.h hit_object): each translate / rotate_y chain's
-// object-space bounds -- the root node's child boxes and hoisted primitives of a BVH, or a primitive's own extent --
-// carried through the chain's object-to-world maps (hittable.cpp:3-85: rotate_y's inverse x = c x' + s z',
-// z = -s x' + c z', then + offset) at the 8 corners in f64, rounded outward to f32 and padded by 1e-5 relative: far
-// more than the f64 rounding between a world-space ray and its object-space image, so a ray that misses the box
-// misses the instance.
-static void prim_bounds(const FlatScene& f, uint32_t ref, double lo[3], double hi[3]) {
-    const uint32_t i = primref_index(ref);
-    switch (primref_type(ref)) {
-        case PRIM_SPHERE: {  // a moving sphere over the unit shutter (its BVH boxes' range, bvh_node(list, 0, 1))
-            const auto& sp = f.spheres[i];
-            for (int a = 0; a < 3; ++a) {
-                double c0 = sp.c[a], c1 = sp.c[a];
-                if (sp.flags & SPH_MOVING) {
-                    c0 = sp.c[a] + ((0.0 - sp.t0) / sp.dt) * sp.d[a];
-                    c1 = sp.c[a] + ((1.0 - sp.t0) / sp.dt) * sp.d[a];
-                }
-                lo[a] = std::min(c0, c1) - std::fabs(sp.r);
-                hi[a] = std::max(c0, c1) + std::fabs(sp.r);
-            }
-            break;
-        }
-        case PRIM_TRIANGLE: {
-            const auto& t = f.tris[i];
-            for (int a = 0; a < 3; ++a) {
-                lo[a] = std::min({t.p[a], t.p[3 + a], t.p[6 + a]});
-                hi[a] = std::max({t.p[a], t.p[3 + a], t.p[6 + a]});
-            }
-            break;
-        }
-        case PRIM_RECT: {  // aarect.h:16-21: the plane coordinate padded by 1e-4
-            const auto& r = f.rects[i];
-            const int ia = r.axis == 2 ? 1 : 0, ib = r.axis == 0 ? 1 : 2, ik = r.axis == 0 ? 2 : r.axis == 1 ? 1 : 0;
-            lo[ia] = r.a0; hi[ia] = r.a1;
-            lo[ib] = r.b0; hi[ib] = r.b1;
-            lo[ik] = r.k - 1e-4; hi[ik] = r.k + 1e-4;
-            break;
-        }
-        default: {
-            const auto& b = f.boxes[i];
-            for (int a = 0; a < 3; ++a) { lo[a] = b.mn[a]; hi[a] = b.mx[a]; }
-        }
-    }
-}
-static std::vector<ObjBox> instance_cull_boxes(const FlatScene& f) {
-    std::vector<ObjBox> out(f.objs.size());
-    const double dinf = std::numeric_limits<double>::infinity();
-    for (size_t o = 0; o < f.objs.size(); ++o) {
-        out[o] = ObjBox{};
-        if (f.objs[o].kind != OBJ_TRANSLATE && f.objs[o].kind != OBJ_ROTATE_Y) continue;
-        std::vector<size_t> chain;  // outermost first
-        size_t in = o;
-        while (f.objs[in].kind == OBJ_TRANSLATE || f.objs[in].kind == OBJ_ROTATE_Y) {
-            chain.push_back(in);
-            in = static_cast<size_t>(f.objs[in].a);
-        }
-        double lo[3] = {dinf, dinf, dinf}, hi[3] = {-dinf, -dinf, -dinf};
-        auto grow = [&](const double l[3], const double h[3]) {
-            for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], l[a]); hi[a] = std::max(hi[a], h[a]); }
-        };
-        const ObjRec<double>& inner = f.objs[in];
-        if (inner.kind == OBJ_PRIM) {
-            double l[3], h[3];
-            prim_bounds(f, static_cast<uint32_t>(inner.a), l, h);
-            grow(l, h);
-        } else if (inner.kind == OBJ_BVH) {
-            const BvhNode& n = f.nodes[static_cast<size_t>(inner.a)];
-            for (int c = 0; c < 4; ++c)
-                if (n.child[c] != kNodeEmpty) {
-                    const double l[3] = {n.lox[c], n.loy[c], n.loz[c]}, h[3] = {n.hix[c], n.hiy[c], n.hiz[c]};
-                    grow(l, h);
-                }
-            if (inner.b != kNodeEmpty)
-                for (uint32_t k = 0; k < leaf_count(inner.b); ++k) {
-                    double l[3], h[3];
-                    prim_bounds(f, f.primrefs[leaf_first(inner.b) + k], l, h);
-                    grow(l, h);
-                }
-        } else {
-            continue;  // no box: the object is tested as before
-        }
-        if (!(lo[0] <= hi[0] && lo[1] <= hi[1] && lo[2] <= hi[2])) continue;
-        double wl[3] = {dinf, dinf, dinf}, wh[3] = {-dinf, -dinf, -dinf};
-        for (int k = 0; k < 8; ++k) {
-            double p[3] = {(k & 1) ? hi[0] : lo[0], (k & 2) ? hi[1] : lo[1], (k & 4) ? hi[2] : lo[2]};
-            for (size_t j = chain.size(); j-- > 0;) {  // innermost transform first
-                const ObjRec<double>& x = f.objs[chain[j]];
-                if (x.kind == OBJ_TRANSLATE) {
-                    for (int a = 0; a < 3; ++a) p[a] += x.p[a];
-                } else {  // object -> world of rotate_y (s = p[0], c = p[1])
-                    const double sn = x.p[0], cs = x.p[1], px = p[0], pz = p[2];
-                    p[0] = cs * px + sn * pz;
-                    p[2] = -sn * px + cs * pz;
-                }
-            }
-            for (int a = 0; a < 3; ++a) { wl[a] = std::min(wl[a], p[a]); wh[a] = std::max(wh[a], p[a]); }
-        }
-        ObjBox b{};
-        for (int a = 0; a < 3; ++a) {
-            const double m = std::max({std::fabs(wl[a]), std::fabs(wh[a]), wh[a] - wl[a]});
-            const double pad = 1e-5 * m + 1e-30;
-            b.lo[a] = std::nextafter(static_cast<float>(wl[a] - pad), -std::numeric_limits<float>::infinity());
-            b.hi[a] = std::nextafter(static_cast<float>(wh[a] + pad), std::numeric_limits<float>::infinity());
-        }
-        b.valid = std::isfinite(b.lo[0]) && std::isfinite(b.lo[1]) && std::isfinite(b.lo[2]) && std::isfinite(b.hi[0]) &&
-                  std::isfinite(b.hi[1]) && std::isfinite(b.hi[2]);
-        out[o] = b;
-    }
-    return out;
-}
 
 template <class R>
 static void build_device_scene(const FlatScene& f, DeviceScene<R>& ds) {
@@ -2080,6 +1746,10 @@ static void build_device_scene(const FlatScene& f, DeviceScene<R>& ds) {
         }
         for (const auto& o : f.objs)
             if (o.kind == OBJ_BVH && o.b != kNodeEmpty) ok = ok && leaf16_ok(leaf_first(o.b), leaf_count(o.b));
+        // ART_CODE16=0 (environment, read per upload; tests): take the 32-bit-code kernels as a scene whose codes do
+        // not fit would (a parity probe of that path on scenes that fit)
+        const char* force = std::getenv("ART_CODE16");
+        if (force && std::atoi(force) == 0) ok = false;
         ds.codes16 = ok;
         ds.view.nodes = ds.upload(nodes);
     }
@@ -2100,7 +1770,6 @@ static void build_device_scene(const FlatScene& f, DeviceScene<R>& ds) {
                       sizeof(RectRec<R>) <= sizeof(PrimRec80) && sizeof(BoxRec<R>) <= sizeof(PrimRec80), "PrimRec80 holds every record");
         ds.view.obj_prims = ds.upload(op);
     }
-    ds.view.obj_box = ds.upload(instance_cull_boxes(f));
     ds.view.world = ds.upload(f.world);
     ds.view.mats = ds.upload(mats);
     ds.view.texs = ds.upload(texs);
@@ -2306,21 +1975,16 @@ static void launch_paths_g_ft(int num_cu, hipStream_t st, const DevScene<double>
                               const Work<double>& w, uint32_t* next_slot) {
     // g.stack = stack_rows: sentinel + entries + spare row
     const size_t lm_head = paths_g_head_bytes(g.stack, kBlockM, (F & F_CODE16) != 0) + paths_g_world_bytes(S.nworld, S.n_objs);
-    const size_t lds_m = align128(lm_head) + paths_g_mesh_bytes(S.n_nodes, S.n_primrefs, (F & F_TRI) ? (ART_LEAF_TRIS ? S.n_primrefs : S.n_tris) : 0u);
-#if ART_LDS_MESH
+    const size_t lds_m = align128(lm_head) + paths_g_mesh_bytes(S.n_nodes, S.n_primrefs, (F & F_TRI) ? S.n_primrefs : 0u);
     if (S.n_nodes > 0 && lds_m <= kPathsGLdsCap) {
         const int blocks = blocks_per_cu(reinterpret_cast<const void*>(k_paths_g<F, TF, 1>), kBlockM, lds_m) * num_cu;
         check_ring_waves(blocks, kBlockM, num_cu);
         hipLaunchKernelGGL((k_paths_g<F, TF, 1>), dim3(blocks), dim3(kBlockM), lds_m, st, S, g, cam, w, next_slot);
         return;
     }
-#else
-    (void)lds_m;
-#endif
-#if ART_LDS_PARTIAL
     // too large for LM 1: as many of the first (top-level) nodes as fit beside the stacks
     const size_t head = align128(lm_head);
-    const size_t node_bytes = kLm2CompactF<F> ? kLdsCompactNode : sizeof(BvhNode);
+    const size_t node_bytes = sizeof(BvhNode);
     const uint32_t fit = head < kPathsGLdsCap ? static_cast<uint32_t>((kPathsGLdsCap - head) / node_bytes) : 0u;
     if (S.n_nodes > 0 && fit >= kLdsPartialMinNodes) {
         DevScene<double> SP = S;
@@ -2336,7 +2000,6 @@ static void launch_paths_g_ft(int num_cu, hipStream_t st, const DevScene<double>
         hipLaunchKernelGGL((k_paths_g<F, TF, 2>), dim3(blocks), dim3(kBlockM), lds_p, st, SP, g, cam, w, next_slot);
         return;
     }
-#endif
     const size_t lds = paths_g_head_bytes(g.stack, kBlock, (F & F_CODE16) != 0);
     const int blocks = blocks_per_cu(reinterpret_cast<const void*>(k_paths_g<F, TF, 0>), kBlock, lds) * num_cu;
     check_ring_waves(blocks, kBlock, num_cu);
@@ -2344,9 +2007,12 @@ static void launch_paths_g_ft(int num_cu, hipStream_t st, const DevScene<double>
 }
 static void launch_paths_g(uint32_t feat, bool tex_basic, bool codes16, int num_cu, hipStream_t st, const DevScene<double>& S, const PassGeom& g,
                            const CameraRec<double>& cam, const Work<double>& w, uint32_t* next_slot) {
-    constexpr uint32_t C = ART_CODE16_G ? F_CODE16 : 0u;
-    if (C && !codes16 && (feat & F_MEDIA_G) == 0) {
-        launch_paths_g_ft<F_ALL, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
+    constexpr uint32_t C = F_CODE16;
+    if (!codes16 && (feat & F_MEDIA_G) == 0) {
+        // 32-bit child codes (more than 32768 nodes or 8192 primitive references): the instantiations without F_CODE16,
+        // the triangle-free one when the scene has no triangles (no triangle code in the kernel)
+        if (feat & F_TRI) launch_paths_g_ft<F_ALL, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
+        else launch_paths_g_ft<F_ALL & ~F_TRI, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
     } else if ((feat & ~kFeatSpheres) == 0) {
         if (tex_basic) launch_paths_g_ft<kFeatSpheres | C, kTexBasic>(num_cu, st, S, g, cam, w, next_slot);
         else launch_paths_g_ft<kFeatSpheres | C, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
@@ -2477,7 +2143,7 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     const size_t o_acc = off; off += al(sizeof(double) * 3 * local_pix);
     const size_t o_rgb = off; off += al(3 * local_pix);
     const size_t o_qsum = off; off += images ? al(sizeof(double) * 3 * local_pix) : 0;  // parallel_images quarter sums
-    const size_t o_pool = off; off += (variant == EXT_MEGA || (ART_RAY_POOL_G && variant == EXT_MEGA_G)) ? al(sizeof(PoolRay) * kPoolRing * kPoolWavesPerCu * static_cast<size_t>(I.num_cu)) : 0;
+    const size_t o_pool = off; off += (variant == EXT_MEGA) ? al(sizeof(PoolRay) * kPoolRing * kPoolWavesPerCu * static_cast<size_t>(I.num_cu)) : 0;
     // adaptive mode: int work frame, pixel list (<= 80 of every 144 pixels per level), square flags, list counter
     const bool adapt_ws = (p.flags & RT_ADAPTIVE) != 0;
     const size_t nsq_ws = adapt_ws ? local_pix / (kBig * kBig) : 0;

@@ -44,7 +44,7 @@ struct TriRec {         // triangle.h: pt1, pt2, pt3
     uint32_t mat;
     uint32_t pad;
 };
-// A leaf triangle with its plane precomputed on the host by the device's own operations (ART_TRI112: the LM 1 kernels'
+// A leaf triangle with its plane precomputed on the host by the device's own operations (the LM 1 kernels'
 // LDS copy): n = cross(pt2 - pt1, pt3 - pt1) and dd = -dot(n, pt1), triangle.h:30-41
 template <class R>
 struct TriRec112 {
@@ -107,20 +107,10 @@ constexpr int kMaxStackDepth = 64;   // per-lane LDS traversal stack entries (si
 // node and sphere fetches of the traversal never touch the vector-memory (TA/L1) path that bounds the global variant.
 // Every plane is an array of 16-B entries, so lanes fetching different nodes/spheres spread over the 16 four-bank slots
 // of the ds_read_b128 bank row, and the plane strides are compile-time (DS immediate offsets, no address VALU).
-// BVH4 nodes: 10 (13) planes -- per axis (lo, hi, lo again) as float4, so the far plane of either direction sign is one
-// plane above the near one (an immediate DS offset); child codes as int4; then, with ART_LDS_MOTION, the motion planes of y (dlo, dhi, dlo):
-// the image's spheres move along y only (the reference's moving spheres, scene_manager.cpp:33), so a child's y slab at
-// ray time tm is [lo + tm * dlo, hi + tm * dhi] -- the lerp of its t = 0 and t = 1 boxes, which bounds every linearly
-// moving sphere below it at tm -- instead of the union over the shutter (a moving sphere's box is 1.6x taller)
-// ART_LDS_MOTION (default 0): measured on the random-spheres scene -- 7.6 % fewer node visits and 6.3 % fewer leaf
-// tests, but the two extra plane loads and FMAs per visit (and 21 more VGPR spills at k_paths' 128-VGPR cap) cost
-// more: -1.5 %.  Off, the nodes keep the 10 planes of the union boxes over the shutter.
-#ifndef ART_CHILD16
-#define ART_CHILD16 1  // the child plane holds a node's four codes as int16 in its first 8 bytes (else int32 x 4)
-#endif
-#ifndef ART_LDS_MOTION
-#define ART_LDS_MOTION 0
-#endif
+// BVH4 nodes: 10 planes -- per axis (lo, hi, lo again) as float4, so the far plane of either direction sign is one
+// plane above the near one (an immediate DS offset); then the four child codes as int16 in the first 8 bytes of the
+// child plane.  The boxes are the union over the shutter (y motion planes, the lerp of a child's t = 0 and t = 1 boxes,
+// measured 7.6 % fewer node visits but -1.5 % overall: two more loads and FMAs per visit, 21 more VGPR spills).
 // LDS node capacity: the random scene's tree without the hoisted ground sphere has 259 nodes (greedy collapse, bvh.cpp;
 // 223 with ART_BVH_COLLAPSE=1).  Every plane stays a multiple of 256 B (bank 0); the 7.5 KiB saved against a 320 cap
 // leave room for deeper traversal stacks (the optimal collapse's tree needs 18 entries instead of 15)
@@ -128,23 +118,17 @@ constexpr int kMaxStackDepth = 64;   // per-lane LDS traversal stack entries (si
 #define ART_LDS_NODE_CAP 272
 #endif
 constexpr uint32_t kLdsNodeCap = ART_LDS_NODE_CAP;
-constexpr uint32_t kLdsNodePlanes = ART_LDS_MOTION ? 13 : 10;
+constexpr uint32_t kLdsNodePlanes = 10;
 constexpr uint32_t kLdsNodePlaneChild = 9;
-constexpr uint32_t kLdsNodePlaneMotion = 10;  // dlo y, dhi y, dlo y
 constexpr uint32_t kLdsSlotCap = 1024;  // leaf slots (= primref array entries): 2 planes (cx, cy), (cz, r) as double2
 constexpr uint32_t kLdsMovCap = 512;    // moving spheres (unit shutter, y motion)
-// ART_LDS_DY_SLOT (default 1): the y motion is a plane of one f64 dy per leaf slot, -0.0 for a static sphere
-// (c.y + tm * -0 == c.y for every c.y and tm >= 0, -0 included), so a leaf test loads it beside the sphere planes and
-// runs one branch-free sequence; 0: one dy per moving sphere, reached through the slot's code (a load that waits
-// on the code load, inside a branch)
-#ifndef ART_LDS_DY_SLOT
-#define ART_LDS_DY_SLOT 1
-#endif
+// The y motion is a plane of one f64 dy per leaf slot, -0.0 for a static sphere (c.y + tm * -0 == c.y for every c.y
+// and tm >= 0, -0 included), so a leaf test loads it beside the sphere planes and runs one branch-free sequence
 constexpr uint32_t kLdsOffNodes = 0;
 constexpr uint32_t kLdsOffSph = kLdsOffNodes + kLdsNodePlanes * kLdsNodeCap * 16;
 constexpr uint32_t kLdsOffMov = kLdsOffSph + 2 * kLdsSlotCap * 16;
 // u32 per slot: sphere index (19 bits) | (moving index + 1) << 19 (10 bits) | material type << 29 (3 bits)
-constexpr uint32_t kLdsOffRef = kLdsOffMov + (ART_LDS_DY_SLOT ? kLdsSlotCap : kLdsMovCap) * 8;
+constexpr uint32_t kLdsOffRef = kLdsOffMov + kLdsSlotCap * 8;
 // Shading table (fused variant): u16 per slot = material entry e | kLdsMatChecker, and kLdsMatCap 32-B entries
 // (c.x, c.y), (c.z, param): lambertian / diffuse_light colour (a checker of two solid colours takes entries e = even,
 // e + 1 = odd), metal albedo + fuzz, dielectric (-, -, -, ir).  A hit is then shaded without any global load.
@@ -185,15 +169,6 @@ struct ObjRec {
     R p[4];         // TRANSLATE: offset xyz; ROTATE_Y: sin, cos; MEDIUM: neg_inv_density
 };
 constexpr int kMaxXformChain = 2;  // translate(rotate_y(X)) is the deepest chain in the reference scenes
-// World-space cull box of an instance (translate / rotate_y chain, hittable.cpp:3-85), indexed like objs: the
-// f32-rounded-outward, padded box of its transformed object-space bounds (DevScene::obj_box).  A ray that misses it
-// cannot hit the instance, so the object-space transform and traversal are skipped (valid == 0: no box, test the object).
-struct alignas(16) ObjBox {
-    float lo[3];
-    uint32_t valid;
-    float hi[3];
-    uint32_t pad;
-};
 // Scene features: kernels are instantiated for feature subsets (spheres only / meshes / everything).
 // F_MEDIA: constant_medium objects; F_MEDIA_G: one of them has a boundary that is not a sphere primitive (its two
 // boundary hits are whole object traversals; a sphere boundary is one quadratic, device.h hit_medium)

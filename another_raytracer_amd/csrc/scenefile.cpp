@@ -131,7 +131,12 @@ void validate(const std::string& path, FlatScene& f) {
         int kids = 0, cs = 0, cd = 0;
         for (int c = 0; c < 4; ++c) {
             const int32_t ch = n.child[c];
-            if (ch == kNodeEmpty) continue;
+            if (ch == kNodeEmpty) {
+                // an empty slot must carry a box no ray enters (lo > hi on every axis: bvh.cpp writes +FLT_MAX /
+                // -FLT_MAX): the traversal's key tests have no per-child empty check (device.h slab4_nf, slab4_packed_nf)
+                if (!(n.lox[c] > n.hix[c] && n.loy[c] > n.hiy[c] && n.loz[c] > n.hiz[c])) bad(path, "empty BVH slot with an enterable box");
+                continue;
+            }
             ++kids;
             if (ch >= 0) {
                 if (static_cast<size_t>(ch) <= k || static_cast<size_t>(ch) >= nn) bad(path, "BVH child out of range");

@@ -111,7 +111,22 @@ def test_tampered_header_and_payload_are_refused(tmp_path):
         off = h.offset[5] - start + 96  # node 0's child[0] (BvhNode: 6 x float4 planes, then int32 child[4])
         pay[off:off + 4] = (0).to_bytes(4, "little")  # node 0 -> node 0: a cycle the GPU would walk forever
 
+    def empty_slot_box(h, pay):
+        # the first node with an empty child slot gets a finite box there (lox..hiz: 6 x float4, child[4] at +96)
+        import struct
+        base = h.offset[5] - start
+        for n in range(h.count[5]):
+            o = base + 128 * n
+            ch = struct.unpack_from("<4i", pay, o + 96)
+            if -1 in ch:
+                c = ch.index(-1)
+                for plane, v in enumerate((0.0, 1.0, 0.0, 1.0, 0.0, 1.0)):
+                    struct.pack_into("<f", pay, o + 16 * plane + 4 * c, v)
+                return
+        raise AssertionError("no empty slot in scene 1's BVH")
+
     cases = {
+        "empty slot box": with_payload(empty_slot_box),
         "offset wraps": with_header(offset=(0, 2 ** 64 - 64)),
         "count wraps": with_header(count=(5, 2 ** 61)),
         "count past end": with_header(count=(12, h0.count[12] + 10 ** 6)),
