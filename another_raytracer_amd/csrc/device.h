@@ -576,7 +576,7 @@ __device__ __forceinline__ bool hit_lds_slot(const uint8_t* lds, uint32_t slot, 
 // Divergence statistics (diagnostic builds only): [0] node-loop wave iterations, [1] node visits (lane sum), [2] leaf-
 // loop wave iterations, [3] leaf tests (lane sum), [4] outer-loop wave iterations, [5] outer iterations (lane sum),
 // [6] traversals, [7] hit_sphere tests with disc >= 0.
-__device__ unsigned long long g_art_stats[24];
+__device__ unsigned long long g_art_stats[32];
 __device__ __forceinline__ void stat_wave(int k) {
     const uint64_t m = __ballot(true);
     if (static_cast<int>(__lane_id()) == __ffsll(static_cast<long long>(m)) - 1) atomicAdd(&g_art_stats[k], 1ull);
@@ -1267,8 +1267,8 @@ __device__ __forceinline__ void set_face_normal(Surf<R>& s, const Ray<R>& r, V3<
     s.n = s.ff ? outward : -outward;
 }
 template <class R, bool UV = true>
-__device__ __forceinline__ void rect_surface(Surf<R>& s, int axis, R a0, R a1, R b0, R b1, R k, const Ray<R>& r, R t) {
-    if (UV) {  // u, v feed image textures only
+__device__ __forceinline__ void rect_surface(Surf<R>& s, int axis, R a0, R a1, R b0, R b1, R k, const Ray<R>& r, R t, bool need_uv = true) {
+    if (UV && need_uv) {  // u, v feed image textures only (materials without MATF_NEEDS_UV skip the two divisions)
         const int ia = axis == 2 ? 1 : 0;
         const int ib = axis == 0 ? 1 : 2;
         const R x = comp(r.o, ia) + t * comp(r.d, ia);
@@ -1318,7 +1318,7 @@ __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref,
             const V3<R> p = r.o + t * r.d;
             s.p = p;
             set_face_normal(s, r, N);
-            if (UV) {  // barycentric u, v feed image textures only (texture.h:135-154)
+            if (UV && (S.mats[tr.mat].flags & MATF_NEEDS_UV)) {  // barycentric u, v feed image textures only (texture.h:135-154)
                 const R u = dot(N, cross(p3 - p2, p - p2));
                 const R v = dot(N, cross(p1 - p3, p - p3));
                 s.u = u / len2(N);
@@ -1333,7 +1333,7 @@ __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref,
         case PRIM_RECT: {
             if (!(F & F_RECT)) break;
             const RectRec<R>& q = S.rects[idx];
-            rect_surface<R, UV>(s, static_cast<int>(q.axis), q.a0, q.a1, q.b0, q.b1, q.k, r, t);
+            rect_surface<R, UV>(s, static_cast<int>(q.axis), q.a0, q.a1, q.b0, q.b1, q.k, r, t, (S.mats[q.mat].flags & MATF_NEEDS_UV) != 0);
             s.mat = q.mat;
             break;
         }
@@ -1343,7 +1343,7 @@ __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref,
             int axis;
             R a0, a1, b0, b1, k;
             box_face(b, static_cast<int>(face), axis, a0, a1, b0, b1, k);
-            rect_surface<R, UV>(s, axis, a0, a1, b0, b1, k, r, t);
+            rect_surface<R, UV>(s, axis, a0, a1, b0, b1, k, r, t, (S.mats[b.mat].flags & MATF_NEEDS_UV) != 0);
             s.mat = b.mat;
             break;
         }
@@ -1412,6 +1412,15 @@ __device__ __forceinline__ R perlin_noise(const PerlinRec<R>& pn, V3<R> p) {  //
     const R u = p.x - floor(p.x), v = p.y - floor(p.y), w = p.z - floor(p.z);
     const int i = static_cast<int>(floor(p.x)), j = static_cast<int>(floor(p.y)), k = static_cast<int>(floor(p.z));
     const R uu = u * u * (R(3) - R(2) * u), vv = v * v * (R(3) - R(2) * v), ww = w * w * (R(3) - R(2) * w);
+    // perlin_interp's weights i*uu + (1-i)*(1-uu) with i in {0, 1}: u, v, w lie in [+0, 1), so uu, vv, ww and 1 - uu,
+    // ... are >= +0 and finite; 0 * x is then +0, 1 * x is x and x + (+0) is x -- the weight is exactly 1 - uu (i = 0)
+    // or uu (i = 1), and u - 0 is exactly u.  Folding them (the compiler may not: 0 * x is not +0 for every double)
+    // leaves the same products and sums in the same order.
+    const R wx[2] = {R(1) - uu, uu}, wy[2] = {R(1) - vv, vv}, wz[2] = {R(1) - ww, ww};
+    const R dx[2] = {u, u - R(1)}, dy[2] = {v, v - R(1)}, dz[2] = {w, w - R(1)};
+    const int px[2] = {pn.perm[0][i & 255], pn.perm[0][(i + 1) & 255]};
+    const int py[2] = {pn.perm[1][j & 255], pn.perm[1][(j + 1) & 255]};
+    const int pz[2] = {pn.perm[2][k & 255], pn.perm[2][(k + 1) & 255]};
     R accum = R(0);
 #pragma unroll
     for (int a = 0; a < 2; a++)
@@ -1419,11 +1428,8 @@ __device__ __forceinline__ R perlin_noise(const PerlinRec<R>& pn, V3<R> p) {  //
         for (int b = 0; b < 2; b++)
 #pragma unroll
             for (int c = 0; c < 2; c++) {
-                const int idx = pn.perm[0][(i + a) & 255] ^ pn.perm[1][(j + b) & 255] ^ pn.perm[2][(k + c) & 255];
-                const V3<R> g = ld3(pn.ranvec[idx]);
-                const V3<R> wv = mk(u - R(a), v - R(b), w - R(c));
-                accum += (R(a) * uu + R(1 - a) * (R(1) - uu)) * (R(b) * vv + R(1 - b) * (R(1) - vv)) *
-                         (R(c) * ww + R(1 - c) * (R(1) - ww)) * dot(g, wv);
+                const V3<R> g = ld3(pn.ranvec[px[a] ^ py[b] ^ pz[c]]);
+                accum += wx[a] * wy[b] * wz[c] * dot(g, mk(dx[a], dy[b], dz[c]));
             }
     return accum;
 }
@@ -1469,11 +1475,17 @@ __device__ __forceinline__ V3<R> tex_value(const DevScene<R>& S, int32_t ti, R u
             continue;
         }
         if ((TF & TF_NOISE) && t.type == TEX_NOISE) {
+            ART_STAT_WAVE(28);
+            ART_STAT_LANE(29);
             const R n = perlin_noise(S.perlins[t.perlin], t.scale * p);
             const R h = (R(1) + n) * R(0.5);
             return mk(h, h, h);
         }
-        if ((TF & TF_IMAGE) && t.type == TEX_IMAGE) return image_value(S, t.image, u, v);
+        if ((TF & TF_IMAGE) && t.type == TEX_IMAGE) {
+            ART_STAT_WAVE(30);
+            ART_STAT_LANE(31);
+            return image_value(S, t.image, u, v);
+        }
         if ((TF & TF_IMAGE) && t.type == TEX_BARY_IMAGE) {
             const R w = R(1) - u - v;
             return image_value(S, t.image, u * t.uv[0] + v * t.uv[2] + w * t.uv[4], u * t.uv[1] + v * t.uv[3] + w * t.uv[5]);

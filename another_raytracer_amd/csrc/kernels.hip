@@ -1009,6 +1009,7 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
 #endif
 #ifdef ART_STATS
     unsigned long long tm_load = 0, tm_trace = 0, tm_shade = 0, tm_app = 0, tm_prev = __builtin_amdgcn_s_memtime();
+    unsigned long long tm_surf = 0, tm_coop = 0, tm_tex = 0;  // the shading phase split (k_paths_g)
 #endif
     for (;;) {
         const uint64_t idle = __ballot(!busy && !drained);
@@ -1087,12 +1088,14 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
                 mtype = S.mats[s.mat].type;
             }
         }
+        ART_TICK(tm_surf);
         // the whole wave draws random_in_unit_sphere for its lambertian, metal and isotropic hits (material.h:33, :55,
         // :129: each scatters with it first; metal's unit_vector draws nothing), as k_paths does
         const bool need = busy && !susp && hitw && (mtype == MAT_LAMBERTIAN || mtype == MAT_METAL || mtype == MAT_ISOTROPIC) &&
                           depth + 1 < max_depth;
         const V3<R> ps = coop_unit_sphere<R>(need, st.rng, jt);
         const V3<R>* pre = &ps;
+        ART_TICK(tm_coop);
         if (busy) {
             bool cont = false;
             if (susp) {
@@ -1120,6 +1123,7 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
                 }
                 const V3<R>* texp = kShared ? &texc : nullptr;
                 const V3<R>* uvp = kShared ? &uv : nullptr;
+                ART_TICK(tm_tex);
                 if (mat.type == MAT_LIGHT) {  // material.h:114-116; diffuse_light never scatters
                     st.L = st.L + st.T * (texp ? *texp : tex_value<R, TF>(S, mat.tex, s.u, s.v, s.p));
                 } else if (depth + 1 < max_depth) {
@@ -1164,6 +1168,9 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
         atomicAdd(&g_art_stats[9], tm_trace);
         atomicAdd(&g_art_stats[10], tm_shade);
         atomicAdd(&g_art_stats[11], tm_app);
+        atomicAdd(&g_art_stats[24], tm_surf);
+        atomicAdd(&g_art_stats[25], tm_coop);
+        atomicAdd(&g_art_stats[26], tm_tex);
     }
 #endif
 }
@@ -2301,7 +2308,7 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     HIP_OK(hipGetLastError());
 #ifdef ART_STATS
     {
-        unsigned long long st[24] = {0};
+        unsigned long long st[32] = {0};
         HIP_OK(hipStreamSynchronize(stream));
         HIP_OK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_art_stats), sizeof st));
         std::fprintf(stderr, "ART_STATS node_w %llu node_l %llu (util %.3f) leaf_w %llu leaf_l %llu (util %.3f) outer_w %llu outer_l %llu (util %.3f) "
@@ -2314,8 +2321,13 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
         if (st[15] + st[17] + st[19] + st[21] > 0)
             std::fprintf(stderr, "ART_STATS leaf tests by type (lane tests, wave iterations running it): box %llu %llu sphere %llu %llu triangle %llu %llu rect %llu %llu\n",
                          st[15], st[16], st[17], st[18], st[19], st[20], st[21], st[22]);
-        const double tt = double(st[8] + st[9] + st[10] + st[11]);
-        if (tt > 0) std::fprintf(stderr, "ART_STATS cycles: load/claim %.3f trace %.3f shade %.3f append/store %.3f\n", st[8] / tt, st[9] / tt, st[10] / tt, st[11] / tt);
+        const double tt = double(st[8] + st[9] + st[10] + st[11] + st[24] + st[25] + st[26]);
+        if (tt > 0)
+            std::fprintf(stderr, "ART_STATS cycles: load/claim %.3f trace %.3f shade %.3f append/store %.3f (k_paths_g shading split: surface %.3f "
+                         "coop-sphere %.3f texture+unit %.3f scatter %.3f)\n",
+                         st[8] / tt, st[9] / tt, (st[10] + st[24] + st[25] + st[26]) / tt, st[11] / tt, st[24] / tt, st[25] / tt, st[26] / tt, st[10] / tt);
+        if (st[28] + st[30] > 0)
+            std::fprintf(stderr, "ART_STATS texture evaluations (wave iterations, lanes): noise %llu %llu image %llu %llu\n", st[28], st[29], st[30], st[31]);
         std::memset(st, 0, sizeof st);
         HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(g_art_stats), st, sizeof st));
     }

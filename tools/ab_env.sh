@@ -13,7 +13,7 @@ for round in 1 2; do
     lib="${v%%@*}"
     envs=""
     [ "$lib" != "$v" ] && envs="${v#*@}"
-    timeout -k 10 120 env ART_LIB=$PWD/another_raytracer_amd/$lib ${envs//,/ } python bench.py --steps 2 --warmup 1 --no-cpu-baseline $ARGS \
+    timeout -k 10 120 env ART_LIB=$PWD/another_raytracer_amd/$lib ${envs//,/ } python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-parity $ARGS \
       > gpurun_out/abe_${i}_$round.log 2>&1
     rc=$?
     echo "$v round $round rc=$rc $(grep -o '"value": [0-9.]*' gpurun_out/abe_${i}_$round.log | head -1)"

@@ -4,7 +4,7 @@
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
 export TMPDIR=/tmp
 TAG=${TAG:-r1}; SPP=${SPP:-64}; SCENE=${SCENE:-1}; PREC=${PREC:-f64}
-ARGS="--steps 1 --warmup 0 --no-cpu-baseline --no-profile --spp $SPP --scene $SCENE --precision $PREC"
+ARGS="--steps 1 --warmup 0 --no-cpu-baseline --no-parity --no-profile --spp $SPP --scene $SCENE --precision $PREC"
 run() { local t=$1; shift; timeout -k 10 "$t" "$@"; local rc=$?; echo "== rc=$rc : $*"; if [ $rc -ne 0 ]; then exit $rc; fi; }
 mkdir -p gpurun_out
 rocprofv3 -L > gpurun_out/pmc_list_$TAG.txt 2>&1 || true
