@@ -4,7 +4,7 @@
 // _run_parallel_stripes).  Here one host thread per GPU renders the row-interleaved band partition of its device
 // (band b of band_rows rows goes to GPU b mod N: sky and object rows spread evenly), each GPU packs its rows into one
 // device buffer, and a single RCCL gather (ncclGather, rccl.h) moves them over xGMI to the first device, where an
-// unpack kernel writes every row to its place in the frame.  The RCCL communicator (ncclCommInitAll) and the per-device
+// unpack kernel writes every row to its place in the frame.  The RCCL communicators (non-blocking, one group) and the per-device
 // scene uploads are made once, when the MultiRenderer is built.
 #pragma once
 #include <cstddef>

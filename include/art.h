@@ -204,7 +204,7 @@ void rt_image_free(uint8_t* pixels);
 /* ---- multi-GPU (one process, one host thread per GPU, RCCL) ----
  * Replaces the reference's CPU-parallel drivers (engine.h:335-376 _run_parallel_stripes: 4 threads on 4 row stripes;
  * SURVEY.md §8(b) rt_render_multi).  An rt_multi holds the scene uploaded on every listed device and one RCCL
- * communicator per device (ncclCommInitAll), made once at creation.  rt_render_multi renders the whole frame: device k
+ * communicator per device (one group of ncclCommInitRankConfig, non-blocking), made once at creation.  rt_render_multi renders the whole frame: device k
  * renders the row bands b (params->band_rows rows each) with b % ngpus == k -- params->band_count / band_index are
  * ignored -- packs them into one buffer, and a single ncclGather moves every device's block to devices[0], whose unpack
  * kernel writes the rows in image order.  out_rgb8: W*H*3 bytes, row 0 = top; host memory, or device memory on

@@ -3,7 +3,7 @@ contract) render of rows chosen THROUGH the objects that stress the HIP path -- 
 box tests, split-BVH duplicate references, LM 2 partial-LDS node fetches), the Next-Week box field and its media --
 at each BASELINE GPU config's full width, height and spp.
 
-    python tests/golden/make_full_size.py [cow|8|dino ...]        (build container; ~5 min on 8 threads)
+    python tests/golden/make_full_size.py [1|cow|8|dino ...]      (build container; ~5 min on 8 threads)
 
 Rows are chosen from primary-ray classification (oracle_trace_rays through pixel centres: a triangle hit is one whose
 hit_record normal is not unit length, triangle.h:32,82 -- SURVEY Q1) and from the projection of the final scene's
@@ -24,7 +24,7 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, ROOT)
 
 # scene, W, H, spp, rows to select
-CONFIGS = {"cow": (1920, 1080, 512, 24), "8": (1920, 1080, 4096, 16), "dino": (4096, 4096, 8192, 48)}
+CONFIGS = {"1": (1920, 1080, 1024, 24), "cow": (1920, 1080, 512, 24), "8": (1920, 1080, 4096, 16), "dino": (4096, 4096, 8192, 48)}
 
 
 def view(scene):
@@ -109,6 +109,34 @@ def final_rows(W, H, n):
     return np.array(sorted(pick)), {"box_field": (int(field.min()), int(field.max())), "fog_sphere": fog, "sphere_cluster": cluster}
 
 
+def random_rows(W, H, n):
+    """The headline scene (scene_manager.cpp:13-64, alias 1): rows through the three r = 1 spheres (dielectric at
+    (0,1,0), lambertian at (-4,1,0), metal at (4,1,0): the LDS image's per-slot f64 leaf tests and the dielectric
+    table) and through the field of small spheres, where the static and moving (Q2 duplicate) balls stand -- the
+    moving ones' per-slot dy -- n in total."""
+    from tests.oracle_lib import oracle_trace_rays
+    scene = "1"
+    big = [project_rows(scene, W, H, c, 1.0) for c in ((0, 1, 0), (-4, 1, 0), (4, 1, 0))]
+    rows = np.arange(0, H, 4)
+    cols = np.linspace(0, W - 1, 256).astype(int)
+    rays = primary_rays(scene, W, H, rows, cols)
+    t, _ = oracle_trace_rays(scene, rays)
+    p = rays[:, :3] + t[:, None] * rays[:, 3:6]
+    near_big = np.zeros(len(p), bool)
+    for c in ((0, 1, 0), (-4, 1, 0), (4, 1, 0)):
+        near_big |= np.linalg.norm(p - np.asarray(c, float), axis=1) < 1.0 + 1e-6
+    small = np.isfinite(t) & (p[:, 1] > 0.01) & ~near_big  # not the r = 1000 ground (p.y ~ 0), not the big three
+    cover = small.reshape(len(rows), len(cols)).mean(axis=1)
+    k = n // 6
+    pick = set()
+    for r0, r1 in big:
+        pick |= set(np.linspace(r0, r1, k + 2)[1:-1].round().astype(int))
+    field = rows[np.argsort(-cover)[: 4 * (n - len(pick))]]
+    pick |= set(np.linspace(field.min(), field.max(), n - len(pick)).round().astype(int))
+    return np.array(sorted(pick)), {"big_spheres": big, "small_sphere_rows": (int(field.min()), int(field.max())),
+                                    "peak_small_cover": float(cover.max())}
+
+
 def row_hashes(acc):
     return np.array([hashlib.sha256(np.ascontiguousarray(r, dtype="<f8").tobytes()).hexdigest() for r in acc])
 
@@ -118,6 +146,8 @@ def make(scene):
     W, H, spp, n = CONFIGS[scene]
     if scene == "8":
         rows, where = final_rows(W, H, n)
+    elif scene == "1":
+        rows, where = random_rows(W, H, n)
     else:
         rows, span, peak = triangle_rows(scene, W, H, n)
         where = {"mesh_rows": span, "peak_row_coverage": peak}

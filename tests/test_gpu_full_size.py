@@ -10,8 +10,9 @@ spheres 1920x1080x1024, C3 cow 1920x1080x512, C4 Next-Week final 1920x1080x4096,
      spread over the host threads in (row, 64-px chunk) work items.
 Asserted, bit for bit: the full frame's sampled rows == the band render (RGB8 and f64 radiance sums), the band
 render == the oracle rows (RGB8 and sums), and the band render's segment count == the oracle's.
-  4. C3-C5 also check the rows tests/golden/make_full_size.py aimed at the geometry (24 cow-silhouette rows, 16 rows
-     through the Next-Week box field, fog sphere and sphere cluster, 48 dino rows = 1.2 % of C5's pixels) against the
+  4. every config also checks the rows tests/golden/make_full_size.py aimed at the geometry (24 C2 rows through the
+     three r = 1 spheres and the small static / moving spheres, 24 cow-silhouette rows, 16 rows through the Next-Week
+     box field, fog sphere and sphere cluster, 48 dino rows = 1.2 % of C5's pixels) against the
      oracle's committed render of them: the whole frame's RGB8 and the SHA-256 of each row's f64 sums.
 """
 import hashlib
@@ -64,4 +65,4 @@ def test_full_size_frame_matches_oracle_rows(gpu, scene, W, H, spp, stride):
         assert not bad, f"{scene}: f64 sums differ on rows {bad}"
         print(f"{scene}: {len(grows)} aimed rows ({100.0 * len(grows) / H:.2f} % of the frame) equal the oracle's")
     else:
-        assert scene == "1", f"missing fixture {fx}"
+        raise AssertionError(f"missing fixture {fx}")
