@@ -231,7 +231,7 @@ struct DevScene {
     const PrimRec80* leaf_prims;  // leaf_prims[slot]: the record of primrefs[slot] of any type (triangle-free kernels)
     const PrimRec80* obj_prims;  // obj_prims[o] = the record of prim object o's primitive (indexed like objs)
     const uint8_t* lds_image;   // layout.h LDS scene image (nullptr unless the scene qualifies)
-    uint32_t n_nodes, n_primrefs, n_tris, n_objs;  // array lengths (k_paths_g's LDS copies)
+    uint32_t n_nodes, n_primrefs, n_tris, n_objs, n_mats;  // array lengths (k_paths_g's LDS copies)
     uint32_t nodes_lds;         // k_paths_g LM 2: LDS byte address of the copy of nodes [0, n_lds_nodes) (top levels)
     uint32_t n_lds_nodes;
     int32_t nworld;
@@ -1035,6 +1035,11 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
                     } else {
                         h = hit_prim_rec<R, F>(primref_type(ref), rec, r, tmin, tmax, tt, fc);
                     }
+                    // the record's material index (sphere / box / rect: dword 18 / 12 / 11) and a rect's axis (dword 10,
+                    // in the face field): the hit's surface then needs no reload of a box or rect record (prim_surface)
+                    const uint32_t ty = primref_type(ref);
+                    m = ty == PRIM_SPHERE ? v4.z : ty == PRIM_BOX ? v3.x : v2.w;
+                    if (ty == PRIM_RECT) fc = v2.z;
                 }
 #ifdef ART_STATS
                 {  // leaf tests by primitive type: lane tests [15/17/19/21], wave iterations running that type [16/18/20/22]
@@ -1095,8 +1100,19 @@ __device__ __forceinline__ bool hit_object(const DevScene<R>& S, const uint8_t* 
         prim = static_cast<uint32_t>(o.a);
         mt = kMatUnknown;
         // HBM-scene kernels: the primitive's record from obj_prims[oi], whose address does not wait on the object
-        if constexpr (!L) return hit_prim_rec<R, F>(primref_type(prim), S.obj_prims[oi], r, tmin, tmax, t, face);
-        else return hit_prim<R, F>(S, prim, r, tmin, tmax, t, face);
+        if constexpr (!L) {
+            const PrimRec80& rec = S.obj_prims[oi];
+            const uint32_t ty = primref_type(prim);
+            const bool h = hit_prim_rec<R, F>(ty, rec, r, tmin, tmax, t, face);
+            if constexpr ((F & F_TRI) == 0) {  // as the leaf records: the material index, a rect's axis in `face`
+                const uint32_t* wd = reinterpret_cast<const uint32_t*>(rec.b);
+                mt = ty == PRIM_SPHERE ? wd[18] : ty == PRIM_BOX ? wd[12] : wd[11];
+                if (ty == PRIM_RECT) face = wd[10];
+            }
+            return h;
+        } else {
+            return hit_prim<R, F>(S, prim, r, tmin, tmax, t, face);
+        }
     }
     return traverse<R, F, B, L, PL, RES>(S, lds, o.a, r, tmin, tmax, stk, t, prim, face, mt, rs, o.b);
 }
@@ -1168,7 +1184,8 @@ __device__ __forceinline__ bool hit_medium(const DevScene<R>& S, const uint8_t* 
 // The world hittable_list (hittable_list.cpp:5-19): objects in order, t_max = closest so far.
 struct HitOut {
     uint32_t prim, obj;  // obj: world slot | box face << 16
-    uint32_t mt;         // material type when the hit came from the LDS scene image, else kMatUnknown
+    uint32_t mt;         // LDS scene image: the material type; HBM-scene triangle-free kernels: the material index of a
+                         // primitive hit (a rect's axis then rides in obj >> 16); else kMatUnknown
 };
 template <class R, uint32_t F, int B, bool L, int PL = 0>
 __device__ __forceinline__ bool trace_world(const DevScene<R>& S, const uint8_t* lds, const Ray<R>& r, StackF<L, F>* stk, uint64_t& rng, R& t,
@@ -1283,8 +1300,12 @@ __device__ __forceinline__ void rect_surface(Surf<R>& s, int axis, R a0, R a1, R
     set_face_normal(s, r, n);
     s.p = r.at(t);
 }
+// mat_hint (HitOut::mt of a triangle-free HBM-scene kernel): the hit's material index, kMatUnknown otherwise.  With it,
+// a box or rect hit whose material samples no u,v builds its surface from the face / axis alone -- normal, point,
+// material -- without reloading the primitive record (its bounds only feed u, v).
 template <class R, uint32_t F, bool UV = true>
-__device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref, uint32_t face, const Ray<R>& r, R t, Surf<R>& s) {
+__device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref, uint32_t face, const Ray<R>& r, R t, Surf<R>& s,
+                                             uint32_t mat_hint = kMatUnknown) {
     const uint32_t idx = primref_index(ref);
     const uint32_t type = (fbase(F) == F_SPHERE) ? PRIM_SPHERE : primref_type(ref);
     switch (type) {
@@ -1332,6 +1353,11 @@ __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref,
         }
         case PRIM_RECT: {
             if (!(F & F_RECT)) break;
+            if (mat_hint != kMatUnknown && !(UV && (S.mats[mat_hint].flags & MATF_NEEDS_UV))) {
+                rect_surface<R, false>(s, static_cast<int>(face), R(0), R(0), R(0), R(0), R(0), r, t);
+                s.mat = mat_hint;
+                break;
+            }
             const RectRec<R>& q = S.rects[idx];
             rect_surface<R, UV>(s, static_cast<int>(q.axis), q.a0, q.a1, q.b0, q.b1, q.k, r, t, (S.mats[q.mat].flags & MATF_NEEDS_UV) != 0);
             s.mat = q.mat;
@@ -1339,6 +1365,11 @@ __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref,
         }
         default: {
             if (!(F & F_BOX)) break;
+            if (mat_hint != kMatUnknown && !(UV && (S.mats[mat_hint].flags & MATF_NEEDS_UV))) {
+                rect_surface<R, false>(s, static_cast<int>(face >> 1), R(0), R(0), R(0), R(0), R(0), r, t);  // box_face: axis = f >> 1
+                s.mat = mat_hint;
+                break;
+            }
             const BoxRec<R>& b = S.boxes[idx];
             int axis;
             R a0, a1, b0, b1, k;
@@ -1384,7 +1415,7 @@ __device__ __forceinline__ void world_surface(const DevScene<R>& S, const HitOut
             }
         }
     }
-    prim_surface<R, F, UV>(S, h.prim, h.obj >> 16, r2, t, s);
+    prim_surface<R, F, UV>(S, h.prim, h.obj >> 16, r2, t, s, (F & F_TRI) == 0 ? h.mt : kMatUnknown);
     if (!(F & F_XFORM)) return;
     auto unwind = [&](int32_t xo, const Ray<R>& inner) {
         const ObjRec<R>& o = S.objs[xo];
@@ -1493,6 +1524,14 @@ __device__ __forceinline__ V3<R> tex_value(const DevScene<R>& S, int32_t ti, R u
         break;
     }
     return mk(R(0), R(1), R(1));
+}
+
+// The texture value of material m (lambertian / diffuse_light / isotropic): the inlined solid colour (MATF_SOLID) or
+// tex_value of its texture tree -- the same doubles either way.
+template <class R, uint32_t TF = TF_ALL>
+__device__ __forceinline__ V3<R> mat_tex_value(const DevScene<R>& S, const MatRec<R>& m, R u, R v, V3<R> p) {
+    if (m.flags & MATF_SOLID) return ld3(m.albedo);
+    return tex_value<R, TF>(S, m.tex, u, v, p);
 }
 
 }  // namespace art

@@ -367,7 +367,7 @@ __device__ __forceinline__ bool scatter(const DevScene<R>& S, const MatRec<R>& m
         const V3<R> rv = unitv ? *unitv : unit(pre ? *pre : in_unit_sphere<R>(st.rng));
         dir = s.n + rv;
         if (near_zero(dir)) dir = s.n;
-        att = texc ? *texc : tex_value<R, TF>(S, m.tex, s.u, s.v, s.p);
+        att = texc ? *texc : mat_tex_value<R, TF>(S, m, s.u, s.v, s.p);
         return true;
     } else if (M == MAT_METAL) {  // material.h:45-61
         const V3<R> reflected = reflect(unitv ? *unitv : unit(st.ray.d), s.n);
@@ -392,7 +392,7 @@ __device__ __forceinline__ bool scatter(const DevScene<R>& S, const MatRec<R>& m
         return true;
     } else if (M == MAT_ISOTROPIC) {  // material.h:120-135
         dir = pre ? *pre : in_unit_sphere<R>(st.rng);
-        att = texc ? *texc : tex_value<R, TF>(S, m.tex, s.u, s.v, s.p);
+        att = texc ? *texc : mat_tex_value<R, TF>(S, m, s.u, s.v, s.p);
         return true;
     }
     return false;  // diffuse_light (material.h:106-110)
@@ -905,9 +905,18 @@ __host__ __device__ constexpr size_t paths_g_head_bytes(uint32_t stack, int bloc
     return align16(paths_g_stack_bytes(stack, block, s16) + sizeof(CameraRec<double>) + sizeof(PassGeom)) + kJumpBytes;
 }
 // LM kernels also hold the world list and the object records (a few KiB): every segment walks them, and a prim
-// object's test otherwise waits on three dependent L1 loads (world slot -> object -> primitive)
-__host__ __device__ constexpr size_t paths_g_world_bytes(int32_t nworld, uint32_t n_objs) {
-    return align16(sizeof(int32_t) * static_cast<uint32_t>(nworld)) + (sizeof(ObjRec<double>) + sizeof(PrimRec80)) * n_objs;
+// object's test otherwise waits on three dependent L1 loads (world slot -> object -> primitive).  The textured ones
+// (noise / image) also hold the material records when there are at most kMatsLdsCap of them (the Next-Week final: 12):
+// every hit's shading reads its material (type, flags, the inlined solid colour) right after the surface, and from
+// HBM that is one more dependent L2 round trip per bounce.
+constexpr uint32_t kMatsLdsCap = 128;
+template <uint32_t TF>
+__host__ __device__ constexpr uint32_t lds_mats(uint32_t n_mats) {
+    return ((TF & (TF_NOISE | TF_IMAGE)) != 0 && n_mats <= kMatsLdsCap) ? n_mats : 0u;
+}
+__host__ __device__ constexpr size_t paths_g_world_bytes(int32_t nworld, uint32_t n_objs, uint32_t n_lds_mats) {
+    return align16(sizeof(int32_t) * static_cast<uint32_t>(nworld)) + (sizeof(ObjRec<double>) + sizeof(PrimRec80)) * n_objs +
+           sizeof(MatRec<double>) * n_lds_mats;
 }
 // LM 1's LDS copy of the leaf triangle records: TriRec112 (plane precomputed, traverse's PL 2 path)
 constexpr size_t kLm1TriBytes = sizeof(TriRec112<double>);
@@ -952,7 +961,15 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
         S.world = reinterpret_cast<const int32_t*>(wb);
         S.objs = reinterpret_cast<const ObjRec<double>*>(ob);
         S.obj_prims = reinterpret_cast<const PrimRec80*>(pb);
-        lm_off += paths_g_world_bytes(S0.nworld, S0.n_objs);
+        const uint32_t nm = lds_mats<TF>(S0.n_mats);
+        if (nm) {
+            uint8_t* mb = pb + sizeof(PrimRec80) * S0.n_objs;
+            const uint2* ms = reinterpret_cast<const uint2*>(S0.mats);
+            static_assert(sizeof(MatRec<double>) % 8 == 0, "material records copied in 8-B pieces");
+            for (uint32_t i = threadIdx.x; i < nm * (sizeof(MatRec<double>) / 8); i += B) reinterpret_cast<uint2*>(mb)[i] = ms[i];
+            S.mats = reinterpret_cast<const MatRec<double>*>(mb);
+        }
+        lm_off += paths_g_world_bytes(S0.nworld, S0.n_objs, nm);
     }
     if constexpr (LM != 0) lm_off = align128(lm_off);  // node addresses multiples of 128 (device.h traverse: near/far planes by XOR)
     if constexpr (LM == 2) {  // the first n_lds_nodes nodes (the top levels of every BVH) into LDS
@@ -1117,7 +1134,7 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
                 if constexpr (kShared) {
                     const bool scat = depth + 1 < max_depth;
                     if (mat.type == MAT_LIGHT || (scat && (mat.type == MAT_LAMBERTIAN || mat.type == MAT_ISOTROPIC)))
-                        texc = tex_value<R, TF>(S, mat.tex, s.u, s.v, s.p);
+                        texc = mat_tex_value<R, TF>(S, mat, s.u, s.v, s.p);
                     if (scat && (mat.type == MAT_LAMBERTIAN || mat.type == MAT_METAL || mat.type == MAT_DIELECTRIC))
                         uv = unit(mat.type == MAT_LAMBERTIAN ? *pre : st.ray.d);
                 }
@@ -1125,7 +1142,7 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
                 const V3<R>* uvp = kShared ? &uv : nullptr;
                 ART_TICK(tm_tex);
                 if (mat.type == MAT_LIGHT) {  // material.h:114-116; diffuse_light never scatters
-                    st.L = st.L + st.T * (texp ? *texp : tex_value<R, TF>(S, mat.tex, s.u, s.v, s.p));
+                    st.L = st.L + st.T * (texp ? *texp : mat_tex_value<R, TF>(S, mat, s.u, s.v, s.p));
                 } else if (depth + 1 < max_depth) {
                     V3<R> att, dir;
                     bool sc = false;
@@ -1216,9 +1233,9 @@ __global__ __launch_bounds__(kBlock) void k_shade(DevScene<R> S, PassGeom g, Wor
             load_path(w.paths, q, st, true);
             const HitRecD<R> h = w.hits[q];
             Surf<R> s;
-            world_surface<R, F, (TF & TF_IMAGE) != 0>(S, HitOut{h.prim, h.obj}, st.ray, h.t, s);
+            world_surface<R, F, (TF & TF_IMAGE) != 0>(S, HitOut{h.prim, h.obj, kMatUnknown}, st.ray, h.t, s);
             const MatRec<R>& mat = S.mats[s.mat];
-            if (M == MAT_LIGHT) st.L = st.L + st.T * tex_value<R, TF>(S, mat.tex, s.u, s.v, s.p);  // material.h:114-116
+            if (M == MAT_LIGHT) st.L = st.L + st.T * mat_tex_value<R, TF>(S, mat, s.u, s.v, s.p);  // material.h:114-116
             if (M != MAT_LIGHT && !last) {
                 V3<R> att, dir;
                 if (scatter<R, M, TF>(S, mat, s, st, att, dir)) {
@@ -1675,6 +1692,15 @@ static void build_device_scene(const FlatScene& f, DeviceScene<R>& ds) {
         mats[i].type = f.mats[i].type; mats[i].tex = f.mats[i].tex; mats[i].flags = f.mats[i].flags; mats[i].pad = 0;
         for (int a = 0; a < 3; ++a) mats[i].albedo[a] = R(f.mats[i].albedo[a]);
         mats[i].fuzz = R(f.mats[i].fuzz); mats[i].ir = R(f.mats[i].ir);
+        mats[i].flags &= ~static_cast<uint32_t>(MATF_SOLID);
+        const int32_t t = f.mats[i].tex;
+        const uint32_t ty = f.mats[i].type;
+        if ((ty == MAT_LAMBERTIAN || ty == MAT_LIGHT || ty == MAT_ISOTROPIC) && t >= 0 && static_cast<size_t>(t) < f.texs.size() &&
+            f.texs[t].type == TEX_SOLID) {
+            // the solid colour itself: tex_value's ld3(t.c), the same doubles
+            for (int a = 0; a < 3; ++a) mats[i].albedo[a] = R(f.texs[t].c[a]);
+            mats[i].flags |= MATF_SOLID;
+        }
     }
     std::vector<TexRec<R>> texs(f.texs.size());
     for (size_t i = 0; i < texs.size(); ++i) {
@@ -1795,6 +1821,7 @@ static void build_device_scene(const FlatScene& f, DeviceScene<R>& ds) {
     }
     ds.view.n_nodes = static_cast<uint32_t>(f.nodes.size());
     ds.view.n_objs = static_cast<uint32_t>(f.objs.size());
+    ds.view.n_mats = static_cast<uint32_t>(f.mats.size());
     ds.view.n_primrefs = static_cast<uint32_t>(f.primrefs.size());
     ds.view.n_tris = static_cast<uint32_t>(f.tris.size());
     ds.view.nworld = static_cast<int32_t>(f.world.size());
@@ -1981,7 +2008,7 @@ template <uint32_t F, uint32_t TF>
 static void launch_paths_g_ft(int num_cu, hipStream_t st, const DevScene<double>& S, const PassGeom& g, const CameraRec<double>& cam,
                               const Work<double>& w, uint32_t* next_slot) {
     // g.stack = stack_rows: sentinel + entries + spare row
-    const size_t lm_head = paths_g_head_bytes(g.stack, kBlockM, (F & F_CODE16) != 0) + paths_g_world_bytes(S.nworld, S.n_objs);
+    const size_t lm_head = paths_g_head_bytes(g.stack, kBlockM, (F & F_CODE16) != 0) + paths_g_world_bytes(S.nworld, S.n_objs, lds_mats<TF>(S.n_mats));
     const size_t lds_m = align128(lm_head) + paths_g_mesh_bytes(S.n_nodes, S.n_primrefs, (F & F_TRI) ? S.n_primrefs : 0u);
     if (S.n_nodes > 0 && lds_m <= kPathsGLdsCap) {
         const int blocks = blocks_per_cu(reinterpret_cast<const void*>(k_paths_g<F, TF, 1>), kBlockM, lds_m) * num_cu;

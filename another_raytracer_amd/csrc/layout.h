@@ -184,7 +184,10 @@ constexpr uint32_t kFeatMesh = F_SPHERE | F_TRI | F_RECT | F_MEDIA;
 // ---------------------------------------------------------------------------------------------- shading
 enum MatType : uint32_t { MAT_LAMBERTIAN = 0, MAT_METAL = 1, MAT_DIELECTRIC = 2, MAT_LIGHT = 3, MAT_ISOTROPIC = 4 };
 constexpr int kNumMatTypes = 5;
-enum MatFlags : uint32_t { MATF_NEEDS_UV = 1u };  // its texture tree samples u,v (image / barycentric image)
+// MATF_NEEDS_UV: its texture tree samples u,v (image / barycentric image).  MATF_SOLID (device records only, set at
+// upload): a lambertian / diffuse_light / isotropic whose texture is a solid colour, copied into `albedo` (which only
+// metal uses otherwise), so its texture value needs no second dependent load (device.h mat_tex_value)
+enum MatFlags : uint32_t { MATF_NEEDS_UV = 1u, MATF_SOLID = 2u };
 template <class R>
 struct MatRec {
     uint32_t type;
