@@ -12,6 +12,7 @@
 
 #include "glibc_log.h"
 #include "layout.h"
+#include "sphere_uv.h"
 
 namespace art {
 
@@ -1319,11 +1320,12 @@ __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref,
             set_face_normal(s, r, outward);
             // u,v only feed image textures: acos/atan2 are skipped for materials that never sample them
             if (UV && !moving && (S.mats[sp.mat].flags & MATF_NEEDS_UV)) {
-                const R pi = R(3.1415926535897932385);
-                const R theta = acos(-outward.y);
-                const R phi = atan2(-outward.z, outward.x) + pi;
-                s.u = phi / (R(2) * pi);
-                s.v = theta / pi;
+                // get_sphere_uv (sphere.h:24-37) with sphere_uv.h's acos / atan2 (their coefficients are loaded where
+                // used, not hoisted into the path loop's registers)
+                double u, v;
+                sphere_uv(static_cast<double>(outward.x), static_cast<double>(outward.y), static_cast<double>(outward.z), u, v);
+                s.u = R(u);
+                s.v = R(v);
             } else {
                 s.u = R(0);
                 s.v = R(0);

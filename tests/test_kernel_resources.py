@@ -4,7 +4,9 @@ analysis assumes them, so a source change that breaks one shows up here, on the 
   * k_paths: at most 128 VGPRs and no spills -> 4 waves per SIMD (16 waves of its one 1024-lane block per CU);
   * k_paths_g: at most 168 VGPRs -> 3 waves per SIMD (ART_PATHS_G_WAVES);
   * the mesh kernels with solid/checker textures (cow, dino: F_CODE16 | kFeatMesh, kTexBasic) spill nothing in
-    LM 1 (dino) and at most a few registers elsewhere."""
+    LM 1 (dino) and at most a few registers elsewhere;
+  * every LM 1 kernel with 16-bit codes spills nothing -- the Next-Week final's <189, 15, 1> among them (54 spilled
+    VGPRs before csrc/sphere_uv.h replaced the device library's acos / atan2, whose hoisted constants were the spills)."""
 import os
 import re
 import sys
@@ -59,3 +61,11 @@ def test_mesh_kernels_do_not_spill(ks):
     assert pg[(F_CODE16 | kFeatMesh, kTexBasic, 1)].get(".vgpr_spill_count", 0) == 0  # dino (LM 1)
     for lm in (0, 2):  # cow (LM 2), larger meshes (LM 0)
         assert pg[(F_CODE16 | kFeatMesh, kTexBasic, lm)].get(".vgpr_spill_count", 0) <= 8
+
+
+def test_lm1_code16_kernels_do_not_spill(ks):
+    F_CODE16 = 128
+    pg = _paths_g(ks)
+    assert (189, 15, 1) in pg  # the final scene's kernel (scene 8: all features, all textures, LDS BVH)
+    spills = {key: k.get(".vgpr_spill_count", 0) for key, k in pg.items() if key[2] == 1 and key[0] & F_CODE16}
+    assert spills and all(v == 0 for v in spills.values()), spills

@@ -3,7 +3,7 @@
 #   tests                       pytest -m gpu (tests/, one process)
 #   testk:EXPR                  pytest -m gpu -k EXPR (a subset first, under a shorter limit)
 #   calib                       tools/valu_calib (VALU issue-cost calibration, plain run)
-#   uvcheck                     tools/uv_check (device vs glibc get_sphere_uv texel choice) -> gpurun_out/uv_check.json
+#   uvcheck                     tools/uv_check (device sphere_uv vs host bits and glibc texel choice) -> gpurun_out/uv_check.json
 #   ab:LIB1,LIB2[:ARGS]         tools/ab_quick.sh over in-tree libart builds (bench.py ARGS, default --spp 256)
 #   abenv:ARGS:V1+V2+...        tools/ab_env.sh over LIB[@VAR=VAL,...] variants (bench.py ARGS)
 #   pmc:TAG:SCENE[:SPP]         tools/pmc.sh counter passes + kernel trace of the current libart (ART_LIB honoured)

@@ -1,13 +1,17 @@
-// tools/uv_check.hip — how often does the device's get_sphere_uv (sphere.h:24-37, via OCML's acos / atan2) pick a
-// different texel than the reference's (glibc's acos / atan2)?  The image texture reads texel
+// tools/uv_check.hip — the device's get_sphere_uv (sphere.h:24-37; csrc/sphere_uv.h, fdlibm acos / atan2, the code
+// k_paths / k_paths_g run): does the device compute the host build's bits (it must: same code, no contraction), and how
+// often does it pick a different texel than the reference's (glibc's acos / atan2)?  The image texture reads texel
 // (int(clamp(u) * W), int((1 - clamp(v)) * H)) (texture.h:67-118), so a last-bit difference in u or v can only move a
 // lookup when u * W or (1 - v) * H lies within a few ulps of an integer.  Two normal sets, each 2^24 unit vectors:
 //   random       uniform directions (a splitmix64 stream), as hit normals (p - c) / r spread over a sphere;
 //   adversarial  directions placed on the texel boundaries of the earth texture (1024 x 512, scene_manager.cpp:117,
 //                the final scene's earth): u = k / 1024 and v = 1 - j / 512, each nudged by -4..+4 ulps per component.
-// Prints one JSON line: per set, normals whose u or v bits differ and normals whose texel differs.
-//   hipcc -O3 -ffp-contract=off --offload-arch=gfx950 tools/uv_check.hip -o tools/uv_check && ./tools/uv_check
+// Prints one JSON line: per set, normals whose u or v bits differ from glibc's, normals whose texel differs, and
+// normals whose device bits differ from the host's sphere_uv (device_vs_host, expected 0).
+//   hipcc -O3 -ffp-contract=off --offload-arch=gfx950 -Ianother_raytracer_amd/csrc tools/uv_check.hip -o tools/uv_check
 #include <hip/hip_runtime.h>
+
+#include "sphere_uv.h"
 
 #include <cmath>
 #include <cstdint>
@@ -18,12 +22,10 @@
 __global__ void k_uv(const double* n, double* uv, uint32_t count) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= count) return;
-    const double x = n[3 * k], y = n[3 * k + 1], z = n[3 * k + 2];
-    const double pi = 3.1415926535897932385;  // device.h prim_surface: the same expression as sphere.h:31-36
-    const double theta = acos(-y);
-    const double phi = atan2(-z, x) + pi;
-    uv[2 * k] = phi / (2.0 * pi);
-    uv[2 * k + 1] = theta / pi;
+    double u, v;
+    art::sphere_uv(n[3 * k], n[3 * k + 1], n[3 * k + 2], u, v);  // device.h prim_surface's call
+    uv[2 * k] = u;
+    uv[2 * k + 1] = v;
 }
 
 static uint64_t splitmix(uint64_t& s) {
@@ -94,7 +96,7 @@ int main() {
         if (hipMemcpy(dn, sets[t].data(), sizeof(double) * 3 * n, hipMemcpyHostToDevice) != hipSuccess) return 2;
         hipLaunchKernelGGL(k_uv, dim3(n / 256), dim3(256), 0, 0, dn, duv, n);
         if (hipMemcpy(uv.data(), duv, sizeof(double) * 2 * n, hipMemcpyDeviceToHost) != hipSuccess) return 2;
-        uint64_t ubad = 0, vbad = 0, tbad = 0;
+        uint64_t ubad = 0, vbad = 0, tbad = 0, hbad = 0;
         for (uint32_t k = 0; k < n; ++k) {
             const double x = sets[t][3 * k], y = sets[t][3 * k + 1], z = sets[t][3 * k + 2];
             const double theta = std::acos(-y), phi = std::atan2(-z, x) + pi;  // glibc: the reference's libm
@@ -105,9 +107,13 @@ int main() {
             texel(u, v, W, H, i0, j0);
             texel(uv[2 * k], uv[2 * k + 1], W, H, i1, j1);
             tbad += (i0 != i1 || j0 != j1);
+            double hu, hv;
+            art::sphere_uv(x, y, z, hu, hv);
+            hbad += bits(hu) != bits(uv[2 * k]) || bits(hv) != bits(uv[2 * k + 1]);
         }
-        std::printf(", \"%s\": {\"u_bits_differ\": %llu, \"v_bits_differ\": %llu, \"texel_differs\": %llu}", names[t],
-                    static_cast<unsigned long long>(ubad), static_cast<unsigned long long>(vbad), static_cast<unsigned long long>(tbad));
+        std::printf(", \"%s\": {\"u_bits_differ\": %llu, \"v_bits_differ\": %llu, \"texel_differs\": %llu, \"device_vs_host\": %llu}", names[t],
+                    static_cast<unsigned long long>(ubad), static_cast<unsigned long long>(vbad), static_cast<unsigned long long>(tbad),
+                    static_cast<unsigned long long>(hbad));
     }
     std::printf("}\n");
     return 0;
