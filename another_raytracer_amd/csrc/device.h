@@ -576,8 +576,11 @@ __device__ __forceinline__ bool hit_lds_slot(const uint8_t* lds, uint32_t slot, 
 #ifdef ART_STATS
 // Divergence statistics (diagnostic builds only): [0] node-loop wave iterations, [1] node visits (lane sum), [2] leaf-
 // loop wave iterations, [3] leaf tests (lane sum), [4] outer-loop wave iterations, [5] outer iterations (lane sum),
-// [6] traversals, [7] hit_sphere tests with disc >= 0.
-__device__ unsigned long long g_art_stats[32];
+// [6] traversals, [7] hit_sphere tests with disc >= 0; [32..45] k_paths_g's surface branches (wave iterations, lanes):
+// sphere u,v, transform unwinds, medium hits, box/rect record reloads, spheres, box/rect from the carried material,
+// world_surface calls.
+constexpr int kArtStats = 48;
+__device__ unsigned long long g_art_stats[kArtStats];
 __device__ __forceinline__ void stat_wave(int k) {
     const uint64_t m = __ballot(true);
     if (static_cast<int>(__lane_id()) == __ffsll(static_cast<long long>(m)) - 1) atomicAdd(&g_art_stats[k], 1ull);
@@ -1311,6 +1314,8 @@ __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref,
     const uint32_t type = (fbase(F) == F_SPHERE) ? PRIM_SPHERE : primref_type(ref);
     switch (type) {
         case PRIM_SPHERE: {  // sphere.h:57-63, :24-37
+            ART_STAT_WAVE(40);
+            ART_STAT_LANE(41);
             const SphereRec<R>& sp = S.spheres[idx];
             V3<R> center = ld3(sp.c);
             const bool moving = (sp.flags & SPH_MOVING) != 0;
@@ -1320,6 +1325,8 @@ __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref,
             set_face_normal(s, r, outward);
             // u,v only feed image textures: acos/atan2 are skipped for materials that never sample them
             if (UV && !moving && (S.mats[sp.mat].flags & MATF_NEEDS_UV)) {
+                ART_STAT_WAVE(32);
+                ART_STAT_LANE(33);
                 // get_sphere_uv (sphere.h:24-37) with sphere_uv.h's acos / atan2 (their coefficients are loaded where
                 // used, not hoisted into the path loop's registers)
                 double u, v;
@@ -1356,10 +1363,14 @@ __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref,
         case PRIM_RECT: {
             if (!(F & F_RECT)) break;
             if (mat_hint != kMatUnknown && !(UV && (S.mats[mat_hint].flags & MATF_NEEDS_UV))) {
+                ART_STAT_WAVE(42);
+                ART_STAT_LANE(43);
                 rect_surface<R, false>(s, static_cast<int>(face), R(0), R(0), R(0), R(0), R(0), r, t);
                 s.mat = mat_hint;
                 break;
             }
+            ART_STAT_WAVE(38);
+            ART_STAT_LANE(39);
             const RectRec<R>& q = S.rects[idx];
             rect_surface<R, UV>(s, static_cast<int>(q.axis), q.a0, q.a1, q.b0, q.b1, q.k, r, t, (S.mats[q.mat].flags & MATF_NEEDS_UV) != 0);
             s.mat = q.mat;
@@ -1368,10 +1379,14 @@ __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref,
         default: {
             if (!(F & F_BOX)) break;
             if (mat_hint != kMatUnknown && !(UV && (S.mats[mat_hint].flags & MATF_NEEDS_UV))) {
+                ART_STAT_WAVE(42);
+                ART_STAT_LANE(43);
                 rect_surface<R, false>(s, static_cast<int>(face >> 1), R(0), R(0), R(0), R(0), R(0), r, t);  // box_face: axis = f >> 1
                 s.mat = mat_hint;
                 break;
             }
+            ART_STAT_WAVE(38);
+            ART_STAT_LANE(39);
             const BoxRec<R>& b = S.boxes[idx];
             int axis;
             R a0, a1, b0, b1, k;
@@ -1389,7 +1404,11 @@ template <class R, uint32_t F, bool UV = true>
 __device__ __forceinline__ void world_surface(const DevScene<R>& S, const HitOut& h, const Ray<R>& r, R t, Surf<R>& s) {
     const int32_t w = static_cast<int32_t>(h.obj & 0xFFFFu);
     int32_t oi = S.world[w];
+    ART_STAT_WAVE(44);
+    ART_STAT_LANE(45);
     if ((F & F_MEDIA) && h.prim == kMediumHit) {  // constant_medium.h:75-79
+        ART_STAT_WAVE(36);
+        ART_STAT_LANE(37);
         s.p = r.at(t);
         s.n = mk(R(1), R(0), R(0));
         s.ff = true;
@@ -1419,6 +1438,12 @@ __device__ __forceinline__ void world_surface(const DevScene<R>& S, const HitOut
     }
     prim_surface<R, F, UV>(S, h.prim, h.obj >> 16, r2, t, s, (F & F_TRI) == 0 ? h.mt : kMatUnknown);
     if (!(F & F_XFORM)) return;
+#ifdef ART_STATS
+    if (o0 >= 0) {
+        ART_STAT_WAVE(34);
+        ART_STAT_LANE(35);
+    }
+#endif
     auto unwind = [&](int32_t xo, const Ray<R>& inner) {
         const ObjRec<R>& o = S.objs[xo];
         if (o.kind == OBJ_TRANSLATE) {

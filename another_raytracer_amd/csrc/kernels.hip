@@ -2335,7 +2335,7 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     HIP_OK(hipGetLastError());
 #ifdef ART_STATS
     {
-        unsigned long long st[32] = {0};
+        unsigned long long st[kArtStats] = {0};
         HIP_OK(hipStreamSynchronize(stream));
         HIP_OK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_art_stats), sizeof st));
         std::fprintf(stderr, "ART_STATS node_w %llu node_l %llu (util %.3f) leaf_w %llu leaf_l %llu (util %.3f) outer_w %llu outer_l %llu (util %.3f) "
@@ -2355,6 +2355,10 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
                          st[8] / tt, st[9] / tt, (st[10] + st[24] + st[25] + st[26]) / tt, st[11] / tt, st[24] / tt, st[25] / tt, st[26] / tt, st[10] / tt);
         if (st[28] + st[30] > 0)
             std::fprintf(stderr, "ART_STATS texture evaluations (wave iterations, lanes): noise %llu %llu image %llu %llu\n", st[28], st[29], st[30], st[31]);
+        if (st[44] > 0)
+            std::fprintf(stderr, "ART_STATS surface branches (wave iterations, lanes): world_surface %llu %llu sphere %llu %llu sphere-uv %llu %llu "
+                         "unwind %llu %llu medium %llu %llu box/rect-record %llu %llu box/rect-carried %llu %llu\n",
+                         st[44], st[45], st[40], st[41], st[32], st[33], st[34], st[35], st[36], st[37], st[38], st[39], st[42], st[43]);
         std::memset(st, 0, sizeof st);
         HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(g_art_stats), st, sizeof st));
     }

@@ -36,22 +36,26 @@ enum UvCoef : int {
     kAtanHi0, kAtanHi1, kAtanHi2, kAtanHi3, kAtanLo0, kAtanLo1, kAtanLo2, kAtanLo3,
     kPi, kPio2Hi, kPio2Lo, kPiLo, kOneHalf3, kTiny, kTwoPi, kUvCoefs
 };
+// (the last: sphere.h:36's 2 * pi; the reference's pi constant, tracer_utils.h, is kPi's double)
+#define ART_UV_COEFS \
+    1.66666666666666657415e-01, -3.25565818622400915405e-01, 2.01212532134862925881e-01, -4.00555345006794114027e-02, \
+    7.91534994289814532176e-04, 3.47933107596021167570e-05, -2.40339491173441421878e+00, 2.02094576023350569471e+00, \
+    -6.88283971605453293030e-01, 7.70381505559019352791e-02, \
+    3.33333333333329318027e-01, -1.99999999998764832476e-01, 1.42857142725034663711e-01, -1.11111104054623557880e-01, \
+    9.09088713343650656196e-02, -7.69187620504482999495e-02, 6.66107313738753120669e-02, -5.83357013379057348645e-02, \
+    4.97687799461593236017e-02, -3.65315727442169155270e-02, 1.62858201153657823623e-02, \
+    4.63647609000806093515e-01, 7.85398163397448278999e-01, 9.82793723247329054082e-01, 1.57079632679489655800e+00, \
+    2.26987774529616870924e-17, 3.06161699786838301793e-17, 1.39033110312309984516e-17, 6.12323399573676603587e-17, \
+    3.14159265358979311600e+00, 1.57079632679489655800e+00, 6.12323399573676603587e-17, 1.2246467991473531772e-16, \
+    1.5, 1.0e-300, \
+    2.0 * 3.1415926535897932385
+// The device reads its own copy (constant memory); a HIP translation unit's host side reads the plain one (the host
+// shadow of a __constant__ variable holds no initialiser).
+static const double kUvCoefHost[kUvCoefs] = {ART_UV_COEFS};
 #if defined(__HIPCC__)
-__constant__
+__constant__ static const double kUvCoefDev[kUvCoefs] = {ART_UV_COEFS};
 #endif
-static const double kUvCoefTable[kUvCoefs] = {
-    1.66666666666666657415e-01, -3.25565818622400915405e-01, 2.01212532134862925881e-01, -4.00555345006794114027e-02,
-    7.91534994289814532176e-04, 3.47933107596021167570e-05, -2.40339491173441421878e+00, 2.02094576023350569471e+00,
-    -6.88283971605453293030e-01, 7.70381505559019352791e-02,
-    3.33333333333329318027e-01, -1.99999999998764832476e-01, 1.42857142725034663711e-01, -1.11111104054623557880e-01,
-    9.09088713343650656196e-02, -7.69187620504482999495e-02, 6.66107313738753120669e-02, -5.83357013379057348645e-02,
-    4.97687799461593236017e-02, -3.65315727442169155270e-02, 1.62858201153657823623e-02,
-    4.63647609000806093515e-01, 7.85398163397448278999e-01, 9.82793723247329054082e-01, 1.57079632679489655800e+00,
-    2.26987774529616870924e-17, 3.06161699786838301793e-17, 1.39033110312309984516e-17, 6.12323399573676603587e-17,
-    3.14159265358979311600e+00, 1.57079632679489655800e+00, 6.12323399573676603587e-17, 1.2246467991473531772e-16,
-    1.5, 1.0e-300,
-    2.0 * 3.1415926535897932385,  // sphere.h:36's 2*pi (the reference's pi constant, tracer_utils.h, is this double)
-};
+#undef ART_UV_COEFS
 
 // The coefficient table with an offset the compiler cannot see through (device): each coefficient is a scalar load at
 // its use, never a value hoisted into a register for the life of the path loop.
@@ -61,9 +65,9 @@ struct UvTab {
 #if defined(__HIP_DEVICE_COMPILE__)
         uint32_t z;
         __asm__ volatile("s_mov_b32 %0, 0" : "=s"(z));
-        t = kUvCoefTable + z;
+        t = kUvCoefDev + z;
 #else
-        t = kUvCoefTable;
+        t = kUvCoefHost;
 #endif
     }
     ART_UV_HD double operator[](int k) const { return t[k]; }

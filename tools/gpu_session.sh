@@ -12,6 +12,9 @@
 #   configs:TAG                 tools/configs.sh (one bench line per BASELINE GPU config)
 #   stats:TAG                   tools/stats_configs.sh over the four GPU configs (libart_stats.so: divergence counters
 #                               and the per-phase cycle split) -> gpurun_out/stats_TAG.txt
+#   pcs:TAG:METHOD[:ARGS]       rocprofv3 PC sampling (METHOD host_trap | stochastic) of one bench.py run (default
+#                               --scene 8 --spp 16) -> gpurun_out/pcs_TAG (samples per instruction of the path kernels)
+#   pcslist                     rocprofv3 -L (the PC sampling configurations the box offers) -> gpurun_out/pcs_list.txt
 # Usage (GPU box): bash tools/gpu_session.sh tests ab:libart_x.so,libart.so pmc:r2b:1
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
 export TMPDIR=/tmp
@@ -54,6 +57,16 @@ for step in "$@"; do
     prof)
       run 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$a -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline $b > gpurun_out/rocprof_$a.log 2>&1
       tail -1 gpurun_out/rocprof_$a.log ;;
+    pcslist)
+      run 60 rocprofv3 -L > gpurun_out/pcs_list.txt 2>&1
+      grep -i -A12 "pc.sampl" gpurun_out/pcs_list.txt | head -60 || true ;;
+    pcs)
+      unit=time; ival=1; [ "$b" = "stochastic" ] && { unit=cycles; ival=1048576; }
+      export ROCPROFILER_PC_SAMPLING_BETA_ENABLED=1
+      run 150 rocprofv3 --pc-sampling-beta-enabled --pc-sampling-method $b --pc-sampling-unit $unit --pc-sampling-interval $ival \
+        --output-format csv -d gpurun_out/pcs_$a -o run -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-parity \
+        ${c:---scene 8 --spp 16} > gpurun_out/pcs_$a.log 2>&1
+      tail -2 gpurun_out/pcs_$a.log; find gpurun_out/pcs_$a -type f | head ;;
     configs)
       TAG=$a bash tools/configs.sh || exit 1 ;;
     stats)

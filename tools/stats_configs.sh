@@ -7,5 +7,5 @@ CFGS=${CFGS:-"--scene cow --spp 64|--scene 8 --spp 64|--scene dino --width 4096 
 IFS='|' read -ra CFG_ARR <<< "$CFGS"
 for cfg in "${CFG_ARR[@]}"; do
   timeout -k 10 200 env ART_LIB=$PWD/another_raytracer_amd/libart_stats.so python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-parity $cfg > gpurun_out/stats.log 2>&1 || exit 1
-  echo "$cfg"; grep ART_STATS gpurun_out/stats.log | head -4
+  echo "$cfg"; grep ART_STATS gpurun_out/stats.log | head -8
 done
