@@ -3,6 +3,7 @@
 #   tests                       pytest -m gpu (tests/, one process)
 #   testk:EXPR                  pytest -m gpu -k EXPR (a subset first, under a shorter limit)
 #   calib                       tools/valu_calib (VALU issue-cost calibration, plain run)
+#   logcheck                    tools/log_check (device logs vs glibc over all 2^24 draws) -> gpurun_out/log_check.json
 #   uvcheck                     tools/uv_check (device sphere_uv vs host bits and glibc texel choice) -> gpurun_out/uv_check.json
 #   ab:LIB1,LIB2[:ARGS]         tools/ab_quick.sh over in-tree libart builds (bench.py ARGS, default --spp 256)
 #   abenv:ARGS:V1+V2+...        tools/ab_env.sh over LIB[@VAR=VAL,...] variants (bench.py ARGS)
@@ -12,9 +13,6 @@
 #   configs:TAG                 tools/configs.sh (one bench line per BASELINE GPU config)
 #   stats:TAG                   tools/stats_configs.sh over the four GPU configs (libart_stats.so: divergence counters
 #                               and the per-phase cycle split) -> gpurun_out/stats_TAG.txt
-#   pcs:TAG:METHOD[:ARGS]       rocprofv3 PC sampling (METHOD host_trap | stochastic) of one bench.py run (default
-#                               --scene 8 --spp 16) -> gpurun_out/pcs_TAG (samples per instruction of the path kernels)
-#   pcslist                     rocprofv3 -L (the PC sampling configurations the box offers) -> gpurun_out/pcs_list.txt
 # Usage (GPU box): bash tools/gpu_session.sh tests ab:libart_x.so,libart.so pmc:r2b:1
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
 export TMPDIR=/tmp
@@ -37,6 +35,9 @@ for step in "$@"; do
     calib)
       run 120 ./tools/valu_calib > gpurun_out/valu_calib.jsonl 2>&1
       cat gpurun_out/valu_calib.jsonl ;;
+    logcheck)
+      run 200 ./tools/log_check gpurun_out/log_exceptions.txt > gpurun_out/log_check.json 2>&1
+      cat gpurun_out/log_check.json ;;
     uvcheck)
       run 300 ./tools/uv_check > gpurun_out/uv_check.json 2>&1
       cat gpurun_out/uv_check.json ;;
@@ -57,16 +58,6 @@ for step in "$@"; do
     prof)
       run 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$a -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline $b > gpurun_out/rocprof_$a.log 2>&1
       tail -1 gpurun_out/rocprof_$a.log ;;
-    pcslist)
-      run 60 rocprofv3 -L > gpurun_out/pcs_list.txt 2>&1
-      grep -i -A12 "pc.sampl" gpurun_out/pcs_list.txt | head -60 || true ;;
-    pcs)
-      unit=time; ival=1; [ "$b" = "stochastic" ] && { unit=cycles; ival=1048576; }
-      export ROCPROFILER_PC_SAMPLING_BETA_ENABLED=1
-      run 150 rocprofv3 --pc-sampling-beta-enabled --pc-sampling-method $b --pc-sampling-unit $unit --pc-sampling-interval $ival \
-        --output-format csv -d gpurun_out/pcs_$a -o run -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-parity \
-        ${c:---scene 8 --spp 16} > gpurun_out/pcs_$a.log 2>&1
-      tail -2 gpurun_out/pcs_$a.log; find gpurun_out/pcs_$a -type f | head ;;
     configs)
       TAG=$a bash tools/configs.sh || exit 1 ;;
     stats)
