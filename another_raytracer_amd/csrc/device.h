@@ -541,6 +541,14 @@ __device__ __forceinline__ void cas(float& ka, int32_t& ca, float& kb, int32_t& 
 #ifndef ART_LDS_LEAF_NOREF
 #define ART_LDS_LEAF_NOREF 0  // 1 (k_paths object, Makefile PATHS_NOREF): the leaf test skips the per-slot code
 #endif
+// ART_COOP_LEAF (experiment, k_paths only): the wave-cooperative leaf test.  A leaf phase's tests (up to 8 per lane)
+// are spread over the lanes still traversing, one test per lane, instead of each lane looping over its own; the
+// owner then folds its tests' results in its own order.  Per-wave LDS scratch: [0, 64) the lane of each rank,
+// [64, 192) the phase's tests (slot | owner lane << 10).
+#ifndef ART_COOP_LEAF
+#define ART_COOP_LEAF 0
+#endif
+constexpr uint32_t kCoopLeafWaveBytes = 192;
 // Leaf slot test of the LDS scene image (layout.h): the same root selection as hit_sphere on the same f64 values.
 // d_a = |d|^2 and d_inv_a = 1 / d_a come from the traversal (once per ray).  The image sits at LDS address 0, so
 // every read takes an integer LDS byte address (one shift-add, the plane offset folded in).  Moving spheres of the
@@ -578,7 +586,8 @@ __device__ __forceinline__ bool hit_lds_slot(const uint8_t* lds, uint32_t slot, 
 // loop wave iterations, [3] leaf tests (lane sum), [4] outer-loop wave iterations, [5] outer iterations (lane sum),
 // [6] traversals, [7] hit_sphere tests with disc >= 0; [32..45] k_paths_g's surface branches (wave iterations, lanes):
 // sphere u,v, transform unwinds, medium hits, box/rect record reloads, spheres, box/rect from the carried material,
-// world_surface calls.
+// world_surface calls; [46] leaf phases (wave), [47] the wave iterations a wave-cooperative leaf test would need
+// (sum over leaf phases of ceil(the phase's leaf tests / the lanes still traversing)).
 constexpr int kArtStats = 48;
 __device__ unsigned long long g_art_stats[kArtStats];
 __device__ __forceinline__ void stat_wave(int k) {
@@ -962,6 +971,9 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
         }
         uint32_t first, cnt;
         uint32_t first2 = 0, cnt12 = 0;
+#ifdef ART_STATS
+        const bool stats_phase = true;
+#endif
         if constexpr (L) {
             const uint32_t x = ~static_cast<uint32_t>(leaf);
             first = x & ((1u << kLdsLeafShift) - 1);
@@ -982,6 +994,74 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
             first2 = leaf_first(leaf2) - cnt;
             cnt12 = cnt + leaf_count(leaf2);
         }
+#if ART_COOP_LEAF
+        if constexpr (L && ART_LDS_LEAF_NOREF) {
+            // the phase's tests numbered in lane order: this lane's are [pre, pre + cnt12) of total
+            const uint32_t lane = __lane_id();
+            const uint64_t below = (1ull << lane) - 1ull;
+            const uint64_t act = __ballot(true);
+            uint32_t total = 0, pre = 0;
+            for (int b = 0; b < 4; ++b) {
+                const uint64_t m = __ballot((cnt12 >> b) & 1u);
+                total += static_cast<uint32_t>(__popcll(m)) << b;
+                pre += static_cast<uint32_t>(__popcll(m & below)) << b;
+            }
+            const uint32_t nact = static_cast<uint32_t>(__popcll(act));
+            if (total <= nact && total > 1) {  // one test per lane (more tests than lanes: the loop below)
+                const uint32_t rank = static_cast<uint32_t>(__popcll(act & below));
+                const uint32_t base = S.nodes_lds;
+                *(__attribute__((address_space(3))) uint8_t*)(size_t)(base + rank) = static_cast<uint8_t>(lane);
+                for (uint32_t k = 0; k < cnt12; ++k) {
+                    const uint32_t slot = (k < cnt ? first : first2) + k;
+                    *(__attribute__((address_space(3))) uint16_t*)(size_t)(base + 64u + 2u * (pre + k)) = static_cast<uint16_t>(slot | (lane << 10));
+                }
+                __builtin_amdgcn_wave_barrier();
+                __asm__ volatile("" ::: "memory");
+                // test number `rank`, for its owner's ray (every active lane takes part in the shuffles)
+                const uint32_t e = *(__attribute__((address_space(3))) const uint16_t*)(size_t)(base + 64u + 2u * (rank < total ? rank : 0u));
+                const int o = static_cast<int>(e >> 10);
+                Ray<double> ro;
+                ro.o = mk(__shfl(r.o.x, o), __shfl(r.o.y, o), __shfl(r.o.z, o));
+                ro.d = mk(__shfl(r.d.x, o), __shfl(r.d.y, o), __shfl(r.d.z, o));
+                ro.tm = __shfl(r.tm, o);
+                const double da = __shfl(d_a, o), dia = __shfl(d_inv_a, o), tmn = __shfl(tmin, o), tmx = __shfl(tmax, o);
+                double wt = 0.0;
+                uint32_t pr, mm;
+                const bool wh = hit_lds_slot(lds, e & 1023u, ro, da, dia, tmn, tmx, wt, pr, mm) && rank < total;
+                // the owner folds its tests in order (a result t <= the tmax so far is what the sequential test would
+                // have accepted: the root choices against a larger tmax differ only above it)
+                for (uint32_t k = 0; __ballot(k < cnt12) != 0; ++k) {
+                    const uint32_t j = pre + k;
+                    const int wl = static_cast<int>(*(__attribute__((address_space(3))) const uint8_t*)(size_t)(base + (j < 64u ? j : 0u)));
+                    const int hk = __shfl(static_cast<int>(wh), wl);
+                    const double tk = __shfl(wt, wl);
+                    if (k < cnt12 && hk && !(tmax < tk)) {
+                        tmax = tk;
+                        t = tk;
+                        prim = 0;
+                        face = (k < cnt ? first : first2) + k;
+                        mt = kMatUnknown;
+                        hit = true;
+                        tmaxf = f_hi(tk);
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+                __asm__ volatile("" ::: "memory");
+                continue;
+            }
+        }
+#endif
+#ifdef ART_STATS
+        if (stats_phase) {  // the cooperative leaf test's iterations: the phase's tests spread over the lanes still here
+            uint32_t total = 0;
+            for (int b = 0; b < 4; ++b) total += static_cast<uint32_t>(__popcll(__ballot((cnt12 >> b) & 1u))) << b;
+            const uint32_t active = static_cast<uint32_t>(__popcll(__ballot(true)));
+            if (static_cast<int>(__lane_id()) == __ffsll(static_cast<long long>(__ballot(true))) - 1) {
+                atomicAdd(&g_art_stats[46], 1ull);
+                atomicAdd(&g_art_stats[47], static_cast<unsigned long long>((total + active - 1) / active));
+            }
+        }
+#endif
         for (uint32_t k = 0; k < cnt12; ++k) {
             ART_STAT_WAVE(2);
             ART_STAT_LANE(3);
@@ -1287,57 +1367,85 @@ __device__ __forceinline__ void set_face_normal(Surf<R>& s, const Ray<R>& r, V3<
     s.ff = dot(r.d, outward) < R(0);
     s.n = s.ff ? outward : -outward;
 }
+// hittable.h:18-22 into locals (prim_surface)
+template <class R>
+__device__ __forceinline__ void face_normal(const Ray<R>& r, V3<R> outward, bool& ff, V3<R>& n) {
+    ff = dot(r.d, outward) < R(0);
+    n = ff ? outward : -outward;
+}
+// An axis-aligned rect's surface into prim_surface's locals.  prim_surface builds every field in locals and stores s
+// once: stores into s in several branches were merged by the compiler into one store through a phi of addresses
+// (different fields), which kept parts of Surf in scratch memory.
 template <class R, bool UV = true>
-__device__ __forceinline__ void rect_surface(Surf<R>& s, int axis, R a0, R a1, R b0, R b1, R k, const Ray<R>& r, R t, bool need_uv = true) {
+__device__ __forceinline__ void rect_surface(V3<R>& p, V3<R>& n, bool& ff, R& su, R& sv, int axis, R a0, R a1, R b0, R b1, const Ray<R>& r,
+                                             R t, bool need_uv = true) {
     if (UV && need_uv) {  // u, v feed image textures only (materials without MATF_NEEDS_UV skip the two divisions)
         const int ia = axis == 2 ? 1 : 0;
         const int ib = axis == 0 ? 1 : 2;
         const R x = comp(r.o, ia) + t * comp(r.d, ia);
         const R y = comp(r.o, ib) + t * comp(r.d, ib);
-        s.u = (x - a0) / (a1 - a0);
-        s.v = (y - b0) / (b1 - b0);
-    } else {
-        s.u = R(0);
-        s.v = R(0);
+        su = (x - a0) / (a1 - a0);
+        sv = (y - b0) / (b1 - b0);
     }
-    const V3<R> n = axis == 0 ? mk(R(0), R(0), R(1)) : (axis == 1 ? mk(R(0), R(1), R(0)) : mk(R(1), R(0), R(0)));
-    set_face_normal(s, r, n);
-    s.p = r.at(t);
+    const V3<R> on = axis == 0 ? mk(R(0), R(0), R(1)) : (axis == 1 ? mk(R(0), R(1), R(0)) : mk(R(1), R(0), R(0)));
+    face_normal(r, on, ff, n);
+    p = r.at(t);
 }
 // mat_hint (HitOut::mt of a triangle-free HBM-scene kernel): the hit's material index, kMatUnknown otherwise.  With it,
 // a box or rect hit whose material samples no u,v builds its surface from the face / axis alone -- normal, point,
 // material -- without reloading the primitive record (its bounds only feed u, v).
-template <class R, uint32_t F, bool UV = true>
+// A sphere record's fields as scalars (world_surface's prefetch: no array members, nothing for the compiler to keep in
+// private memory)
+template <class R>
+struct SphPre {
+    V3<R> c, d;
+    R r, t0, dt;
+    uint32_t mat, flags;
+};
+// PRE: a sphere hit's record was loaded by the caller into sph_pre (world_surface's prefetch).
+template <class R, uint32_t F, bool UV = true, bool PRE = false>
 __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref, uint32_t face, const Ray<R>& r, R t, Surf<R>& s,
-                                             uint32_t mat_hint = kMatUnknown) {
+                                             uint32_t mat_hint = kMatUnknown, const SphPre<R>& sph_pre = SphPre<R>{}) {
     const uint32_t idx = primref_index(ref);
     const uint32_t type = (fbase(F) == F_SPHERE) ? PRIM_SPHERE : primref_type(ref);
+    V3<R> sp_p = mk(R(0), R(0), R(0)), sp_n = mk(R(0), R(0), R(0));
+    bool ff = false;
+    R su = R(0), sv = R(0);
+    uint32_t mat = 0;
     switch (type) {
         case PRIM_SPHERE: {  // sphere.h:57-63, :24-37
             ART_STAT_WAVE(40);
             ART_STAT_LANE(41);
-            const SphereRec<R>& sp = S.spheres[idx];
-            V3<R> center = ld3(sp.c);
+            SphPre<R> sp;
+            if constexpr (PRE) {
+                sp = sph_pre;
+            } else {
+                const SphereRec<R>& sr = S.spheres[idx];
+                sp.c = ld3(sr.c);
+                sp.d = ld3(sr.d);
+                sp.r = sr.r;
+                sp.t0 = sr.t0;
+                sp.dt = sr.dt;
+                sp.mat = sr.mat;
+                sp.flags = sr.flags;
+            }
+            V3<R> center = sp.c;
             const bool moving = (sp.flags & SPH_MOVING) != 0;
-            if (moving) center = center + motion_fraction(r.tm, sp.t0, sp.dt) * ld3(sp.d);
-            s.p = r.at(t);
-            const V3<R> outward = divs(s.p - center, sp.r);
-            set_face_normal(s, r, outward);
+            if (moving) center = center + motion_fraction(r.tm, sp.t0, sp.dt) * sp.d;
+            sp_p = r.at(t);
+            const V3<R> outward = divs(sp_p - center, sp.r);
+            face_normal(r, outward, ff, sp_n);
             // u,v only feed image textures: acos/atan2 are skipped for materials that never sample them
             if (UV && !moving && (S.mats[sp.mat].flags & MATF_NEEDS_UV)) {
                 ART_STAT_WAVE(32);
                 ART_STAT_LANE(33);
                 // get_sphere_uv (sphere.h:24-37) with sphere_uv.h's acos / atan2 (their coefficients are loaded where
                 // used, not hoisted into the path loop's registers)
-                double u, v;
-                sphere_uv(static_cast<double>(outward.x), static_cast<double>(outward.y), static_cast<double>(outward.z), u, v);
-                s.u = R(u);
-                s.v = R(v);
-            } else {
-                s.u = R(0);
-                s.v = R(0);
+                const UvPair uv = sphere_uv(static_cast<double>(outward.x), static_cast<double>(outward.y), static_cast<double>(outward.z));
+                su = R(uv.u);
+                sv = R(uv.v);
             }
-            s.mat = sp.mat;
+            mat = sp.mat;
             break;
         }
         case PRIM_TRIANGLE: {  // triangle.h:57-85
@@ -1346,18 +1454,15 @@ __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref,
             const V3<R> p1 = ld3(tr.p), p2 = ld3(tr.p + 3), p3 = ld3(tr.p + 6);
             const V3<R> N = cross(p2 - p1, p3 - p1);
             const V3<R> p = r.o + t * r.d;
-            s.p = p;
-            set_face_normal(s, r, N);
+            sp_p = p;
+            face_normal(r, N, ff, sp_n);
             if (UV && (S.mats[tr.mat].flags & MATF_NEEDS_UV)) {  // barycentric u, v feed image textures only (texture.h:135-154)
                 const R u = dot(N, cross(p3 - p2, p - p2));
                 const R v = dot(N, cross(p1 - p3, p - p3));
-                s.u = u / len2(N);
-                s.v = v / len2(N);
-            } else {
-                s.u = R(0);
-                s.v = R(0);
+                su = u / len2(N);
+                sv = v / len2(N);
             }
-            s.mat = tr.mat;
+            mat = tr.mat;
             break;
         }
         case PRIM_RECT: {
@@ -1365,15 +1470,15 @@ __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref,
             if (mat_hint != kMatUnknown && !(UV && (S.mats[mat_hint].flags & MATF_NEEDS_UV))) {
                 ART_STAT_WAVE(42);
                 ART_STAT_LANE(43);
-                rect_surface<R, false>(s, static_cast<int>(face), R(0), R(0), R(0), R(0), R(0), r, t);
-                s.mat = mat_hint;
+                rect_surface<R, false>(sp_p, sp_n, ff, su, sv, static_cast<int>(face), R(0), R(0), R(0), R(0), r, t);
+                mat = mat_hint;
                 break;
             }
             ART_STAT_WAVE(38);
             ART_STAT_LANE(39);
             const RectRec<R>& q = S.rects[idx];
-            rect_surface<R, UV>(s, static_cast<int>(q.axis), q.a0, q.a1, q.b0, q.b1, q.k, r, t, (S.mats[q.mat].flags & MATF_NEEDS_UV) != 0);
-            s.mat = q.mat;
+            rect_surface<R, UV>(sp_p, sp_n, ff, su, sv, static_cast<int>(q.axis), q.a0, q.a1, q.b0, q.b1, r, t, (S.mats[q.mat].flags & MATF_NEEDS_UV) != 0);
+            mat = q.mat;
             break;
         }
         default: {
@@ -1381,8 +1486,8 @@ __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref,
             if (mat_hint != kMatUnknown && !(UV && (S.mats[mat_hint].flags & MATF_NEEDS_UV))) {
                 ART_STAT_WAVE(42);
                 ART_STAT_LANE(43);
-                rect_surface<R, false>(s, static_cast<int>(face >> 1), R(0), R(0), R(0), R(0), R(0), r, t);  // box_face: axis = f >> 1
-                s.mat = mat_hint;
+                rect_surface<R, false>(sp_p, sp_n, ff, su, sv, static_cast<int>(face >> 1), R(0), R(0), R(0), R(0), r, t);  // box_face: axis = f >> 1
+                mat = mat_hint;
                 break;
             }
             ART_STAT_WAVE(38);
@@ -1391,11 +1496,17 @@ __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref,
             int axis;
             R a0, a1, b0, b1, k;
             box_face(b, static_cast<int>(face), axis, a0, a1, b0, b1, k);
-            rect_surface<R, UV>(s, axis, a0, a1, b0, b1, k, r, t, (S.mats[b.mat].flags & MATF_NEEDS_UV) != 0);
-            s.mat = b.mat;
+            rect_surface<R, UV>(sp_p, sp_n, ff, su, sv, axis, a0, a1, b0, b1, r, t, (S.mats[b.mat].flags & MATF_NEEDS_UV) != 0);
+            mat = b.mat;
             break;
         }
     }
+    s.p = sp_p;
+    s.n = sp_n;
+    s.ff = ff;
+    s.u = su;
+    s.v = sv;
+    s.mat = mat;
 }
 
 // Rebuilds the hit_record of the world object that won (transform chain unwound as translate::hit / rotate_y::hit
@@ -1403,6 +1514,25 @@ __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref,
 template <class R, uint32_t F, bool UV = true>
 __device__ __forceinline__ void world_surface(const DevScene<R>& S, const HitOut& h, const Ray<R>& r, R t, Surf<R>& s) {
     const int32_t w = static_cast<int32_t>(h.obj & 0xFFFFu);
+#ifndef ART_SPH_PREFETCH
+#define ART_SPH_PREFETCH 1
+#endif
+    // A sphere hit's record, loaded first: its address is the hit's primref alone, so its L2 round trip overlaps the
+    // world slot / object loads and the transform arithmetic that prim_surface would otherwise issue it behind
+    constexpr bool kPre = ART_SPH_PREFETCH && (F & F_SPHERE) != 0 && (F & F_XFORM) != 0;
+    [[maybe_unused]] SphPre<R> sph{};
+    if constexpr (kPre) {
+        if (h.prim != kMediumHit && (fbase(F) == F_SPHERE || primref_type(h.prim) == PRIM_SPHERE)) {
+            const SphereRec<R>& sr = S.spheres[primref_index(h.prim)];
+            sph.c = ld3(sr.c);
+            sph.d = ld3(sr.d);
+            sph.r = sr.r;
+            sph.t0 = sr.t0;
+            sph.dt = sr.dt;
+            sph.mat = sr.mat;
+            sph.flags = sr.flags;
+        }
+    }
     int32_t oi = S.world[w];
     ART_STAT_WAVE(44);
     ART_STAT_LANE(45);
@@ -1436,7 +1566,7 @@ __device__ __forceinline__ void world_surface(const DevScene<R>& S, const HitOut
             }
         }
     }
-    prim_surface<R, F, UV>(S, h.prim, h.obj >> 16, r2, t, s, (F & F_TRI) == 0 ? h.mt : kMatUnknown);
+    prim_surface<R, F, UV, kPre>(S, h.prim, h.obj >> 16, r2, t, s, (F & F_TRI) == 0 ? h.mt : kMatUnknown, sph);
     if (!(F & F_XFORM)) return;
 #ifdef ART_STATS
     if (o0 >= 0) {

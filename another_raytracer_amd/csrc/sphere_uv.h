@@ -228,13 +228,15 @@ ART_UV_HD inline double uv_atan2(double y, double x) {
 
 // get_sphere_uv (sphere.h:24-37) of an outward unit normal (ox, oy, oz): theta = acos(-y), phi = atan2(-z, x) + pi,
 // u = phi / (2 pi), v = theta / pi -- the reference's operation order, pi = 3.1415926535897932385 (tracer_utils.h)
-ART_UV_HD inline void sphere_uv(double ox, double oy, double oz, double& u, double& v) {
+struct UvPair {
+    double u, v;
+};
+ART_UV_HD inline UvPair sphere_uv(double ox, double oy, double oz) {
     const UvTab c;
     const double pi = c[kPi];  // 3.1415926535897932385 (tracer_utils.h) is this double
     const double theta = uv_acos(-oy);
     const double phi = uv_atan2(-oz, ox) + pi;
-    u = phi / c[kTwoPi];
-    v = theta / pi;
+    return UvPair{phi / c[kTwoPi], theta / pi};
 }
 
 }  // namespace art

@@ -82,7 +82,9 @@ int main(int argc, char** argv) {
             atan2_bad += et != 0;
             const double u0 = (gt + pi) / (2.0 * pi), v0 = ga / pi;
             double u1, v1;
-            art::sphere_uv(x, y, z, u1, v1);
+            const art::UvPair w1 = art::sphere_uv(x, y, z);
+            u1 = w1.u;
+            v1 = w1.v;
             ubad += std::memcmp(&u0, &u1, 8) != 0 && !(std::isnan(u0) && std::isnan(u1));
             vbad += std::memcmp(&v0, &v1, 8) != 0 && !(std::isnan(v0) && std::isnan(v1));
             int i0, j0, i1, j1;

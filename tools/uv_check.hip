@@ -23,7 +23,9 @@ __global__ void k_uv(const double* n, double* uv, uint32_t count) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= count) return;
     double u, v;
-    art::sphere_uv(n[3 * k], n[3 * k + 1], n[3 * k + 2], u, v);  // device.h prim_surface's call
+    const art::UvPair w = art::sphere_uv(n[3 * k], n[3 * k + 1], n[3 * k + 2]);  // device.h prim_surface's call
+    u = w.u;
+    v = w.v;
     uv[2 * k] = u;
     uv[2 * k + 1] = v;
 }
@@ -108,7 +110,9 @@ int main() {
             texel(uv[2 * k], uv[2 * k + 1], W, H, i1, j1);
             tbad += (i0 != i1 || j0 != j1);
             double hu, hv;
-            art::sphere_uv(x, y, z, hu, hv);
+            const art::UvPair hw = art::sphere_uv(x, y, z);
+            hu = hw.u;
+            hv = hw.v;
             hbad += bits(hu) != bits(uv[2 * k]) || bits(hv) != bits(uv[2 * k + 1]);
         }
         std::printf(", \"%s\": {\"u_bits_differ\": %llu, \"v_bits_differ\": %llu, \"texel_differs\": %llu, \"device_vs_host\": %llu}", names[t],
