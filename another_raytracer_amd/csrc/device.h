@@ -541,14 +541,7 @@ __device__ __forceinline__ void cas(float& ka, int32_t& ca, float& kb, int32_t& 
 #ifndef ART_LDS_LEAF_NOREF
 #define ART_LDS_LEAF_NOREF 0  // 1 (k_paths object, Makefile PATHS_NOREF): the leaf test skips the per-slot code
 #endif
-// ART_COOP_LEAF (experiment, k_paths only): the wave-cooperative leaf test.  A leaf phase's tests (up to 8 per lane)
-// are spread over the lanes still traversing, one test per lane, instead of each lane looping over its own; the
-// owner then folds its tests' results in its own order.  Per-wave LDS scratch: [0, 64) the lane of each rank,
-// [64, 192) the phase's tests (slot | owner lane << 10).
-#ifndef ART_COOP_LEAF
-#define ART_COOP_LEAF 0
-#endif
-constexpr uint32_t kCoopLeafWaveBytes = 192;
+
 // Leaf slot test of the LDS scene image (layout.h): the same root selection as hit_sphere on the same f64 values.
 // d_a = |d|^2 and d_inv_a = 1 / d_a come from the traversal (once per ray).  The image sits at LDS address 0, so
 // every read takes an integer LDS byte address (one shift-add, the plane offset folded in).  Moving spheres of the
@@ -994,63 +987,6 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
             first2 = leaf_first(leaf2) - cnt;
             cnt12 = cnt + leaf_count(leaf2);
         }
-#if ART_COOP_LEAF
-        if constexpr (L && ART_LDS_LEAF_NOREF) {
-            // the phase's tests numbered in lane order: this lane's are [pre, pre + cnt12) of total
-            const uint32_t lane = __lane_id();
-            const uint64_t below = (1ull << lane) - 1ull;
-            const uint64_t act = __ballot(true);
-            uint32_t total = 0, pre = 0;
-            for (int b = 0; b < 4; ++b) {
-                const uint64_t m = __ballot((cnt12 >> b) & 1u);
-                total += static_cast<uint32_t>(__popcll(m)) << b;
-                pre += static_cast<uint32_t>(__popcll(m & below)) << b;
-            }
-            const uint32_t nact = static_cast<uint32_t>(__popcll(act));
-            if (total <= nact && total > 1) {  // one test per lane (more tests than lanes: the loop below)
-                const uint32_t rank = static_cast<uint32_t>(__popcll(act & below));
-                const uint32_t base = S.nodes_lds;
-                *(__attribute__((address_space(3))) uint8_t*)(size_t)(base + rank) = static_cast<uint8_t>(lane);
-                for (uint32_t k = 0; k < cnt12; ++k) {
-                    const uint32_t slot = (k < cnt ? first : first2) + k;
-                    *(__attribute__((address_space(3))) uint16_t*)(size_t)(base + 64u + 2u * (pre + k)) = static_cast<uint16_t>(slot | (lane << 10));
-                }
-                __builtin_amdgcn_wave_barrier();
-                __asm__ volatile("" ::: "memory");
-                // test number `rank`, for its owner's ray (every active lane takes part in the shuffles)
-                const uint32_t e = *(__attribute__((address_space(3))) const uint16_t*)(size_t)(base + 64u + 2u * (rank < total ? rank : 0u));
-                const int o = static_cast<int>(e >> 10);
-                Ray<double> ro;
-                ro.o = mk(__shfl(r.o.x, o), __shfl(r.o.y, o), __shfl(r.o.z, o));
-                ro.d = mk(__shfl(r.d.x, o), __shfl(r.d.y, o), __shfl(r.d.z, o));
-                ro.tm = __shfl(r.tm, o);
-                const double da = __shfl(d_a, o), dia = __shfl(d_inv_a, o), tmn = __shfl(tmin, o), tmx = __shfl(tmax, o);
-                double wt = 0.0;
-                uint32_t pr, mm;
-                const bool wh = hit_lds_slot(lds, e & 1023u, ro, da, dia, tmn, tmx, wt, pr, mm) && rank < total;
-                // the owner folds its tests in order (a result t <= the tmax so far is what the sequential test would
-                // have accepted: the root choices against a larger tmax differ only above it)
-                for (uint32_t k = 0; __ballot(k < cnt12) != 0; ++k) {
-                    const uint32_t j = pre + k;
-                    const int wl = static_cast<int>(*(__attribute__((address_space(3))) const uint8_t*)(size_t)(base + (j < 64u ? j : 0u)));
-                    const int hk = __shfl(static_cast<int>(wh), wl);
-                    const double tk = __shfl(wt, wl);
-                    if (k < cnt12 && hk && !(tmax < tk)) {
-                        tmax = tk;
-                        t = tk;
-                        prim = 0;
-                        face = (k < cnt ? first : first2) + k;
-                        mt = kMatUnknown;
-                        hit = true;
-                        tmaxf = f_hi(tk);
-                    }
-                }
-                __builtin_amdgcn_wave_barrier();
-                __asm__ volatile("" ::: "memory");
-                continue;
-            }
-        }
-#endif
 #ifdef ART_STATS
         if (stats_phase) {  // the cooperative leaf test's iterations: the phase's tests spread over the lanes still here
             uint32_t total = 0;
@@ -1394,18 +1330,9 @@ __device__ __forceinline__ void rect_surface(V3<R>& p, V3<R>& n, bool& ff, R& su
 // mat_hint (HitOut::mt of a triangle-free HBM-scene kernel): the hit's material index, kMatUnknown otherwise.  With it,
 // a box or rect hit whose material samples no u,v builds its surface from the face / axis alone -- normal, point,
 // material -- without reloading the primitive record (its bounds only feed u, v).
-// A sphere record's fields as scalars (world_surface's prefetch: no array members, nothing for the compiler to keep in
-// private memory)
-template <class R>
-struct SphPre {
-    V3<R> c, d;
-    R r, t0, dt;
-    uint32_t mat, flags;
-};
-// PRE: a sphere hit's record was loaded by the caller into sph_pre (world_surface's prefetch).
-template <class R, uint32_t F, bool UV = true, bool PRE = false>
+template <class R, uint32_t F, bool UV = true>
 __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref, uint32_t face, const Ray<R>& r, R t, Surf<R>& s,
-                                             uint32_t mat_hint = kMatUnknown, const SphPre<R>& sph_pre = SphPre<R>{}) {
+                                             uint32_t mat_hint = kMatUnknown) {
     const uint32_t idx = primref_index(ref);
     const uint32_t type = (fbase(F) == F_SPHERE) ? PRIM_SPHERE : primref_type(ref);
     V3<R> sp_p = mk(R(0), R(0), R(0)), sp_n = mk(R(0), R(0), R(0));
@@ -1416,22 +1343,10 @@ __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref,
         case PRIM_SPHERE: {  // sphere.h:57-63, :24-37
             ART_STAT_WAVE(40);
             ART_STAT_LANE(41);
-            SphPre<R> sp;
-            if constexpr (PRE) {
-                sp = sph_pre;
-            } else {
-                const SphereRec<R>& sr = S.spheres[idx];
-                sp.c = ld3(sr.c);
-                sp.d = ld3(sr.d);
-                sp.r = sr.r;
-                sp.t0 = sr.t0;
-                sp.dt = sr.dt;
-                sp.mat = sr.mat;
-                sp.flags = sr.flags;
-            }
-            V3<R> center = sp.c;
+            const SphereRec<R>& sp = S.spheres[idx];
+            V3<R> center = ld3(sp.c);
             const bool moving = (sp.flags & SPH_MOVING) != 0;
-            if (moving) center = center + motion_fraction(r.tm, sp.t0, sp.dt) * sp.d;
+            if (moving) center = center + motion_fraction(r.tm, sp.t0, sp.dt) * ld3(sp.d);
             sp_p = r.at(t);
             const V3<R> outward = divs(sp_p - center, sp.r);
             face_normal(r, outward, ff, sp_n);
@@ -1514,25 +1429,6 @@ __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref,
 template <class R, uint32_t F, bool UV = true>
 __device__ __forceinline__ void world_surface(const DevScene<R>& S, const HitOut& h, const Ray<R>& r, R t, Surf<R>& s) {
     const int32_t w = static_cast<int32_t>(h.obj & 0xFFFFu);
-#ifndef ART_SPH_PREFETCH
-#define ART_SPH_PREFETCH 1
-#endif
-    // A sphere hit's record, loaded first: its address is the hit's primref alone, so its L2 round trip overlaps the
-    // world slot / object loads and the transform arithmetic that prim_surface would otherwise issue it behind
-    constexpr bool kPre = ART_SPH_PREFETCH && (F & F_SPHERE) != 0 && (F & F_XFORM) != 0;
-    [[maybe_unused]] SphPre<R> sph{};
-    if constexpr (kPre) {
-        if (h.prim != kMediumHit && (fbase(F) == F_SPHERE || primref_type(h.prim) == PRIM_SPHERE)) {
-            const SphereRec<R>& sr = S.spheres[primref_index(h.prim)];
-            sph.c = ld3(sr.c);
-            sph.d = ld3(sr.d);
-            sph.r = sr.r;
-            sph.t0 = sr.t0;
-            sph.dt = sr.dt;
-            sph.mat = sr.mat;
-            sph.flags = sr.flags;
-        }
-    }
     int32_t oi = S.world[w];
     ART_STAT_WAVE(44);
     ART_STAT_LANE(45);
@@ -1566,7 +1462,7 @@ __device__ __forceinline__ void world_surface(const DevScene<R>& S, const HitOut
             }
         }
     }
-    prim_surface<R, F, UV, kPre>(S, h.prim, h.obj >> 16, r2, t, s, (F & F_TRI) == 0 ? h.mt : kMatUnknown, sph);
+    prim_surface<R, F, UV>(S, h.prim, h.obj >> 16, r2, t, s, (F & F_TRI) == 0 ? h.mt : kMatUnknown);
     if (!(F & F_XFORM)) return;
 #ifdef ART_STATS
     if (o0 >= 0) {

@@ -760,9 +760,7 @@ constexpr size_t kPathsWorldBytes = sizeof(int32_t) * kPathsWorldCap + sizeof(Ob
 __host__ __device__ constexpr size_t paths_lds_head(uint32_t stack) {
     return ((kLdsImageBytes + paths_stack_bytes(stack) + kJumpBytes + sizeof(CameraRec<double>) + sizeof(PassGeom)) + 15u) & ~size_t(15);
 }
-// ART_COOP_LEAF (experiment, device.h traverse): per-wave scratch of the wave-cooperative leaf test after the world
-constexpr size_t kCoopLeafBytes = ART_COOP_LEAF ? (kBlockL / 64) * kCoopLeafWaveBytes : 0;
-__host__ __device__ constexpr size_t paths_lds_bytes(uint32_t stack) { return paths_lds_head(stack) + kPathsWorldBytes + kCoopLeafBytes; }
+__host__ __device__ constexpr size_t paths_lds_bytes(uint32_t stack) { return paths_lds_head(stack) + kPathsWorldBytes; }
 #if ART_SPLIT_PATHS == 0 || ART_SPLIT_PATHS == 2
 __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S0, PassGeom g, CameraRec<double> cam, Work<double> w, uint32_t* next_slot) {
     using R = double;
@@ -793,8 +791,6 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S0, PassG
             reinterpret_cast<uint4*>(ob)[threadIdx.x] = reinterpret_cast<const uint4*>(S0.objs)[threadIdx.x];
         S.world = reinterpret_cast<const int32_t*>(wb);
         S.objs = reinterpret_cast<const ObjRec<double>*>(ob);
-        if constexpr (ART_COOP_LEAF != 0)  // this wave's cooperative-leaf scratch (LDS byte address; nodes_lds is unused here)
-            S.nodes_lds = static_cast<uint32_t>(paths_lds_head(g.stack) + kPathsWorldBytes) + (threadIdx.x / 64u) * kCoopLeafWaveBytes;
     }
     __syncthreads();
     const uint32_t lane = __lane_id();
@@ -1032,14 +1028,9 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
     unsigned long long tm_load = 0, tm_trace = 0, tm_shade = 0, tm_app = 0, tm_prev = __builtin_amdgcn_s_memtime();
     unsigned long long tm_surf = 0, tm_coop = 0, tm_tex = 0;  // the shading phase split (k_paths_g)
 #endif
-#ifndef ART_START_MIN_G
-#define ART_START_MIN_G 1
-#endif
     for (;;) {
         const uint64_t idle = __ballot(!busy && !drained);
-        // path starts (the camera-ray code, run by the wave for however few lanes start) only once ART_START_MIN_G lanes
-        // are idle or none is busy
-        if (idle && (ART_START_MIN_G <= 1 || __popcll(idle) >= ART_START_MIN_G || __ballot(busy) == 0)) {
+        if (idle) {
             const uint32_t n = static_cast<uint32_t>(__popcll(idle));
             const uint32_t rank = static_cast<uint32_t>(__popcll(idle & below));
             uint32_t slot;

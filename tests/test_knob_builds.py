@@ -17,15 +17,12 @@ HIPCC = "/opt/rocm/bin/hipcc"
 
 # knob sets, each compiled once (sets combine knobs that do not interact, to keep the CPU suite short)
 VARIANTS = {
-    "stats": ["-DART_SPLIT_PATHS=0", "-DART_STATS", "-DART_SUSPEND_LANES=0", "-DART_POOL_RING=128", "-DART_LDS_NODE_CAP=320", "-DART_START_MIN_G=8"],
-    "trace": ["-DART_SPLIT_PATHS=0", "-DART_TRACE", "-DART_PATHS_G_WAVES=2", "-DART_EXTEND_MIN_WAVES=2", "-DART_LDS_LEAF_NOREF=1", "-DART_SPH_PREFETCH=0"],
+    "stats": ["-DART_SPLIT_PATHS=0", "-DART_STATS", "-DART_SUSPEND_LANES=0", "-DART_POOL_RING=128", "-DART_LDS_NODE_CAP=320"],
+    "trace": ["-DART_SPLIT_PATHS=0", "-DART_TRACE", "-DART_PATHS_G_WAVES=2", "-DART_EXTEND_MIN_WAVES=2", "-DART_LDS_LEAF_NOREF=1"],
     "paths_ref": ["-DART_SPLIT_PATHS=2", "-DART_LDS_LEAF_NOREF=0", "-DART_SUSPEND_LANES=16"],
-    "coop_leaf": ["-DART_SPLIT_PATHS=2", "-DART_LDS_LEAF_NOREF=1", "-DART_COOP_LEAF=1"],
 }
 SURVIVING = {"ART_STATS", "ART_TRACE", "ART_SPLIT_PATHS", "ART_SPLIT_MESH", "ART_LDS_LEAF_NOREF", "ART_SUSPEND_LANES", "ART_PATHS_G_WAVES",
-             "ART_POOL_RING", "ART_LDS_NODE_CAP", "ART_EXTEND_MIN_WAVES", "ART_LDS_BLOCK",
-             # r4 experiments awaiting their A/B: a losing one is deleted from the sources
-             "ART_SPH_PREFETCH", "ART_START_MIN_G", "ART_COOP_LEAF"}
+             "ART_POOL_RING", "ART_LDS_NODE_CAP", "ART_EXTEND_MIN_WAVES", "ART_LDS_BLOCK"}
 
 
 def _compile(args, out):
