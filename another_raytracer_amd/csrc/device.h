@@ -232,6 +232,7 @@ struct DevScene {
     const PrimRec80* leaf_prims;  // leaf_prims[slot]: the record of primrefs[slot] of any type (triangle-free kernels)
     const PrimRec80* obj_prims;  // obj_prims[o] = the record of prim object o's primitive (indexed like objs)
     const uint8_t* lds_image;   // layout.h LDS scene image (nullptr unless the scene qualifies)
+    const double* uv_coef;      // sphere_uv.h coefficients (a device copy of kUvCoefHost; k_paths_g: its LDS copy)
     uint32_t n_nodes, n_primrefs, n_tris, n_objs, n_mats;  // array lengths (k_paths_g's LDS copies)
     uint32_t nodes_lds;         // k_paths_g LM 2: LDS byte address of the copy of nodes [0, n_lds_nodes) (top levels)
     uint32_t n_lds_nodes;
@@ -1356,7 +1357,7 @@ __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref,
                 ART_STAT_LANE(33);
                 // get_sphere_uv (sphere.h:24-37) with sphere_uv.h's acos / atan2 (their coefficients are loaded where
                 // used, not hoisted into the path loop's registers)
-                const UvPair uv = sphere_uv(static_cast<double>(outward.x), static_cast<double>(outward.y), static_cast<double>(outward.z));
+                const UvPair uv = sphere_uv(static_cast<double>(outward.x), static_cast<double>(outward.y), static_cast<double>(outward.z), S.uv_coef);
                 su = R(uv.u);
                 sv = R(uv.v);
             }

@@ -901,8 +901,9 @@ __host__ __device__ constexpr size_t align16(size_t x) { return (x + 15u) & ~siz
 __host__ __device__ constexpr size_t align128(size_t x) { return (x + 127u) & ~size_t(127); }
 // s16: 16-bit stack entries (F_CODE16 instantiations, device.h StackF)
 __host__ __device__ constexpr size_t paths_g_stack_bytes(uint32_t stack, int block, bool s16) { return (s16 ? 2u : 4u) * stack * block; }
-__host__ __device__ constexpr size_t paths_g_head_bytes(uint32_t stack, int block, bool s16) {  // stack, camera, pass geometry, jumps
-    return align16(paths_g_stack_bytes(stack, block, s16) + sizeof(CameraRec<double>) + sizeof(PassGeom)) + kJumpBytes;
+constexpr size_t kUvCoefBytes = (sizeof(double) * kUvCoefs + 15u) & ~size_t(15);  // sphere_uv.h's table, LDS copy
+__host__ __device__ constexpr size_t paths_g_head_bytes(uint32_t stack, int block, bool s16) {  // stack, camera, pass geometry, jumps, u,v
+    return align16(paths_g_stack_bytes(stack, block, s16) + sizeof(CameraRec<double>) + sizeof(PassGeom)) + kJumpBytes + kUvCoefBytes;
 }
 // LM kernels also hold the world list and the object records (a few KiB): every segment walks them, and a prim
 // object's test otherwise waits on three dependent L1 loads (world slot -> object -> primitive).  The textured ones
@@ -948,6 +949,11 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
     [[maybe_unused]] JumpEntry* jt = reinterpret_cast<JumpEntry*>(smem + align16(paths_g_stack_bytes(g.stack, B, S16) + sizeof(CameraRec<double>) + sizeof(PassGeom)));
     if (threadIdx.x < static_cast<uint32_t>(kJumpEntries)) jt[threadIdx.x] = pcg_jump(3u * threadIdx.x);
     DevScene<double> S = S0;
+    if constexpr ((TF & TF_IMAGE) != 0) {  // sphere u, v coefficients from LDS (ds_read at each use, nothing hoisted)
+        double* uc = reinterpret_cast<double*>(jt + kJumpEntries);
+        if (threadIdx.x < static_cast<uint32_t>(kUvCoefs)) uc[threadIdx.x] = S0.uv_coef[threadIdx.x];
+        S.uv_coef = uc;
+    }
     size_t lm_off = paths_g_head_bytes(g.stack, B, S16);  // LM: world list and objects, then the BVH arrays
     if constexpr (LM != 0) {
         uint8_t* wb = smem + lm_off;
@@ -1809,6 +1815,7 @@ static void build_device_scene(const FlatScene& f, DeviceScene<R>& ds) {
     ds.view.perlins = ds.upload(per);
     ds.view.images = ds.upload(f.images);
     ds.view.texels = ds.upload(f.texels);
+    ds.view.uv_coef = ds.upload(std::vector<double>(kUvCoefHost, kUvCoefHost + kUvCoefs));
     if (std::is_same<R, double>::value) {
         uint32_t nmov = 0;
         bool shade_ok = false;

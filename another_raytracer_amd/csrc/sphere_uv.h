@@ -10,8 +10,11 @@
 //
 // What this header buys is control of the code.  The device library's acos / atan2 materialise ~30 f64 polynomial
 // constants that the compiler hoists out of k_paths_g's path loop and spills to scratch at kernel start (the Next-Week
-// final's kernel: 50+ spilled VGPRs).  Here the coefficients live in one table read through an opaque zero offset, so
-// every use is a scalar load inside the (rarely executed) u, v code and nothing is hoisted.  The algorithms are
+// final's kernel: 50+ spilled VGPRs).  Here the coefficients are read from a table the caller passes (DevScene::uv_coef:
+// a device copy of kUvCoefHost, or k_paths_g's LDS copy of it), so every use is a load inside the (rarely executed)
+// u, v code: nothing is hoisted into the path loop's registers.  (A __constant__ table read through an opaque zero
+// offset was r4's first form: its scalar loads were merged into 16-dword batches whose SGPRs spilled into VGPR lanes,
+// ~300 v_readlane per evaluation.)  The algorithms are
 // fdlibm 5.3's (Sun Microsystems; e_acos.c rational approximation, s_atan.c four-interval reduction, e_atan2.c
 // quadrants), accurate to < 1 ulp, with one change: atan2 returns +-pio2_hi once |y / x| > 2^60 in every quadrant (the
 // correct rounding, as glibc gives it; fdlibm is 1 ulp high for x < 0) -- tests/test_sphere_uv.py measures them against glibc and the texel choices they
@@ -49,27 +52,13 @@ enum UvCoef : int {
     3.14159265358979311600e+00, 1.57079632679489655800e+00, 6.12323399573676603587e-17, 1.2246467991473531772e-16, \
     1.5, 1.0e-300, \
     2.0 * 3.1415926535897932385
-// The device reads its own copy (constant memory); a HIP translation unit's host side reads the plain one (the host
-// shadow of a __constant__ variable holds no initialiser).
+// The host's table; the device reads a copy of it (DevScene::uv_coef, uploaded with the scene).
 static const double kUvCoefHost[kUvCoefs] = {ART_UV_COEFS};
-#if defined(__HIPCC__)
-__constant__ static const double kUvCoefDev[kUvCoefs] = {ART_UV_COEFS};
-#endif
 #undef ART_UV_COEFS
 
-// The coefficient table with an offset the compiler cannot see through (device): each coefficient is a scalar load at
-// its use, never a value hoisted into a register for the life of the path loop.
 struct UvTab {
     const double* t;
-    ART_UV_HD explicit UvTab() {
-#if defined(__HIP_DEVICE_COMPILE__)
-        uint32_t z;
-        __asm__ volatile("s_mov_b32 %0, 0" : "=s"(z));
-        t = kUvCoefDev + z;
-#else
-        t = kUvCoefHost;
-#endif
-    }
+    ART_UV_HD explicit UvTab(const double* p) : t(p) {}
     ART_UV_HD double operator[](int k) const { return t[k]; }
 };
 
@@ -94,8 +83,7 @@ ART_UV_HD inline double uv_sqrt(double x) {
 }
 
 // fdlibm e_acos.c
-ART_UV_HD inline double uv_acos(double x) {
-    const UvTab c;
+ART_UV_HD inline double uv_acos(double x, const UvTab& c) {
     const uint64_t b = uv_bits(x);
     const int32_t hx = static_cast<int32_t>(b >> 32);
     const int32_t ix = hx & 0x7fffffff;
@@ -167,8 +155,7 @@ ART_UV_HD inline double uv_atan_pos(double x, const UvTab& c) {
 }
 
 // fdlibm e_atan2.c (finite arguments: the components of a unit normal; inf / NaN handled as fdlibm does)
-ART_UV_HD inline double uv_atan2(double y, double x) {
-    const UvTab c;
+ART_UV_HD inline double uv_atan2(double y, double x, const UvTab& c) {
     const uint64_t bx = uv_bits(x), by = uv_bits(y);
     const int32_t hx = static_cast<int32_t>(bx >> 32), hy = static_cast<int32_t>(by >> 32);
     const int32_t ix = hx & 0x7fffffff, iy = hy & 0x7fffffff;
@@ -231,12 +218,17 @@ ART_UV_HD inline double uv_atan2(double y, double x) {
 struct UvPair {
     double u, v;
 };
-ART_UV_HD inline UvPair sphere_uv(double ox, double oy, double oz) {
-    const UvTab c;
+// coef: the kUvCoefHost table or a copy of it
+ART_UV_HD inline UvPair sphere_uv(double ox, double oy, double oz, const double* coef) {
+    const UvTab c(coef);
     const double pi = c[kPi];  // 3.1415926535897932385 (tracer_utils.h) is this double
-    const double theta = uv_acos(-oy);
-    const double phi = uv_atan2(-oz, ox) + pi;
+    const double theta = uv_acos(-oy, c);
+    const double phi = uv_atan2(-oz, ox, c) + pi;
     return UvPair{phi / c[kTwoPi], theta / pi};
 }
+// host callers (tests, tools): the host table
+inline double uv_acos(double x) { return uv_acos(x, UvTab(kUvCoefHost)); }
+inline double uv_atan2(double y, double x) { return uv_atan2(y, x, UvTab(kUvCoefHost)); }
+inline UvPair sphere_uv(double ox, double oy, double oz) { return sphere_uv(ox, oy, oz, kUvCoefHost); }
 
 }  // namespace art

@@ -19,11 +19,11 @@
 #include <cstring>
 #include <vector>
 
-__global__ void k_uv(const double* n, double* uv, uint32_t count) {
+__global__ void k_uv(const double* n, double* uv, uint32_t count, const double* coef) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= count) return;
     double u, v;
-    const art::UvPair w = art::sphere_uv(n[3 * k], n[3 * k + 1], n[3 * k + 2]);  // device.h prim_surface's call
+    const art::UvPair w = art::sphere_uv(n[3 * k], n[3 * k + 1], n[3 * k + 2], coef);  // device.h prim_surface's call
     u = w.u;
     v = w.v;
     uv[2 * k] = u;
@@ -90,13 +90,17 @@ int main() {
         sets[1][3 * k + 2] = nudge(z, dz);
     }
     double *dn = nullptr, *duv = nullptr;
-    if (hipMalloc(&dn, sizeof(double) * 3 * n) != hipSuccess || hipMalloc(&duv, sizeof(double) * 2 * n) != hipSuccess) return 2;
+    double* dcoef = nullptr;
+    if (hipMalloc(&dn, sizeof(double) * 3 * n) != hipSuccess || hipMalloc(&duv, sizeof(double) * 2 * n) != hipSuccess ||
+        hipMalloc(&dcoef, sizeof(art::kUvCoefHost)) != hipSuccess)
+        return 2;
+    if (hipMemcpy(dcoef, art::kUvCoefHost, sizeof(art::kUvCoefHost), hipMemcpyHostToDevice) != hipSuccess) return 2;
     std::vector<double> uv(2 * size_t(n));
     const char* names[2] = {"random", "adversarial"};
     std::printf("{\"normals_per_set\": %u, \"texture\": [%d, %d]", n, W, H);
     for (int t = 0; t < 2; ++t) {
         if (hipMemcpy(dn, sets[t].data(), sizeof(double) * 3 * n, hipMemcpyHostToDevice) != hipSuccess) return 2;
-        hipLaunchKernelGGL(k_uv, dim3(n / 256), dim3(256), 0, 0, dn, duv, n);
+        hipLaunchKernelGGL(k_uv, dim3(n / 256), dim3(256), 0, 0, dn, duv, n, dcoef);
         if (hipMemcpy(uv.data(), duv, sizeof(double) * 2 * n, hipMemcpyDeviceToHost) != hipSuccess) return 2;
         uint64_t ubad = 0, vbad = 0, tbad = 0, hbad = 0;
         for (uint32_t k = 0; k < n; ++k) {
