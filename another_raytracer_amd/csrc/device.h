@@ -232,13 +232,20 @@ struct DevScene {
     const PrimRec80* leaf_prims;  // leaf_prims[slot]: the record of primrefs[slot] of any type (triangle-free kernels)
     const PrimRec80* obj_prims;  // obj_prims[o] = the record of prim object o's primitive (indexed like objs)
     const uint8_t* lds_image;   // layout.h LDS scene image (nullptr unless the scene qualifies)
-    const double* uv_coef;      // sphere_uv.h coefficients (a device copy of kUvCoefHost; k_paths_g: its LDS copy)
     uint32_t n_nodes, n_primrefs, n_tris, n_objs, n_mats;  // array lengths (k_paths_g's LDS copies)
     uint32_t nodes_lds;         // k_paths_g LM 2: LDS byte address of the copy of nodes [0, n_lds_nodes) (top levels)
     uint32_t n_lds_nodes;
     int32_t nworld;
     R bg[3];
 };
+
+// sphere_uv.h's coefficient table rides in front of the image records (DevScene::images - kUvTableBytes, uploaded with
+// them), so the scene view -- the kernels' argument block -- keeps its layout (a new field moved every later kernel
+// argument and cost k_paths 0.3 %)
+template <class R>
+__device__ __forceinline__ const double* uv_table(const DevScene<R>& S) {
+    return reinterpret_cast<const double*>(reinterpret_cast<const uint8_t*>(S.images) - kUvTableBytes);
+}
 
 constexpr uint32_t kMediumHit = 0xFFFFFFFFu;  // hit.prim value of a constant_medium scattering event
 
@@ -1331,9 +1338,10 @@ __device__ __forceinline__ void rect_surface(V3<R>& p, V3<R>& n, bool& ff, R& su
 // mat_hint (HitOut::mt of a triangle-free HBM-scene kernel): the hit's material index, kMatUnknown otherwise.  With it,
 // a box or rect hit whose material samples no u,v builds its surface from the face / axis alone -- normal, point,
 // material -- without reloading the primitive record (its bounds only feed u, v).
+// uvc: sphere_uv.h's table (uv_table(S) or an LDS copy; read only when UV)
 template <class R, uint32_t F, bool UV = true>
 __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref, uint32_t face, const Ray<R>& r, R t, Surf<R>& s,
-                                             uint32_t mat_hint = kMatUnknown) {
+                                             uint32_t mat_hint, const double* uvc) {
     const uint32_t idx = primref_index(ref);
     const uint32_t type = (fbase(F) == F_SPHERE) ? PRIM_SPHERE : primref_type(ref);
     V3<R> sp_p = mk(R(0), R(0), R(0)), sp_n = mk(R(0), R(0), R(0));
@@ -1357,7 +1365,7 @@ __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref,
                 ART_STAT_LANE(33);
                 // get_sphere_uv (sphere.h:24-37) with sphere_uv.h's acos / atan2 (their coefficients are loaded where
                 // used, not hoisted into the path loop's registers)
-                const UvPair uv = sphere_uv(static_cast<double>(outward.x), static_cast<double>(outward.y), static_cast<double>(outward.z), S.uv_coef);
+                const UvPair uv = sphere_uv(static_cast<double>(outward.x), static_cast<double>(outward.y), static_cast<double>(outward.z), uvc);
                 su = R(uv.u);
                 sv = R(uv.v);
             }
@@ -1428,7 +1436,7 @@ __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref,
 // Rebuilds the hit_record of the world object that won (transform chain unwound as translate::hit / rotate_y::hit
 // do it: hittable.cpp:7-11, :72-84, including set_face_normal against the transformed ray).
 template <class R, uint32_t F, bool UV = true>
-__device__ __forceinline__ void world_surface(const DevScene<R>& S, const HitOut& h, const Ray<R>& r, R t, Surf<R>& s) {
+__device__ __forceinline__ void world_surface(const DevScene<R>& S, const HitOut& h, const Ray<R>& r, R t, Surf<R>& s, const double* uvc = nullptr) {
     const int32_t w = static_cast<int32_t>(h.obj & 0xFFFFu);
     int32_t oi = S.world[w];
     ART_STAT_WAVE(44);
@@ -1463,7 +1471,7 @@ __device__ __forceinline__ void world_surface(const DevScene<R>& S, const HitOut
             }
         }
     }
-    prim_surface<R, F, UV>(S, h.prim, h.obj >> 16, r2, t, s, (F & F_TRI) == 0 ? h.mt : kMatUnknown);
+    prim_surface<R, F, UV>(S, h.prim, h.obj >> 16, r2, t, s, (F & F_TRI) == 0 ? h.mt : kMatUnknown, uvc);
     if (!(F & F_XFORM)) return;
 #ifdef ART_STATS
     if (o0 >= 0) {

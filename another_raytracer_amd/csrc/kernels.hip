@@ -901,9 +901,8 @@ __host__ __device__ constexpr size_t align16(size_t x) { return (x + 15u) & ~siz
 __host__ __device__ constexpr size_t align128(size_t x) { return (x + 127u) & ~size_t(127); }
 // s16: 16-bit stack entries (F_CODE16 instantiations, device.h StackF)
 __host__ __device__ constexpr size_t paths_g_stack_bytes(uint32_t stack, int block, bool s16) { return (s16 ? 2u : 4u) * stack * block; }
-constexpr size_t kUvCoefBytes = (sizeof(double) * kUvCoefs + 15u) & ~size_t(15);  // sphere_uv.h's table, LDS copy
 __host__ __device__ constexpr size_t paths_g_head_bytes(uint32_t stack, int block, bool s16) {  // stack, camera, pass geometry, jumps, u,v
-    return align16(paths_g_stack_bytes(stack, block, s16) + sizeof(CameraRec<double>) + sizeof(PassGeom)) + kJumpBytes + kUvCoefBytes;
+    return align16(paths_g_stack_bytes(stack, block, s16) + sizeof(CameraRec<double>) + sizeof(PassGeom)) + kJumpBytes + kUvTableBytes;
 }
 // LM kernels also hold the world list and the object records (a few KiB): every segment walks them, and a prim
 // object's test otherwise waits on three dependent L1 loads (world slot -> object -> primitive).  The textured ones
@@ -949,11 +948,9 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
     [[maybe_unused]] JumpEntry* jt = reinterpret_cast<JumpEntry*>(smem + align16(paths_g_stack_bytes(g.stack, B, S16) + sizeof(CameraRec<double>) + sizeof(PassGeom)));
     if (threadIdx.x < static_cast<uint32_t>(kJumpEntries)) jt[threadIdx.x] = pcg_jump(3u * threadIdx.x);
     DevScene<double> S = S0;
-    if constexpr ((TF & TF_IMAGE) != 0) {  // sphere u, v coefficients from LDS (ds_read at each use, nothing hoisted)
-        double* uc = reinterpret_cast<double*>(jt + kJumpEntries);
-        if (threadIdx.x < static_cast<uint32_t>(kUvCoefs)) uc[threadIdx.x] = S0.uv_coef[threadIdx.x];
-        S.uv_coef = uc;
-    }
+    [[maybe_unused]] double* uvc = reinterpret_cast<double*>(jt + kJumpEntries);  // sphere u, v coefficients, LDS copy
+    if constexpr ((TF & TF_IMAGE) != 0)
+        if (threadIdx.x < static_cast<uint32_t>(kUvCoefs)) uvc[threadIdx.x] = uv_table(S0)[threadIdx.x];
     size_t lm_off = paths_g_head_bytes(g.stack, B, S16);  // LM: world list and objects, then the BVH arrays
     if constexpr (LM != 0) {
         uint8_t* wb = smem + lm_off;
@@ -1107,7 +1104,7 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
             susp = in_trace;  // suspended: nothing to shade this round
             ART_TICK(tm_trace);
             if (!susp && hitw) {
-                world_surface<R, F, (TF & TF_IMAGE) != 0>(S, h, st.ray, t, s);
+                world_surface<R, F, (TF & TF_IMAGE) != 0>(S, h, st.ray, t, s, uvc);
                 mtype = S.mats[s.mat].type;
             }
         }
@@ -1239,7 +1236,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(DevScene<R> S, PassGeom g, Wor
             load_path(w.paths, q, st, true);
             const HitRecD<R> h = w.hits[q];
             Surf<R> s;
-            world_surface<R, F, (TF & TF_IMAGE) != 0>(S, HitOut{h.prim, h.obj, kMatUnknown}, st.ray, h.t, s);
+            world_surface<R, F, (TF & TF_IMAGE) != 0>(S, HitOut{h.prim, h.obj, kMatUnknown}, st.ray, h.t, s, uv_table(S));
             const MatRec<R>& mat = S.mats[s.mat];
             if (M == MAT_LIGHT) st.L = st.L + st.T * mat_tex_value<R, TF>(S, mat, s.u, s.v, s.p);  // material.h:114-116
             if (M != MAT_LIGHT && !last) {
@@ -1813,9 +1810,13 @@ static void build_device_scene(const FlatScene& f, DeviceScene<R>& ds) {
     ds.view.mats = ds.upload(mats);
     ds.view.texs = ds.upload(texs);
     ds.view.perlins = ds.upload(per);
-    ds.view.images = ds.upload(f.images);
+    {  // [sphere_uv.h's table][image records]: device.h uv_table reads the table in front of DevScene::images
+        std::vector<uint8_t> ib(kUvTableBytes + sizeof(ImageRec) * f.images.size(), 0);
+        std::memcpy(ib.data(), kUvCoefHost, sizeof(kUvCoefHost));
+        if (!f.images.empty()) std::memcpy(ib.data() + kUvTableBytes, f.images.data(), sizeof(ImageRec) * f.images.size());
+        ds.view.images = reinterpret_cast<const ImageRec*>(ds.upload(ib) + kUvTableBytes);
+    }
     ds.view.texels = ds.upload(f.texels);
-    ds.view.uv_coef = ds.upload(std::vector<double>(kUvCoefHost, kUvCoefHost + kUvCoefs));
     if (std::is_same<R, double>::value) {
         uint32_t nmov = 0;
         bool shade_ok = false;

@@ -10,8 +10,8 @@
 //
 // What this header buys is control of the code.  The device library's acos / atan2 materialise ~30 f64 polynomial
 // constants that the compiler hoists out of k_paths_g's path loop and spills to scratch at kernel start (the Next-Week
-// final's kernel: 50+ spilled VGPRs).  Here the coefficients are read from a table the caller passes (DevScene::uv_coef:
-// a device copy of kUvCoefHost, or k_paths_g's LDS copy of it), so every use is a load inside the (rarely executed)
+// final's kernel: 50+ spilled VGPRs).  Here the coefficients are read from a table the caller passes (device.h
+// uv_table: a device copy of kUvCoefHost, or k_paths_g's LDS copy of it), so every use is a load inside the (rarely executed)
 // u, v code: nothing is hoisted into the path loop's registers.  (A __constant__ table read through an opaque zero
 // offset was r4's first form: its scalar loads were merged into 16-dword batches whose SGPRs spilled into VGPR lanes,
 // ~300 v_readlane per evaluation.)  The algorithms are
@@ -52,8 +52,9 @@ enum UvCoef : int {
     3.14159265358979311600e+00, 1.57079632679489655800e+00, 6.12323399573676603587e-17, 1.2246467991473531772e-16, \
     1.5, 1.0e-300, \
     2.0 * 3.1415926535897932385
-// The host's table; the device reads a copy of it (DevScene::uv_coef, uploaded with the scene).
+// The host's table; the device reads a copy of it (uploaded with the scene: device.h uv_table).
 static const double kUvCoefHost[kUvCoefs] = {ART_UV_COEFS};
+constexpr size_t kUvTableBytes = (sizeof(double) * kUvCoefs + 15u) & ~size_t(15);  // the copy's size, 16-B aligned
 #undef ART_UV_COEFS
 
 struct UvTab {
