@@ -239,8 +239,8 @@ struct DevScene {
     R bg[3];
 };
 
-// sphere_uv.h's coefficient table rides in front of the image records (DevScene::images - kUvTableBytes, uploaded with
-// them), so the scene view -- the kernels' argument block -- keeps its layout (a new field moved every later kernel
+// sphere_uv.h's table (glibc_trig.h's constants, then its acos / atan tables) rides in front of the image records
+// (DevScene::images - kUvTableBytes, uploaded with them), so the scene view -- the kernels' argument block -- keeps its layout (a new field moved every later kernel
 // argument and cost k_paths 0.3 %)
 template <class R>
 __device__ __forceinline__ const double* uv_table(const DevScene<R>& S) {
@@ -1338,7 +1338,8 @@ __device__ __forceinline__ void rect_surface(V3<R>& p, V3<R>& n, bool& ff, R& su
 // mat_hint (HitOut::mt of a triangle-free HBM-scene kernel): the hit's material index, kMatUnknown otherwise.  With it,
 // a box or rect hit whose material samples no u,v builds its surface from the face / axis alone -- normal, point,
 // material -- without reloading the primitive record (its bounds only feed u, v).
-// uvc: sphere_uv.h's table (uv_table(S) or an LDS copy; read only when UV)
+// uvc: glibc_trig.h's constants (uv_table(S) or k_paths_g's LDS copy of its head; read only when UV); the tables
+// behind them are read from uv_table(S)
 template <class R, uint32_t F, bool UV = true>
 __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref, uint32_t face, const Ray<R>& r, R t, Surf<R>& s,
                                              uint32_t mat_hint, const double* uvc) {
@@ -1363,9 +1364,10 @@ __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref,
             if (UV && !moving && (S.mats[sp.mat].flags & MATF_NEEDS_UV)) {
                 ART_STAT_WAVE(32);
                 ART_STAT_LANE(33);
-                // get_sphere_uv (sphere.h:24-37) with sphere_uv.h's acos / atan2 (their coefficients are loaded where
-                // used, not hoisted into the path loop's registers)
-                const UvPair uv = sphere_uv(static_cast<double>(outward.x), static_cast<double>(outward.y), static_cast<double>(outward.z), uvc);
+                // get_sphere_uv (sphere.h:24-37) with glibc's acos / atan2 restated (sphere_uv.h; their constants are
+                // loaded where used, not hoisted into the path loop's registers)
+                const UvPair uv = sphere_uv(static_cast<double>(outward.x), static_cast<double>(outward.y), static_cast<double>(outward.z),
+                                            TrigTab(uvc, uv_table(S)));
                 su = R(uv.u);
                 sv = R(uv.v);
             }

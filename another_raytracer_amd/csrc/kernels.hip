@@ -902,7 +902,7 @@ __host__ __device__ constexpr size_t align128(size_t x) { return (x + 127u) & ~s
 // s16: 16-bit stack entries (F_CODE16 instantiations, device.h StackF)
 __host__ __device__ constexpr size_t paths_g_stack_bytes(uint32_t stack, int block, bool s16) { return (s16 ? 2u : 4u) * stack * block; }
 __host__ __device__ constexpr size_t paths_g_head_bytes(uint32_t stack, int block, bool s16) {  // stack, camera, pass geometry, jumps, u,v
-    return align16(paths_g_stack_bytes(stack, block, s16) + sizeof(CameraRec<double>) + sizeof(PassGeom)) + kJumpBytes + kUvTableBytes;
+    return align16(paths_g_stack_bytes(stack, block, s16) + sizeof(CameraRec<double>) + sizeof(PassGeom)) + kJumpBytes + kUvConstBytes;
 }
 // LM kernels also hold the world list and the object records (a few KiB): every segment walks them, and a prim
 // object's test otherwise waits on three dependent L1 loads (world slot -> object -> primitive).  The textured ones
@@ -948,9 +948,9 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
     [[maybe_unused]] JumpEntry* jt = reinterpret_cast<JumpEntry*>(smem + align16(paths_g_stack_bytes(g.stack, B, S16) + sizeof(CameraRec<double>) + sizeof(PassGeom)));
     if (threadIdx.x < static_cast<uint32_t>(kJumpEntries)) jt[threadIdx.x] = pcg_jump(3u * threadIdx.x);
     DevScene<double> S = S0;
-    [[maybe_unused]] double* uvc = reinterpret_cast<double*>(jt + kJumpEntries);  // sphere u, v coefficients, LDS copy
+    [[maybe_unused]] double* uvc = reinterpret_cast<double*>(jt + kJumpEntries);  // sphere u, v constants, LDS copy
     if constexpr ((TF & TF_IMAGE) != 0)
-        if (threadIdx.x < static_cast<uint32_t>(kUvCoefs)) uvc[threadIdx.x] = uv_table(S0)[threadIdx.x];
+        if (threadIdx.x < static_cast<uint32_t>(kUvConsts)) uvc[threadIdx.x] = uv_table(S0)[threadIdx.x];
     size_t lm_off = paths_g_head_bytes(g.stack, B, S16);  // LM: world list and objects, then the BVH arrays
     if constexpr (LM != 0) {
         uint8_t* wb = smem + lm_off;
@@ -1812,7 +1812,7 @@ static void build_device_scene(const FlatScene& f, DeviceScene<R>& ds) {
     ds.view.perlins = ds.upload(per);
     {  // [sphere_uv.h's table][image records]: device.h uv_table reads the table in front of DevScene::images
         std::vector<uint8_t> ib(kUvTableBytes + sizeof(ImageRec) * f.images.size(), 0);
-        std::memcpy(ib.data(), kUvCoefHost, sizeof(kUvCoefHost));
+        std::memcpy(ib.data(), glibc_trig_data::kTrigHost, sizeof(glibc_trig_data::kTrigHost));
         if (!f.images.empty()) std::memcpy(ib.data() + kUvTableBytes, f.images.data(), sizeof(ImageRec) * f.images.size());
         ds.view.images = reinterpret_cast<const ImageRec*>(ds.upload(ib) + kUvTableBytes);
     }

@@ -1,12 +1,11 @@
-"""get_sphere_uv (sphere.h:24-37) as the product computes it: csrc/sphere_uv.h (fdlibm 5.3 acos / atan2, one code for
-host and device) against glibc's acos / atan2, the reference's libm.  tests/native/sphere_uv_check.cpp is built with
-g++ here and run over 2^20 uniform unit normals and 2^20 normals placed on the earth texture's texel edges
-(1024 x 512, scene_manager.cpp:117) nudged by -4..+4 ulps.
+"""get_sphere_uv (sphere.h:24-37) as the product computes it: csrc/sphere_uv.h (glibc 2.35's acos / atan2 restated in
+glibc_trig.h, one code for host and device) against glibc's acos / atan2, the reference's libm.
+tests/native/sphere_uv_check.cpp is built with g++ here and run over 2^20 uniform unit normals and 2^20 normals placed
+on the earth texture's texel edges (1024 x 512, scene_manager.cpp:117) nudged by -4..+4 ulps.
 
-The bar ("sphere u, v"): glibc is not correctly rounded either, so last bits differ in ~8 % of the calls,
-but never by more than 1 ulp; the exact cases (signed zeros, poles, infinities, huge y / x) agree bit for bit; no
-uniform normal picks a different texel; texel-edge normals built to sit within 4 ulps of an edge disagree at the rate
-any 1-ulp difference implies.  tools/uv_check.hip checks on the GPU that the device computes the host's bits."""
+The bar ("sphere u, v"): every acos / atan2 result, every u and v, and so every texel choice equals the
+reference's, including the exact cases (signed zeros, poles, infinities, huge y / x).  tools/uv_check.hip checks on the
+GPU that the device computes the host's bits over 2^24 normals of each kind."""
 import os
 import re
 import shutil
@@ -33,11 +32,11 @@ def report(tmp_path_factory):
     return rows
 
 
-def test_last_bit_differences_stay_within_one_ulp(report):
-    assert report["max_ulp"]["acos"] <= 1 and report["max_ulp"]["atan2"] <= 1, report["max_ulp"]
+def test_acos_atan2_bits_equal_glibc(report):
+    assert report["max_ulp"]["acos"] == 0 and report["max_ulp"]["atan2"] == 0, report["max_ulp"]
     for s in ("random", "adversarial"):
-        assert report[s]["acos_differs"] < 0.15 * report[s]["n"]
-        assert report[s]["atan2_differs"] < 0.25 * report[s]["n"]
+        assert report[s]["n"] == 1 << 20
+        assert report[s]["acos_differs"] == 0 and report[s]["atan2_differs"] == 0, report[s]
 
 
 def test_exact_cases_agree_bit_for_bit(report):
@@ -45,11 +44,8 @@ def test_exact_cases_agree_bit_for_bit(report):
     assert report["special"]["differs"] == 0, report["special"]
 
 
-def test_uniform_normals_pick_the_reference_texel(report):
-    assert report["random"]["texel_differs"] == 0, report["random"]
-
-
-def test_texel_edge_normals_disagree_only_near_edges(report):
-    # a 1-ulp u or v difference changes the texel only when u * W or (1 - v) * H is within an ulp of an integer; the
-    # adversarial set puts every normal within 4 ulps of one, so a few percent of them flip
-    assert 0 < report["adversarial"]["texel_differs"] < 0.05 * report["adversarial"]["n"], report["adversarial"]
+@pytest.mark.parametrize("normals", ["random", "adversarial"])
+def test_u_v_and_texel_equal_the_reference(report, normals):
+    # the adversarial set puts every normal within 4 ulps of a texel edge: any last-bit difference would flip texels
+    r = report[normals]
+    assert r["u_bits_differ"] == 0 and r["v_bits_differ"] == 0 and r["texel_differs"] == 0, r

@@ -1,13 +1,13 @@
-// tools/uv_check.hip — the device's get_sphere_uv (sphere.h:24-37; csrc/sphere_uv.h, fdlibm acos / atan2, the code
-// k_paths / k_paths_g run): does the device compute the host build's bits (it must: same code, no contraction), and how
-// often does it pick a different texel than the reference's (glibc's acos / atan2)?  The image texture reads texel
-// (int(clamp(u) * W), int((1 - clamp(v)) * H)) (texture.h:67-118), so a last-bit difference in u or v can only move a
-// lookup when u * W or (1 - v) * H lies within a few ulps of an integer.  Two normal sets, each 2^24 unit vectors:
+// tools/uv_check.hip — the device's get_sphere_uv (sphere.h:24-37; csrc/sphere_uv.h, glibc's acos / atan2 restated in
+// glibc_trig.h, the code k_paths / k_paths_g run): does the device compute the host build's bits, and are they glibc's
+// (the reference's libm)?  Both must hold exactly.  The image texture reads texel (int(clamp(u) * W),
+// int((1 - clamp(v)) * H)) (texture.h:67-118), so a last-bit difference in u or v would move a lookup when u * W or
+// (1 - v) * H lies within a few ulps of an integer; the second set is built to sit there.  Two sets, 2^24 unit vectors each:
 //   random       uniform directions (a splitmix64 stream), as hit normals (p - c) / r spread over a sphere;
 //   adversarial  directions placed on the texel boundaries of the earth texture (1024 x 512, scene_manager.cpp:117,
 //                the final scene's earth): u = k / 1024 and v = 1 - j / 512, each nudged by -4..+4 ulps per component.
 // Prints one JSON line: per set, normals whose u or v bits differ from glibc's, normals whose texel differs, and
-// normals whose device bits differ from the host's sphere_uv (device_vs_host, expected 0).
+// normals whose device bits differ from the host's sphere_uv (all expected 0).
 //   hipcc -O3 -ffp-contract=off --offload-arch=gfx950 -Ianother_raytracer_amd/csrc tools/uv_check.hip -o tools/uv_check
 #include <hip/hip_runtime.h>
 
@@ -19,11 +19,11 @@
 #include <cstring>
 #include <vector>
 
-__global__ void k_uv(const double* n, double* uv, uint32_t count, const double* coef) {
+__global__ void k_uv(const double* n, double* uv, uint32_t count, const double* tab) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= count) return;
     double u, v;
-    const art::UvPair w = art::sphere_uv(n[3 * k], n[3 * k + 1], n[3 * k + 2], coef);  // device.h prim_surface's call
+    const art::UvPair w = art::sphere_uv(n[3 * k], n[3 * k + 1], n[3 * k + 2], art::TrigTab(tab, tab));  // device.h prim_surface's call
     u = w.u;
     v = w.v;
     uv[2 * k] = u;
@@ -90,17 +90,17 @@ int main() {
         sets[1][3 * k + 2] = nudge(z, dz);
     }
     double *dn = nullptr, *duv = nullptr;
-    double* dcoef = nullptr;
+    double* dtab = nullptr;
     if (hipMalloc(&dn, sizeof(double) * 3 * n) != hipSuccess || hipMalloc(&duv, sizeof(double) * 2 * n) != hipSuccess ||
-        hipMalloc(&dcoef, sizeof(art::kUvCoefHost)) != hipSuccess)
+        hipMalloc(&dtab, sizeof(art::glibc_trig_data::kTrigHost)) != hipSuccess)
         return 2;
-    if (hipMemcpy(dcoef, art::kUvCoefHost, sizeof(art::kUvCoefHost), hipMemcpyHostToDevice) != hipSuccess) return 2;
+    if (hipMemcpy(dtab, art::glibc_trig_data::kTrigHost, sizeof(art::glibc_trig_data::kTrigHost), hipMemcpyHostToDevice) != hipSuccess) return 2;
     std::vector<double> uv(2 * size_t(n));
     const char* names[2] = {"random", "adversarial"};
     std::printf("{\"normals_per_set\": %u, \"texture\": [%d, %d]", n, W, H);
     for (int t = 0; t < 2; ++t) {
         if (hipMemcpy(dn, sets[t].data(), sizeof(double) * 3 * n, hipMemcpyHostToDevice) != hipSuccess) return 2;
-        hipLaunchKernelGGL(k_uv, dim3(n / 256), dim3(256), 0, 0, dn, duv, n, dcoef);
+        hipLaunchKernelGGL(k_uv, dim3(n / 256), dim3(256), 0, 0, dn, duv, n, dtab);
         if (hipMemcpy(uv.data(), duv, sizeof(double) * 2 * n, hipMemcpyDeviceToHost) != hipSuccess) return 2;
         uint64_t ubad = 0, vbad = 0, tbad = 0, hbad = 0;
         for (uint32_t k = 0; k < n; ++k) {
