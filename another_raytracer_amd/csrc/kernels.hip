@@ -211,6 +211,7 @@ struct PassGeom {
     double inv_w1, inv_h1;      // RN(1 / (W - 1)), RN(1 / (H - 1)) for gen_ray's div_rcp (rt_render rejects W or H < 2)
     const uint32_t* list;       // pixel-list mode (engine_mode::adaptive levels): slot pixel = list[qi] (local ly*W+lx)
     uint32_t nlist;             //   for qi < nlist; nullptr = every local pixel in 8x8 tile order
+    uint32_t chunk;             // persistent kernels: slots per claim (path_chunk; a multiple of 64)
 };
 template <class R>
 struct Work {
@@ -640,10 +641,21 @@ __global__ __launch_bounds__(L ? kBlockL : kBlock, L ? 1 : ART_EXTEND_MIN_WAVES)
 // shade_hit_lds, repeat until a miss, an absorption, a light or max_depth), then writes the slot's radiance and takes
 // the next slot -- no path records, queues or per-depth launches, and the deep bounces of old paths share the waves
 // with the first bounces of new ones instead of running as a tail of nearly empty launches.  Slots are claimed in
-// increasing order in wave chunks of kPathChunk from one counter (one atomic per chunk: ~10 M/s at full rate, far
-// below the ~88 M/s a single word sustains).  The bounce arithmetic and the RNG draws are those of the fused
-// k_extend, so images are bit-identical to the wavefront variants.
-constexpr uint32_t kPathChunk = 256;
+// increasing order in wave chunks of PassGeom::chunk from one counter (one atomic per chunk).  The bounce arithmetic
+// and the RNG draws are those of the fused k_extend, so images are bit-identical to the wavefront variants.
+// The chunk (PassGeom::chunk, path_chunk on the host) is the pass's slots / (16 claims per wave of a full CU), as a
+// power of two in [64, cap]: cap 2048 for k_paths, 1024 for k_paths_g.  The counter is one word every wave of the
+// chip claims from: at 256 slots per claim k_paths took ~67 M claims/s, and each claim stalls its wave for the
+// device-scope atomic's round trip.  Measured (r4r, against 256): C2 +2.5 % (2048), cow +3.9 % and the final +1.2 %
+// (1024); larger chunks lost on k_paths_g (cow -2.7 % at 2048, -8 % at 4096), and claiming the next chunk one chunk
+// ahead lost 1.5-2 % (its return is waited for by the loop's next vmcnt wait).  Small passes (pixel lists, small
+// frames) keep at least 16 claims per wave.
+__host__ inline uint32_t path_chunk(uint32_t P, int num_cu, uint32_t cap) {
+    const uint64_t per = static_cast<uint64_t>(P) / (static_cast<uint64_t>(num_cu > 0 ? num_cu : 1) * 16u * 16u);
+    uint32_t c = 64;
+    while (c < cap && 2ull * c <= per) c *= 2;
+    return c;
+}
 // Camera-ray pool: a path start is run by the whole wave for however few lanes start a path (~a third
 // of them per round), so the camera rays are generated 64 at a time -- one per lane, converged -- into a per-wave ring
 // in global memory (L2-resident: 8 KiB per wave), and a starting lane loads the next ring entry instead.  Entry pos
@@ -691,11 +703,12 @@ struct RayRing {
     }
     __device__ __forceinline__ void refill(const PassGeom& sg, const CameraRec<double>& sc, uint32_t* next_slot, uint32_t lane) {
         if (cur == end) {
+            const uint32_t chunk = sg.chunk;
             uint32_t nb = 0;
-            if (lane == 0) nb = atomicAdd(next_slot, kPathChunk);
+            if (lane == 0) nb = atomicAdd(next_slot, chunk);
             nb = __shfl(nb, 0);
             cur = nb;
-            end = nb + kPathChunk;
+            end = nb + chunk;
         }
         const uint32_t b = cur;
         cur += 64;
@@ -1038,13 +1051,14 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
             const uint32_t rank = static_cast<uint32_t>(__popcll(idle & below));
             uint32_t slot;
             if (cur + n > end) {
+                const uint32_t chunk = s_g.chunk;
                 uint32_t nb = 0;
-                if (lane == 0) nb = atomicAdd(next_slot, kPathChunk);
+                if (lane == 0) nb = atomicAdd(next_slot, chunk);
                 nb = __shfl(nb, 0);
                 const uint32_t left = end - cur;
                 slot = rank < left ? cur + rank : nb + (rank - left);
                 cur = nb + (n - left);
-                end = nb + kPathChunk;
+                end = nb + chunk;
             } else {
                 slot = cur + rank;
                 cur += n;
@@ -2266,6 +2280,7 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
                     persistent = true;
                     if (p.max_depth > 0) {
                         if (prof) mark();
+                        g.chunk = path_chunk(g.P, I.num_cu, variant == EXT_MEGA ? 2048u : 1024u);
                         if (variant == EXT_MEGA) launch_paths(I.num_cu, stream, ds.view, g, cam, w, counter(w, 0, 0, 0));
                         else launch_paths_g(ds.features, ds.tex_basic, ds.codes16, I.num_cu, stream, ds.view, g, cam, w, counter(w, 0, 0, 0));
                         if (prof) { mark(); mark(); }
