@@ -211,7 +211,7 @@ struct PassGeom {
     double inv_w1, inv_h1;      // RN(1 / (W - 1)), RN(1 / (H - 1)) for gen_ray's div_rcp (rt_render rejects W or H < 2)
     const uint32_t* list;       // pixel-list mode (engine_mode::adaptive levels): slot pixel = list[qi] (local ly*W+lx)
     uint32_t nlist;             //   for qi < nlist; nullptr = every local pixel in 8x8 tile order
-    uint32_t chunk;             // persistent kernels: slots per claim (path_chunk; a multiple of 64)
+    uint32_t chunk;             // persistent kernels: slots per claim (path_chunk: a power of two >= 64)
 };
 template <class R>
 struct Work {
@@ -643,17 +643,18 @@ __global__ __launch_bounds__(L ? kBlockL : kBlock, L ? 1 : ART_EXTEND_MIN_WAVES)
 // with the first bounces of new ones instead of running as a tail of nearly empty launches.  Slots are claimed in
 // increasing order in wave chunks of PassGeom::chunk from one counter (one atomic per chunk).  The bounce arithmetic
 // and the RNG draws are those of the fused k_extend, so images are bit-identical to the wavefront variants.
-// The chunk (PassGeom::chunk, path_chunk on the host) is the pass's slots / (16 claims per wave of a full CU), as a
-// power of two in [64, cap]: cap 2048 for k_paths, 1024 for k_paths_g.  The counter is one word every wave of the
-// chip claims from: at 256 slots per claim k_paths took ~67 M claims/s, and each claim stalls its wave for the
-// device-scope atomic's round trip.  Measured (r4r, against 256): C2 +2.5 % (2048), cow +3.9 % and the final +1.2 %
-// (1024); larger chunks lost on k_paths_g (cow -2.7 % at 2048, -8 % at 4096), and claiming the next chunk one chunk
-// ahead lost 1.5-2 % (its return is waited for by the loop's next vmcnt wait).  Small passes (pixel lists, small
-// frames) keep at least 16 claims per wave.
-__host__ inline uint32_t path_chunk(uint32_t P, int num_cu, uint32_t cap) {
-    const uint64_t per = static_cast<uint64_t>(P) / (static_cast<uint64_t>(num_cu > 0 ? num_cu : 1) * 16u * 16u);
+// The chunk (PassGeom::chunk, path_chunk on the host) is a power of two in [64, 2048], at most the pass's slots / 64
+// claims per wave of a full CU.  The counter is one word every wave of the chip claims from: at 256 slots per claim
+// k_paths took ~67 M claims/s, and each claim stalls its wave for the device-scope atomic's round trip.  Against 256
+// (r4r_ab_path_chunk.txt): C2 +2.9 %, cow +3.2 %, the final +1.2 %, dino +1.2 %.  Larger chunks leave longer tails at
+// the end of a pass: at 0.27-0.54 G slots per pass k_paths_g was fastest at 1024 (2048: -1 to -2.6 %, 4096: -3 to
+// -8 %), at the configs' 1.1-1.7 G at 2048 (cow +0.9 % over 1024, the final +-0); k_paths (C2, 2.1 G) +-0 from 2048
+// to 4096.  Claiming the next chunk one chunk ahead lost 1.5-2 % (its return is waited for at the loop's next vmcnt
+// wait).  Small passes (pixel lists, small frames) keep at least 64 claims per wave.
+__host__ inline uint32_t path_chunk(uint32_t P, int num_cu) {
+    const uint64_t per = static_cast<uint64_t>(P) / (static_cast<uint64_t>(num_cu > 0 ? num_cu : 1) * 16u * 64u);
     uint32_t c = 64;
-    while (c < cap && 2ull * c <= per) c *= 2;
+    while (c < 2048u && 2ull * c <= per) c *= 2;
     return c;
 }
 // Camera-ray pool: a path start is run by the whole wave for however few lanes start a path (~a third
@@ -2280,7 +2281,7 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
                     persistent = true;
                     if (p.max_depth > 0) {
                         if (prof) mark();
-                        g.chunk = path_chunk(g.P, I.num_cu, variant == EXT_MEGA ? 2048u : 1024u);
+                        g.chunk = path_chunk(g.P, I.num_cu);
                         if (variant == EXT_MEGA) launch_paths(I.num_cu, stream, ds.view, g, cam, w, counter(w, 0, 0, 0));
                         else launch_paths_g(ds.features, ds.tex_basic, ds.codes16, I.num_cu, stream, ds.view, g, cam, w, counter(w, 0, 0, 0));
                         if (prof) { mark(); mark(); }
