@@ -260,15 +260,6 @@ __device__ __forceinline__ R div_rcp(R x, R a, R inv_a) {
     const R q = x * inv_a;
     return fma(fma(-q, a, x), inv_a, q);
 }
-#ifndef ART_MEDIUM_RCP
-#define ART_MEDIUM_RCP 0
-#endif
-// div_rcp's range: 2^-500 <= |x| < 2^501 (zero, subnormals, infinities and NaN fall outside).  With the divisor and
-// the dividend inside it, the quotient and div_rcp's residual stay normal and finite.
-__device__ __forceinline__ bool rcp_range(double x) {
-    const uint32_t e = static_cast<uint32_t>(static_cast<uint64_t>(__double_as_longlong(x)) >> 52) & 0x7ffu;
-    return e - 523u <= 1000u;
-}
 
 // sphere.h:39-65 / moving_sphere.h:41-58 (root selection only; the surface is rebuilt in shade).  a = |d|^2 of the
 // ray; RCP: the two root divisions by a use div_rcp with inv_a = 1 / a (same bits).
@@ -1182,21 +1173,7 @@ __device__ __forceinline__ bool hit_medium(const DevScene<R>& S, const uint8_t* 
         const R disc = half_b * half_b - a * c;
         if (disc < R(0)) return false;
         const R sqrtd = sqrt_rn(disc);
-#if ART_MEDIUM_RCP
-        // both roots' divisions by a through one reciprocal (div_rcp: the division's bits inside its range)
-        R r_near = -half_b - sqrtd, r_far = -half_b + sqrtd;
-        if (rcp_range(a) && rcp_range(r_near) && rcp_range(r_far)) {
-            const R inv_a = R(1) / a;
-            r_near = div_rcp(r_near, a, inv_a);
-            r_far = div_rcp(r_far, a, inv_a);
-        } else {
-            __asm__ volatile("" : "+v"(r_near), "+v"(r_far));
-            r_near = r_near / a;
-            r_far = r_far / a;
-        }
-#else
         const R r_near = (-half_b - sqrtd) / a, r_far = (-half_b + sqrtd) / a;
-#endif
         t1 = r_near;  // first call, t in [-inf, inf]
         if (t1 < -inf || inf < t1) {
             t1 = r_far;
