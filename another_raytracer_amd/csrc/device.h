@@ -761,9 +761,11 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
     constexpr bool PK = !L && (F & F_CODE16) != 0;
     static_assert(!PK || (F & F_MEDIA_G) == 0, "packed keys need tmin > 0: no medium boundary traversals");
     LaneStack<B, L || PK> st(stk);
-    // kNfHoist: the near-plane offsets computed once per traversal in kernels with every node in LDS (PL 2) and no
-    // instance transforms (the lighter register budgets: dino's LM 1 kernel), instead of 6 VALU per node visit
-    constexpr bool kNfHoist = !L && PL == 2 && (F & F_XFORM) == 0;
+    // kNfHoist: the near-plane offsets computed once per traversal in kernels with every node in LDS (PL 2), instead
+    // of 6 VALU per node visit: without instance transforms (dino's LM 1 kernel), and with them where the kernel has
+    // no triangles or medium-boundary traversals (the Next-Week final's: +0.8 %, r4y_ab_nf_hoist.txt; in the F_ALL
+    // kernels it spilled)
+    constexpr bool kNfHoist = !L && PL == 2 && ((F & F_XFORM) == 0 || (F & (F_TRI | F_MEDIA_G)) == 0);
     [[maybe_unused]] const uint32_t nf_hx = (__float_as_uint(ix) >> 31) << 4, nf_hy = (__float_as_uint(iy) >> 31) << 4,
                                     nf_hz = (__float_as_uint(iz) >> 31) << 4;
     // L: inner nodes are coded by their byte offset in a node plane (index * 16, layout.h), so a visit's plane
