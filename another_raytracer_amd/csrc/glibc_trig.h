@@ -3,11 +3,11 @@
 //
 // glibc 2.35 (this image) selects, on x86-64 CPUs with FMA and AVX2, the FMA builds of sysdeps/ieee754/dbl-64/
 // e_asin.c (__ieee754_acos) and e_atan2.c (__ieee754_atan2): IBM's table-driven algorithms with their multi-precision
-// fallbacks removed.  Neither is correctly rounded (tools/acos_atan2_cr.c against MPFR: 0.07 % / 0.09 % of unit-vector arguments differ from
-// the correct rounding), so no independent implementation reproduces their last bits; the sequences below are those
-// builds' machine code read back instruction for instruction -- which products are fused (the compiler contracted
-// a * b + c into FMAs), which are rounded separately, in its order -- with their data (glibc_trig_data.h, generated
-// from libm.so.6 by tools/gen_glibc_trig.py).  tests/test_glibc_trig.py compares both with the C library on tens of
+// fallbacks removed.  Neither is correctly rounded (tools/acos_atan2_cr.c against MPFR: 0.07 % / 0.09 % of unit-vector
+// arguments differ from the correct rounding), so no independent implementation reproduces their last bits; the
+// sequences below are those builds' machine code read back instruction for instruction -- which products are fused
+// (the compiler contracted a * b + c into FMAs), which are rounded separately, in its order -- with their data
+// (glibc_trig_data.h, generated from libm.so.6 by tools/gen_glibc_trig.py).  tests/test_glibc_trig.py compares both with the C library on tens of
 // millions of arguments (every branch, the unit-vector components get_sphere_uv passes, the special values);
 // tools/uv_check.hip checks that the device computes the host's bits.
 //
