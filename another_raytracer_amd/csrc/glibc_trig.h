@@ -7,9 +7,9 @@
 // arguments differ from the correct rounding), so no independent implementation reproduces their last bits; the
 // sequences below are those builds' machine code read back instruction for instruction -- which products are fused
 // (the compiler contracted a * b + c into FMAs), which are rounded separately, in its order -- with their data
-// (glibc_trig_data.h, generated from libm.so.6 by tools/gen_glibc_trig.py).  tests/test_glibc_trig.py compares both with the C library on tens of
-// millions of arguments (every branch, the unit-vector components get_sphere_uv passes, the special values);
-// tools/uv_check.hip checks that the device computes the host's bits.
+// (glibc_trig_data.h, generated from libm.so.6 by tools/gen_glibc_trig.py).  tests/test_glibc_trig.py compares both
+// with the C library on tens of millions of arguments (every branch, the unit-vector components get_sphere_uv passes,
+// the special values); tools/uv_check.hip checks that the device computes the host's bits.
 //
 // The data sits in one table the caller passes (TrigTab): on the host the arrays below, on the device a copy uploaded
 // with the scene (device.h uv_table), so that no constant becomes a literal the compiler would hoist into the path
