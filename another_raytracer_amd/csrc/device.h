@@ -1174,6 +1174,11 @@ __device__ __forceinline__ bool hit_object(const DevScene<R>& S, const uint8_t* 
 // Out of line: measured +0.2 % (cow) to +1.8 % (Next-Week final) over the inlined body, which raised the register
 // pressure of the whole path loop for a function most segments do not reach.
 static __device__ __noinline__ double glibc_log_call(double x) { return glibc_log(x); }
+// get_sphere_uv out of line as well (glibc_trig.h's acos / atan2 are long and run only for image-textured spheres):
+// measured r4z2 the earth scene +3.1 % (its kernel: 166 -> 160 VGPRs, SGPR spills 28 -> 12), the Next-Week final +-0
+[[maybe_unused]] static __device__ __noinline__ UvPair sphere_uv_call(double x, double y, double z, const double* c, const double* t) {
+    return sphere_uv(x, y, z, TrigTab(c, t));
+}
 // constant_medium.h:37-82.  Consumes one uniform when the clamped interval is non-empty.
 template <class R, uint32_t F, int B, bool L, int PL = 0>
 __device__ __forceinline__ bool hit_medium(const DevScene<R>& S, const uint8_t* lds, const ObjRec<R>& m, const Ray<R>& r, R tmin, R tmax,
@@ -1392,8 +1397,8 @@ __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref,
                 ART_STAT_LANE(33);
                 // get_sphere_uv (sphere.h:24-37) with glibc's acos / atan2 restated (sphere_uv.h; their constants are
                 // loaded where used, not hoisted into the path loop's registers)
-                const UvPair uv = sphere_uv(static_cast<double>(outward.x), static_cast<double>(outward.y), static_cast<double>(outward.z),
-                                            TrigTab(uvc, uv_table(S)));
+                const UvPair uv = sphere_uv_call(static_cast<double>(outward.x), static_cast<double>(outward.y), static_cast<double>(outward.z),
+                                                 uvc, uv_table(S));
                 su = R(uv.u);
                 sv = R(uv.v);
             }
