@@ -17,7 +17,7 @@ dielectric, diffuse_light; solid_color, checker_texture, noise_texture, image_te
 OBJ/MTL meshes (mesh().parse(path) / .build(), mesh.h) — see scene.py.
 All compute runs in libart.so (HIP, gfx950) behind include/art.h.
 """
-from ._lib import RTError, lib  # noqa: F401  (fails loudly when libart.so is missing)
+from ._lib import RTError, get_option, lib, set_option  # noqa: F401  (fails loudly when libart.so is missing)
 from .engine import camera, engine, engine_mode, tracer_constants  # noqa: F401
 from .scene import (  # noqa: F401
     barycentric_image_texture, box, bvh_node, checker_texture, constant_medium, dielectric, diffuse_light, hittable_list, image_texture,
@@ -27,7 +27,7 @@ from .scene import (  # noqa: F401
 from . import imageio  # noqa: F401
 
 __all__ = [
-    "RTError", "camera", "engine", "engine_mode", "tracer_constants", "scene", "scene_alias", "scene_manager",
+    "RTError", "set_option", "get_option", "camera", "engine", "engine_mode", "tracer_constants", "scene", "scene_alias", "scene_manager",
     "hittable_list", "bvh_node", "sphere", "moving_sphere", "triangle", "xy_rect", "xz_rect", "yz_rect", "box",
     "translate", "rotate_y", "constant_medium", "lambertian", "metal", "dielectric", "diffuse_light", "solid_color",
     "checker_texture", "noise_texture", "image_texture", "barycentric_image_texture", "mesh", "random_double", "reset_scene_rng", "imageio", "save_scene",

@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("ART_LIB") or os.path.join(_HERE, "libart.so")  # ART_
 
 RT_OK = 0
 RT_FP64 = 0  # the only fp_mode since ABI 2 (include/art.h)
-RT_ABI_VERSION = 4
+RT_ABI_VERSION = 5
 RT_OUT_DEVICE, RT_PROFILE, RT_GLOBAL_SCENE, RT_SPLIT_SHADE, RT_ADAPTIVE, RT_WAVEFRONT, RT_PARALLEL_IMAGES = 1, 2, 4, 8, 16, 32, 64
 ERRORS = {-1: "RT_E_INVALID", -2: "RT_E_SCENE", -3: "RT_E_DEVICE", -4: "RT_E_INTERNAL"}
 
@@ -43,7 +43,8 @@ class rt_stats(ctypes.Structure):
                 ("extend_ms", ctypes.c_double), ("shade_ms", ctypes.c_double),
                 ("extend_launches", ctypes.c_uint64), ("shade_launches", ctypes.c_uint64),
                 ("passes", ctypes.c_int32), ("samples_per_pass", ctypes.c_int32), ("local_rows", ctypes.c_int32),
-                ("extend_variant", ctypes.c_int32)]
+                ("extend_variant", ctypes.c_int32), ("kernel_features", ctypes.c_uint32), ("kernel_textures", ctypes.c_uint32),
+                ("kernel_lds_mode", ctypes.c_int32)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}
@@ -78,6 +79,8 @@ SIGNATURES = {
     "rt_abi_version": (_I, []),
     "rt_last_error": (ctypes.c_char_p, []),
     "rt_device_count": (_I, []),
+    "rt_option_set": (_I, [ctypes.c_char_p, _D]),
+    "rt_option_get": (_I, [ctypes.c_char_p, _DP]),
     "rt_scene_build": (_I, [ctypes.c_char_p, ctypes.c_char_p, _I, ctypes.POINTER(_P)]),
     "rt_scene_info_get": (_I, [_P, ctypes.POINTER(rt_scene_info)]),
     "rt_scene_dump": (_S, [_P, ctypes.c_char_p, _S]),
@@ -161,6 +164,17 @@ def check(code, where):
     if code < 0:
         raise RTError(code, where)
     return code
+
+
+def set_option(name, value):
+    """rt_option_set (include/art.h): a process-wide library option; name None resets every option to its default."""
+    check(lib.rt_option_set(None if name is None else name.encode(), float(value)), f"rt_option_set({name})")
+
+
+def get_option(name):
+    v = ctypes.c_double()
+    check(lib.rt_option_get(name.encode(), ctypes.byref(v)), f"rt_option_get({name})")
+    return v.value
 
 
 def dvec(v):

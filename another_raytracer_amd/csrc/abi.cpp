@@ -14,6 +14,7 @@
 #include "renderer.h"
 #include "scenefile.h"
 #include "objmesh.h"
+#include "options.h"
 #include "scene.h"
 
 namespace art {
@@ -101,6 +102,9 @@ void fill_stats(const art::RenderStats& st, rt_stats* stats) {
     stats->samples_per_pass = st.samples_per_pass;
     stats->local_rows = st.local_rows;
     stats->extend_variant = st.extend_variant;
+    stats->kernel_features = st.kernel_features;
+    stats->kernel_textures = st.kernel_textures;
+    stats->kernel_lds_mode = st.kernel_lds_mode;
 }
 art::CameraRec<double> camera_of(const rt_camera* cam) {
     return art::make_camera(cam->lookfrom, cam->lookat, cam->vup, cam->vfov, cam->aspect, cam->aperture, cam->focus_dist, cam->time0, cam->time1);
@@ -133,6 +137,20 @@ int scene_from_graph(art::SceneGraph graph, int device, rt_scene** out) {
 extern "C" {
 
 int rt_abi_version(void) { return RT_ABI_VERSION; }
+int rt_option_set(const char* name, double value) {
+    if (!name) {
+        art::opt_reset_all();
+        return RT_OK;
+    }
+    const char* why = "";
+    if (!art::opt_set(name, value, &why)) return fail(RT_E_INVALID, std::string("rt_option_set(") + name + "): " + why);
+    return RT_OK;
+}
+int rt_option_get(const char* name, double* value) {
+    if (!name || !value) return fail(RT_E_INVALID, "rt_option_get: name and value must be non-NULL");
+    if (!art::opt_get(name, value)) return fail(RT_E_INVALID, std::string("rt_option_get(") + name + "): unknown option");
+    return RT_OK;
+}
 const char* rt_last_error(void) { return g_err.c_str(); }
 int rt_device_count(void) {
     return guard(RT_E_DEVICE, [] { return art::device_count(); });

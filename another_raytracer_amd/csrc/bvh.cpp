@@ -1,5 +1,6 @@
 // bvh.cpp — full-sweep SAH binary tree, collapsed into the 4-wide node array of layout.h (see bvh.h).
 #include "bvh.h"
+#include "options.h"
 
 #include <algorithm>
 #include <array>
@@ -14,33 +15,17 @@ namespace art {
 namespace {
 
 constexpr double kCostTraverse = 1.0;
-// SAH primitive-test cost relative to a (binary) node step; ART_SAH_CI / ART_SAH_LEAF override it and the leaf size
-// for builder experiments (tools/, not part of the product contract)
-double sah_ci() {
-    static const double v = [] {
-        const char* e = std::getenv("ART_SAH_CI");
-        return e ? std::atof(e) : 1.5;
-    }();
-    return v;
-}
-int sah_leaf() {
-    static const int v = [] {
-        const char* e = std::getenv("ART_SAH_LEAF");
-        return e ? std::max(1, std::min(16, std::atoi(e))) : kMaxLeafPrims;
-    }();
-    return v;
-}
+// SAH primitive-test cost relative to a (binary) node step and the leaf size: options bvh.sah_ci / bvh.sah_leaf
+// (rt_option_set; builder experiments, tools/sah_sweep*.sh)
+double sah_ci() { return opt(Opt::SahCi); }
+int sah_leaf() { return static_cast<int>(opt(Opt::SahLeaf)); }  // 1..16 (the option's range)
 
 int collapse_mode();
-// Leaf size of the binary tree: the wide tree's under the greedy collapse; ART_DP_BINARY_LEAF (default 1) under the
+// Leaf size of the binary tree: the wide tree's under the greedy collapse; bvh.dp_binary_leaf (default 1) under the
 // SAH-optimal collapse, which then chooses the wide tree's leaves itself (merging binary leaves up to sah_leaf())
 int binary_leaf() {
-    static const int v = [] {
-        if (collapse_mode() != 1) return sah_leaf();
-        const char* e = std::getenv("ART_DP_BINARY_LEAF");
-        return std::max(1, std::min(sah_leaf(), e ? std::atoi(e) : 1));
-    }();
-    return v;
+    if (collapse_mode() != 1) return sah_leaf();
+    return std::max(1, std::min(sah_leaf(), static_cast<int>(opt(Opt::DpBinaryLeaf))));
 }
 
 double area(const AABBd& b) {
@@ -155,21 +140,9 @@ struct Builder {
 // a spatial split references a straddling primitive from both sides with its clipped boxes.  Tighter boxes for meshes
 // (fewer node visits and leaf tests), at the price of duplicated references (capped by kSbvhRefBudget).
 constexpr double kSbvhRefBudget = 1.5;
-double sbvh_alpha() {  // overlap / root area below which no spatial split is tried
-    static const double v = [] {
-        const char* e = std::getenv("ART_SBVH_ALPHA");
-        return e ? std::atof(e) : 1e-5;
-    }();
-    return v;
-}
+double sbvh_alpha() { return opt(Opt::SbvhAlpha); }  // overlap / root area below which no spatial split is tried
 constexpr int kSbvhBins = 32;
-double sbvh_budget() {
-    static const double v = [] {
-        const char* e = std::getenv("ART_SBVH");
-        return e ? std::atof(e) : kSbvhRefBudget;  // 0 (or < 1): object splits only
-    }();
-    return v;
-}
+double sbvh_budget() { return opt(Opt::Sbvh); }  // kSbvhRefBudget by default; < 1: object splits only
 
 struct SItem {
     uint32_t ref;
@@ -349,25 +322,13 @@ struct SBuilder {
 // C(n, i) = the least SAH cost of covering n's primitives with at most i wide-node children, each either a wide node
 // (cost A·1 + the best spread of its 4 slots over n's two children) or a leaf of n's primitives (cost A·ci·count, when
 // they are contiguous in the primref array and at most the leaf size).  The greedy alternative pulls the largest-area
-// children up and never merges binary leaves.  ART_BVH_COLLAPSE: 0 greedy (default), 1 dp; ART_COLLAPSE_CI: the
+// children up and never merges binary leaves.  bvh.collapse: 0 greedy (default), 1 dp; bvh.collapse_ci: the
 // primitive test cost relative to a 4-wide node visit.  Measured (r3k, A/B on one box, Msamples/s): the optimal
 // collapse visits fewer nodes (scene 1: 6.21 vs 6.36 per traversal) but diverges more (node-loop lane utilization
 // 0.441 vs 0.474) and loses on the GPU: scene 1 -3.4 %, cow -1.2 %, Next-Week final -6.1 %, dino +0.6 % (ci 0.6;
 // ci 0.4 / 1.0 and a leaf-size-4 binary tree no better), so the greedy collapse stays the default.
-int collapse_mode() {
-    static const int v = [] {
-        const char* e = std::getenv("ART_BVH_COLLAPSE");
-        return e ? std::atoi(e) : 0;
-    }();
-    return v;
-}
-double collapse_ci() {
-    static const double v = [] {
-        const char* e = std::getenv("ART_COLLAPSE_CI");
-        return e ? std::atof(e) : 0.6;
-    }();
-    return v;
-}
+int collapse_mode() { return static_cast<int>(opt(Opt::BvhCollapse)); }
+double collapse_ci() { return opt(Opt::CollapseCi); }
 struct CollapseDP {
     static constexpr int kW = 4;
     const std::vector<BNode>& tree;

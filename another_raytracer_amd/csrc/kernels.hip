@@ -18,24 +18,23 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <functional>
-#include <map>
-#include <mutex>
-#include <tuple>
-#include <algorithm>
 #include <array>
 #include <cmath>
-#include <functional>
-#include <limits>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <limits>
+#include <map>
+#include <mutex>
 #include <stdexcept>
-#include <type_traits>
 #include <string>
+#include <tuple>
+#include <type_traits>
 #include <vector>
 
 #include "device.h"
+#include "options.h"
 #include "pass_plan.h"
 #include "renderer.h"
 
@@ -1785,10 +1784,9 @@ static void build_device_scene(const FlatScene& f, DeviceScene<R>& ds) {
         }
         for (const auto& o : f.objs)
             if (o.kind == OBJ_BVH && o.b != kNodeEmpty) ok = ok && leaf16_ok(leaf_first(o.b), leaf_count(o.b));
-        // ART_CODE16=0 (environment, read per upload; tests): take the 32-bit-code kernels as a scene whose codes do
+        // option render.codes16 = 0 (read per upload; tests): take the 32-bit-code kernels as a scene whose codes do
         // not fit would (a parity probe of that path on scenes that fit)
-        const char* force = std::getenv("ART_CODE16");
-        if (force && std::atoi(force) == 0) ok = false;
+        if (opt(Opt::Codes16) == 0) ok = false;
         ds.codes16 = ok;
         ds.view.nodes = ds.upload(nodes);
     }
@@ -1869,15 +1867,15 @@ struct Renderer::Impl {
     // ws / ws_bytes describe a live allocation at every point: a failed hipMalloc leaves them at {nullptr, 0}, so the
     // next render allocates again instead of handing out offsets from a null base.
     void* workspace(size_t bytes) {
-        // fault injection (tests): ART_FAULT_WORKSPACE_BYTES=N makes every workspace growth beyond N bytes fail as a
-        // refused hipMalloc would, after the old buffer is released
-        const char* lim = std::getenv("ART_FAULT_WORKSPACE_BYTES");
+        // fault point (tests): option test.fault_workspace_bytes = N > 0 makes every workspace growth beyond N bytes
+        // fail as a refused hipMalloc would, after the old buffer is released
+        const double lim = opt(Opt::FaultWorkspaceBytes);
         if (bytes > ws_bytes) {
-            if (lim && bytes > std::strtoull(lim, nullptr, 10)) {
+            if (lim > 0 && static_cast<double>(bytes) > lim) {
                 if (ws) (void)hipFree(ws);
                 ws = nullptr;
                 ws_bytes = 0;
-                throw std::runtime_error("workspace allocation of " + std::to_string(bytes) + " bytes refused (ART_FAULT_WORKSPACE_BYTES)");
+                throw std::runtime_error("workspace allocation of " + std::to_string(bytes) + " bytes refused (test.fault_workspace_bytes)");
             }
             if (ws) {
                 void* old = ws;
@@ -2015,17 +2013,24 @@ static void check_ring_waves(int blocks, int block, int num_cu) {
     if (padded * static_cast<size_t>(block / 64) > static_cast<size_t>(num_cu) * kPoolWavesPerCu)
         throw std::runtime_error("internal: persistent grid larger than the camera-ray rings");
 }
+// Which persistent-path kernel a render ran (rt_stats.kernel_*): k_paths_g<F, TF, LM>, or k_paths as LM 3
+struct KernelId {
+    uint32_t f = 0, tf = 0;
+    int lm = -1;
+};
 template <uint32_t F, uint32_t TF>
-static void launch_paths_g_ft(int num_cu, hipStream_t st, const DevScene<double>& S, const PassGeom& g, const CameraRec<double>& cam,
+static KernelId launch_paths_g_ft(int num_cu, hipStream_t st, const DevScene<double>& S, const PassGeom& g, const CameraRec<double>& cam,
                               const Work<double>& w, uint32_t* next_slot) {
     // g.stack = stack_rows: sentinel + entries + spare row
     const size_t lm_head = paths_g_head_bytes(g.stack, kBlockM, (F & F_CODE16) != 0) + paths_g_world_bytes(S.nworld, S.n_objs, lds_mats<TF>(S.n_mats));
     const size_t lds_m = align128(lm_head) + paths_g_mesh_bytes(S.n_nodes, S.n_primrefs, (F & F_TRI) ? S.n_primrefs : 0u);
-    if (S.n_nodes > 0 && lds_m <= kPathsGLdsCap) {
+    // LM 1 also for a scene without BVH nodes (the earth scene: one sphere object): its world and objects in LDS and no
+    // LM 0 suspend machinery (which spilled the earth's textured kernel)
+    if (lds_m <= kPathsGLdsCap) {
         const int blocks = blocks_per_cu(reinterpret_cast<const void*>(k_paths_g<F, TF, 1>), kBlockM, lds_m) * num_cu;
         check_ring_waves(blocks, kBlockM, num_cu);
         hipLaunchKernelGGL((k_paths_g<F, TF, 1>), dim3(blocks), dim3(kBlockM), lds_m, st, S, g, cam, w, next_slot);
-        return;
+        return {F, TF, 1};
     }
     // too large for LM 1: as many of the first (top-level) nodes as fit beside the stacks
     const size_t head = align128(lm_head);
@@ -2033,48 +2038,57 @@ static void launch_paths_g_ft(int num_cu, hipStream_t st, const DevScene<double>
     const uint32_t fit = head < kPathsGLdsCap ? static_cast<uint32_t>((kPathsGLdsCap - head) / node_bytes) : 0u;
     if (S.n_nodes > 0 && fit >= kLdsPartialMinNodes) {
         DevScene<double> SP = S;
-        // ART_LDS_NODES_MAX (diagnostic): a cap on the LDS-resident nodes, to measure what each one is worth
-        static const uint32_t cap = [] {
-            const char* e = std::getenv("ART_LDS_NODES_MAX");
-            return e ? static_cast<uint32_t>(std::atoi(e)) : 0xFFFFFFFFu;
-        }();
+        // option render.lds_nodes_max (diagnostic): a cap on the LDS-resident nodes, to measure what each one is worth
+        const uint32_t cap = static_cast<uint32_t>(opt(Opt::LdsNodesMax));
         SP.n_lds_nodes = std::min<uint32_t>(std::min<uint32_t>(fit, S.n_nodes), std::max<uint32_t>(cap, kLdsPartialMinNodes));
         const size_t lds_p = head + node_bytes * SP.n_lds_nodes;
         const int blocks = blocks_per_cu(reinterpret_cast<const void*>(k_paths_g<F, TF, 2>), kBlockM, lds_p) * num_cu;
         check_ring_waves(blocks, kBlockM, num_cu);
         hipLaunchKernelGGL((k_paths_g<F, TF, 2>), dim3(blocks), dim3(kBlockM), lds_p, st, SP, g, cam, w, next_slot);
-        return;
+        return {F, TF, 2};
     }
     const size_t lds = paths_g_head_bytes(g.stack, kBlock, (F & F_CODE16) != 0);
     const int blocks = blocks_per_cu(reinterpret_cast<const void*>(k_paths_g<F, TF, 0>), kBlock, lds) * num_cu;
     check_ring_waves(blocks, kBlock, num_cu);
     hipLaunchKernelGGL((k_paths_g<F, TF, 0>), dim3(blocks), dim3(kBlock), lds, st, S, g, cam, w, next_slot);
+    return {F, TF, 0};
 }
-static void launch_paths_g(uint32_t feat, bool tex_basic, bool codes16, int num_cu, hipStream_t st, const DevScene<double>& S, const PassGeom& g,
+static KernelId launch_paths_g(uint32_t feat, bool tex_basic, bool codes16, int num_cu, hipStream_t st, const DevScene<double>& S, const PassGeom& g,
                            const CameraRec<double>& cam, const Work<double>& w, uint32_t* next_slot) {
     constexpr uint32_t C = F_CODE16;
     if (!codes16 && (feat & F_MEDIA_G) == 0) {
-        // 32-bit child codes (more than 32768 nodes or 8192 primitive references): the instantiations without F_CODE16,
-        // the triangle-free one when the scene has no triangles (no triangle code in the kernel)
-        if (feat & F_TRI) launch_paths_g_ft<F_ALL, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
-        else launch_paths_g_ft<F_ALL & ~F_TRI, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
+        // 32-bit child codes (more than 32768 nodes or 8192 primitive references): the instantiations without F_CODE16.
+        // A mesh scene (the capsule: 10 200 triangles, the reference's default scene) gets the mesh feature set, not
+        // F_ALL (whose box, transform and boundary-traversal code spilled 45 VGPRs there); the triangle-free one when
+        // the scene has no triangles (no triangle code in the kernel)
+        if ((feat & ~kFeatMesh) == 0 && (feat & F_TRI)) {
+            if (tex_basic) return launch_paths_g_ft<kFeatMesh, kTexBasic>(num_cu, st, S, g, cam, w, next_slot);
+            return launch_paths_g_ft<kFeatMesh, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
+        }
+        if (feat & F_TRI) return launch_paths_g_ft<F_ALL, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
+        if (tex_basic) return launch_paths_g_ft<F_ALL & ~F_TRI, kTexBasic>(num_cu, st, S, g, cam, w, next_slot);
+        return launch_paths_g_ft<F_ALL & ~F_TRI, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
     } else if ((feat & ~kFeatSpheres) == 0) {
-        if (tex_basic) launch_paths_g_ft<kFeatSpheres | C, kTexBasic>(num_cu, st, S, g, cam, w, next_slot);
-        else launch_paths_g_ft<kFeatSpheres | C, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
+        if (tex_basic) return launch_paths_g_ft<kFeatSpheres | C, kTexBasic>(num_cu, st, S, g, cam, w, next_slot);
+        else return launch_paths_g_ft<kFeatSpheres | C, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
     } else if ((feat & ~kFeatMesh) == 0) {
         // the F_TRI bit of an instantiation <=> the scene has triangles (leaf_tris exists)
         if (feat & F_TRI) {
-            if (tex_basic) launch_paths_g_ft<kFeatMesh | C, kTexBasic>(num_cu, st, S, g, cam, w, next_slot);
-            else launch_paths_g_ft<kFeatMesh | C, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
+            if (tex_basic) return launch_paths_g_ft<kFeatMesh | C, kTexBasic>(num_cu, st, S, g, cam, w, next_slot);
+            else return launch_paths_g_ft<kFeatMesh | C, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
         } else {
-            if (tex_basic) launch_paths_g_ft<(kFeatMesh & ~F_TRI) | C, kTexBasic>(num_cu, st, S, g, cam, w, next_slot);
-            else launch_paths_g_ft<(kFeatMesh & ~F_TRI) | C, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
+            if (tex_basic) return launch_paths_g_ft<(kFeatMesh & ~F_TRI) | C, kTexBasic>(num_cu, st, S, g, cam, w, next_slot);
+            else return launch_paths_g_ft<(kFeatMesh & ~F_TRI) | C, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
         }
     } else if ((feat & F_TRI) == 0) {  // e.g. the Next-Week final: no triangle code in the kernel
-        if (feat & F_MEDIA_G) launch_paths_g_ft<F_ALL & ~F_TRI, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
-        else launch_paths_g_ft<(F_ALL & ~F_TRI & ~F_MEDIA_G) | C, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
+        // a non-sphere medium boundary (F_MEDIA_G: the Cornell smoke boxes) traverses from t = -inf: 32-bit codes
+        if (feat & F_MEDIA_G) {
+            if (tex_basic) return launch_paths_g_ft<F_ALL & ~F_TRI, kTexBasic>(num_cu, st, S, g, cam, w, next_slot);
+            return launch_paths_g_ft<F_ALL & ~F_TRI, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
+        }
+        else return launch_paths_g_ft<(F_ALL & ~F_TRI & ~F_MEDIA_G) | C, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
     } else {
-        launch_paths_g_ft<F_ALL, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
+        return launch_paths_g_ft<F_ALL, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
     }
 }
 #endif
@@ -2145,6 +2159,7 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     g.inv_h1 = 1.0 / static_cast<double>(p.height - 1);
     g.stack = stack_rows(ds.max_stack);
     const int variant = extend_variant(ds, p.flags);
+    KernelId kid;  // the persistent kernel the passes ran (stays {0, 0, -1} for the wavefront variants)
     const bool mega = variant == EXT_MEGA || variant == EXT_MEGA_G;
     // Samples per pass: as many path slots as half of the free HBM holds (plus the workspace this renderer already
     // owns).  Every pass pays max_depth bounces of fixed launch/tail cost whatever its size, so on a 288 GB part the
@@ -2270,8 +2285,12 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
                     if (p.max_depth > 0) {
                         if (prof) mark();
                         g.chunk = path_chunk(g.P, I.num_cu);
-                        if (variant == EXT_MEGA) launch_paths(I.num_cu, stream, ds.view, g, cam, w, counter(w, 0, 0, 0));
-                        else launch_paths_g(ds.features, ds.tex_basic, ds.codes16, I.num_cu, stream, ds.view, g, cam, w, counter(w, 0, 0, 0));
+                        if (variant == EXT_MEGA) {
+                            launch_paths(I.num_cu, stream, ds.view, g, cam, w, counter(w, 0, 0, 0));
+                            kid = KernelId{kFeatSpheres, 0, 3};
+                        } else {
+                            kid = launch_paths_g(ds.features, ds.tex_basic, ds.codes16, I.num_cu, stream, ds.view, g, cam, w, counter(w, 0, 0, 0));
+                        }
                         if (prof) { mark(); mark(); }
                         ++ext_launches;
                     }
@@ -2392,6 +2411,9 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     stats.samples_per_pass = static_cast<int>(k);
     stats.segments = segs;
     stats.extend_variant = variant;
+    stats.kernel_features = kid.f;
+    stats.kernel_textures = kid.tf;
+    stats.kernel_lds_mode = kid.lm;
     stats.primary = traced * static_cast<uint64_t>(stopped ? spp_done : spp_t);
     if (prof) {
         double ext_ms = 0, sh_ms = 0;
@@ -2410,9 +2432,16 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     }
 }
 
-void Renderer::trace_rays(const double* rays, size_t n, bool global_scene, double* t_out, double* n_out) {
+void Renderer::upload() {
     HIP_OK(hipSetDevice(impl_->device));
-    if (!impl_->up64) { build_device_scene(impl_->flat, impl_->s64); impl_->up64 = true; }
+    if (!impl_->up64) {
+        build_device_scene(impl_->flat, impl_->s64);
+        impl_->up64 = true;
+    }
+}
+
+void Renderer::trace_rays(const double* rays, size_t n, bool global_scene, double* t_out, double* n_out) {
+    upload();
     const DeviceScene<double>& ds = impl_->s64;
     if (n == 0) return;
     if (n > (1u << 30)) throw std::runtime_error("too many rays");
@@ -2448,9 +2477,8 @@ void Renderer::trace_rays(const double* rays, size_t n, bool global_scene, doubl
 }
 
 void Renderer::render(const CameraRec<double>& cam, const RenderParams& p, uint8_t* out_rgb, double* out_acc, RenderStats& stats) {
-    HIP_OK(hipSetDevice(impl_->device));
     if (p.fp_mode != RT_FP64) throw std::runtime_error("fp_mode must be RT_FP64");
-    if (!impl_->up64) { build_device_scene(impl_->flat, impl_->s64); impl_->up64 = true; }
+    upload();
     render_impl<double>(*impl_, impl_->s64, cam, p, out_rgb, out_acc, stats);
 }
 

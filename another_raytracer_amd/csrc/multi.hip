@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "multi.h"
+#include "options.h"
 
 namespace art {
 
@@ -110,11 +111,37 @@ static bool rccl_ok(ncclResult_t r) { return r == ncclSuccess || r == ncclInProg
     } while (0)
 
 using Clock = std::chrono::steady_clock;
-static Clock::time_point deadline_from_now() {
-    const char* s = std::getenv("ART_MULTI_TIMEOUT_MS");
-    const double ms = (!s || !*s) ? 120000.0 : std::max(0.0, std::strtod(s, nullptr));
+static Clock::time_point deadline_from_now() {  // option multi.timeout_ms (default: ART_MULTI_TIMEOUT_MS, else 120 s)
+    const double ms = opt(Opt::MultiTimeoutMs);
     return Clock::now() + std::chrono::duration_cast<Clock::duration>(std::chrono::duration<double, std::milli>(ms));
 }
+
+// One ncclGroupStart / ncclGroupEnd bracket that is closed on every exit path.  RCCL's group depth is per thread: a
+// throw between the two (a failed ncclCommInitRankConfig / ncclGather issue, a failed hipSetDevice) would leave the
+// caller's thread inside the group, and its next rt_multi_create or rt_render_multi would have its collectives
+// absorbed into that stale group.  end() closes the group and reports ncclGroupEnd's result; the destructor closes a
+// group still open during unwinding (its result is moot: the caller aborts the communicators and rethrows).
+class RcclGroup {
+public:
+    RcclGroup() {
+        const ncclResult_t r = ncclGroupStart();
+        if (!rccl_ok(r)) throw std::runtime_error(std::string("ncclGroupStart: ") + ncclGetErrorString(r));
+        open_ = true;
+    }
+    ~RcclGroup() {
+        if (open_) (void)ncclGroupEnd();
+    }
+    RcclGroup(const RcclGroup&) = delete;
+    RcclGroup& operator=(const RcclGroup&) = delete;
+    void end() {
+        open_ = false;
+        const ncclResult_t r = ncclGroupEnd();
+        if (!rccl_ok(r)) throw std::runtime_error(std::string("ncclGroupEnd: ") + ncclGetErrorString(r));
+    }
+
+private:
+    bool open_ = false;
+};
 
 struct MultiRenderer::Impl {
     std::vector<int> devices;
@@ -214,7 +241,12 @@ MultiRenderer::MultiRenderer(const FlatScene& flat, const std::vector<int>& devi
     }
     const int n = static_cast<int>(devices.size());
     impl_->devices = devices;
-    for (int k = 0; k < n; ++k) impl_->renderers.push_back(std::make_unique<Renderer>(flat, devices[k]));
+    // the scene is uploaded to every device here, not at the first render: a timed rt_render_multi is the render (the
+    // reference times engine::run only, main.cpp:44-46)
+    for (int k = 0; k < n; ++k) {
+        impl_->renderers.push_back(std::make_unique<Renderer>(flat, devices[k]));
+        impl_->renderers.back()->upload();
+    }
     impl_->streams.assign(n, nullptr);
     impl_->send.resize(n);
     for (int k = 0; k < n; ++k) {
@@ -230,16 +262,23 @@ MultiRenderer::MultiRenderer(const FlatScene& flat, const std::vector<int>& devi
     ncclUniqueId id;
     RCCL_CHECK(ncclGetUniqueId(&id));
     ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-    const char* blk = std::getenv("ART_RCCL_BLOCKING");  // diagnosis: 1 = blocking communicators
-    cfg.blocking = (blk && std::atoi(blk) == 1) ? 1 : 0;
+    cfg.blocking = opt(Opt::RcclBlocking) != 0 ? 1 : 0;  // option multi.rccl_blocking (diagnosis)
     impl_->comms.assign(n, nullptr);
     const auto deadline = deadline_from_now();
-    RCCL_ISSUE(ncclGroupStart());
-    for (int k = 0; k < n; ++k) {
-        HIP_CHECK(hipSetDevice(devices[k]));
-        RCCL_ISSUE(ncclCommInitRankConfig(&impl_->comms[k], n, id, k, &cfg));
+    try {
+        RcclGroup group;
+        for (int k = 0; k < n; ++k) {
+            HIP_CHECK(hipSetDevice(devices[k]));
+            RCCL_ISSUE(ncclCommInitRankConfig(&impl_->comms[k], n, id, k, &cfg));
+            if (k == n - 1 && opt(Opt::FaultRcclGroup) == 1)  // fault point (tests): an error inside the init group
+                throw std::runtime_error("ncclCommInitRankConfig: injected failure (test.fault_rccl_group = 1)");
+        }
+        group.end();
+    } catch (const std::exception& e) {
+        // the group is closed (RcclGroup); half-created communicators are aborted, not destroyed: a destroy would wait
+        // for peers that may never come
+        impl_->abort_all(std::string("RCCL communicator init: ") + e.what());
     }
-    RCCL_ISSUE(ncclGroupEnd());
     impl_->wait_comms("RCCL communicator init", deadline);
     impl_->times.ngpus = n;
     guard.release();
@@ -310,17 +349,25 @@ void MultiRenderer::render(const CameraRec<double>& cam, const RenderParams& p, 
     const auto deadline = deadline_from_now();
     HIP_CHECK(hipSetDevice(I.devices[0]));
     HIP_CHECK(hipEventRecord(I.ev[0], I.streams[0]));
-    RCCL_ISSUE(ncclGroupStart());
-    for (int k = 0; k < n; ++k) {
-        HIP_CHECK(hipSetDevice(I.devices[k]));
-        RCCL_ISSUE(ncclGather(I.send[k].p, k == 0 ? I.recv.p : nullptr, block, ncclUint8, 0, I.comms[k], I.streams[k]));
+    try {
+        RcclGroup group;
+        for (int k = 0; k < n; ++k) {
+            HIP_CHECK(hipSetDevice(I.devices[k]));
+            RCCL_ISSUE(ncclGather(I.send[k].p, k == 0 ? I.recv.p : nullptr, block, ncclUint8, 0, I.comms[k], I.streams[k]));
+            if (k == n - 1 && opt(Opt::FaultRcclGroup) == 2)  // fault point (tests): an error inside the gather group
+                throw std::runtime_error("ncclGather: injected failure inside the group (test.fault_rccl_group = 2)");
+        }
+        group.end();
+    } catch (const std::exception& e) {
+        // part of the group may have been issued to some ranks: the communicators cannot be trusted any more
+        I.times = tm;
+        I.abort_all(std::string("ncclGather issue: ") + e.what());
     }
-    RCCL_ISSUE(ncclGroupEnd());
     ++I.times.collectives;
     tm.collectives = I.times.collectives;
     I.times = tm;
-    // fault injection (tests): the collective fails while in flight, as a peer error or an expired deadline would
-    if (std::getenv("ART_FAULT_GATHER_ABORT")) I.abort_all("ncclGather: injected failure (ART_FAULT_GATHER_ABORT)");
+    // fault point (tests): the collective fails while in flight, as a peer error or an expired deadline would
+    if (opt(Opt::FaultGatherAbort) != 0) I.abort_all("ncclGather: injected failure (test.fault_gather_abort)");
     const auto tw = clock::now();
     I.wait_comms("ncclGather launch", deadline);  // non-blocking group: the gathers are enqueued once this returns
     HIP_CHECK(hipSetDevice(I.devices[0]));
@@ -356,6 +403,9 @@ void MultiRenderer::render(const CameraRec<double>& cam, const RenderParams& p, 
     stats.samples_per_pass = st[0].samples_per_pass;
     stats.local_rows = H;
     stats.extend_variant = st[0].extend_variant;
+    stats.kernel_features = st[0].kernel_features;
+    stats.kernel_textures = st[0].kernel_textures;
+    stats.kernel_lds_mode = st[0].kernel_lds_mode;
     tm.total_ms = stats.ms;
     I.times = tm;
 }

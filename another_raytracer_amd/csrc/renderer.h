@@ -30,6 +30,8 @@ struct RenderStats {
     uint64_t extend_launches = 0, shade_launches = 0;
     int passes = 0, samples_per_pass = 0, local_rows = 0;
     int extend_variant = 0;
+    uint32_t kernel_features = 0, kernel_textures = 0;  // the persistent kernel: k_paths_g<F, TF, LM> / k_paths (LM 3)
+    int kernel_lds_mode = -1;
 };
 
 class Renderer {
@@ -39,6 +41,8 @@ public:
     ~Renderer();
     Renderer(const Renderer&) = delete;
     Renderer& operator=(const Renderer&) = delete;
+    // Uploads the scene to the device now (render and trace_rays otherwise do it at their first call).
+    void upload();
     void render(const CameraRec<double>& cam, const RenderParams& p, uint8_t* out_rgb, double* out_acc, RenderStats& stats);
     // Closest hit of n rays (rays: n x {ox, oy, oz, dx, dy, dz, tm}) through the renderer's traversal: t (inf on a
     // miss) and the face normal (n x 3), host buffers; global_scene forces the HBM traversal on an LDS-image scene.

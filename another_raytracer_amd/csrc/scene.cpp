@@ -1,6 +1,7 @@
 // scene.cpp — scene graph builder, builtin scene recipes, canonical dump and compilation (see scene.h).
 #include "scene.h"
 #include "imagedec.h"
+#include "options.h"
 
 #include <algorithm>
 #include <cctype>
@@ -675,17 +676,11 @@ std::string dump_scene(const SceneGraph& g) {
 // ------------------------------------------------------------------------------------------------ compile
 namespace {
 // BVH primitive hoisting (Compiler::obj, N_BVH): at most kMaxHoist primitives of a BVH of >= kHoistMinPrims whose box
-// area is >= kHoistAreaShare of the whole BVH's.  ART_HOIST=0 turns it off (builder experiments, tools/).
+// area is >= kHoistAreaShare of the whole BVH's.  Option compile.hoist = 0 turns it off (builder experiments).
 constexpr size_t kHoistMinPrims = 8;
 constexpr size_t kMaxHoist = 4;
 constexpr double kHoistAreaShare = 0.5;
-bool hoist_enabled() {
-    static const bool v = [] {
-        const char* e = std::getenv("ART_HOIST");
-        return !(e && e[0] == '0');
-    }();
-    return v;
-}
+bool hoist_enabled() { return opt(Opt::Hoist) != 0; }
 AABBd box_union(const AABBd& a, const AABBd& b) {
     AABBd r;
     for (int k = 0; k < 3; ++k) {
@@ -918,14 +913,11 @@ struct Compiler {
     // to exact-t ties, as any BVH); a constant_medium ends a run, so every medium still sees the closest hit of the
     // objects before it when it clips its interval and decides whether to draw (constant_medium.h:37-62): the RNG
     // sequence is unchanged.  The loose primitives are then tested only when a ray enters their boxes instead of
-    // once per segment by every lane.  ART_WORLD_MERGE=0 turns it off, 1 merges BVH runs only (experiments, tools/).
+    // once per segment by every lane.  Option compile.world_merge = 0 turns it off, 1 merges BVH runs only (experiments).
     void world(const std::vector<int>& roots) {
         std::vector<int> items;
         for (int w : roots) flatten(w, items);
-        static const int merge = [] {
-            const char* e = std::getenv("ART_WORLD_MERGE");
-            return e ? std::atoi(e) : 2;
-        }();
+        const int merge = static_cast<int>(opt(Opt::WorldMerge));
         auto mergeable = [&](int idx) { const NodeType t = g.nodes[idx].type; return t == N_BVH || is_prim(t); };
         for (size_t i = 0; i < items.size();) {
             size_t j = i;

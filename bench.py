@@ -99,6 +99,8 @@ def parse():
     ap.add_argument("--cpu-baseline-spp", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true", help="skip the oracle check of the timed frame's rows")
+    ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
+                    help="rt_option_set before the scene is built (builder experiments, e.g. bvh.sah_ci=1.0; repeatable)")
     return ap.parse_args()
 
 
@@ -202,11 +204,12 @@ def latest_pmc(precision, scene, variant, build):
     return best
 
 
-def choose_driver(gpus, world_env, device_count):
-    """How `bench.py --gpus N` runs: ("procs", N) under torchrun (one process per GPU, WORLD_SIZE = N ranks), else
+def choose_driver(gpus, world_env, device_count, torchrun=False):
+    """How `bench.py --gpus N` runs: ("procs", N) under torchrun (one process per GPU, WORLD_SIZE = N ranks; a single
+    torchrun rank too, which is how the one-process-per-GPU A/B switches run on one GPU), else
     ("multi", N): this one process drives N GPUs through the C ABI (rt_render_multi: one host thread and one RCCL rank
     per device, ncclGather + unpack kernel on device 0).  Never silently fewer GPUs than asked: SystemExit instead."""
-    if world_env > 1:
+    if world_env > 1 or torchrun:
         if gpus is not None and gpus != world_env:
             raise SystemExit(f"bench.py: --gpus {gpus} but torchrun started WORLD_SIZE={world_env} ranks")
         return "procs", world_env
@@ -268,7 +271,7 @@ def main():
     import torch.distributed as dist
 
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
-    driver, n = choose_driver(args.gpus, world_env, torch.cuda.device_count())
+    driver, n = choose_driver(args.gpus, world_env, torch.cuda.device_count(), torchrun="TORCHELASTIC_RUN_ID" in os.environ)
     rank = int(os.environ.get("RANK", "0"))
     if driver == "procs":
         local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -286,6 +289,9 @@ def main():
     from another_raytracer_amd.distributed import frame_renderer, multi_engine
 
     build = kernel_build_id()
+    for o in args.option:
+        name, _, value = o.partition("=")
+        art.set_option(name, float(value))
     profile = not args.no_profile
     if driver == "multi":
         if args.global_scene or args.split_shade or args.wavefront or args.samples_per_pass:

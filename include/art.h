@@ -49,8 +49,11 @@ extern "C" {
  * e.g. one process per GPU over torch.distributed), rt_multi_ngpus, rt_multi_scene_info, rt_multi_device_stats.
  * ABI 4: rt_unpack_bands takes the byte sizes of both buffers and refuses a mismatch with the layout; rt_multi_times
  * (per-phase timing of the last rt_render_multi: renders, gather, unpack); rt_render_multi bounds its wait on the
- * collective (RT_E_DEVICE on an RCCL error or timeout, after which the rt_multi refuses further renders). */
-#define RT_ABI_VERSION 4
+ * collective (RT_E_DEVICE on an RCCL error or timeout, after which the rt_multi refuses further renders).
+ * ABI 5: rt_option_set / rt_option_get (process-wide options; the library reads no environment knobs but the documented
+ * ART_MULTI_TIMEOUT_MS); rt_stats.kernel_features / kernel_textures / kernel_lds_mode name the persistent kernel a
+ * render ran; rt_multi_create uploads the scene to every device before it returns. */
+#define RT_ABI_VERSION 5
 
 /* return codes */
 #define RT_OK 0
@@ -122,6 +125,10 @@ typedef struct rt_stats {
                                    2: LDS-resident scene with shading fused into the extend kernel (one launch per
                                    depth); 3: persistent paths (the fused bounce loop in registers, one launch per pass);
                                    4: persistent paths over the HBM scene (every other scene; k_paths_g) */
+    uint32_t kernel_features;   /* the persistent kernel that ran (variants 3, 4): k_paths_g<kernel_features, */
+    uint32_t kernel_textures;   /*   kernel_textures, kernel_lds_mode> (layout.h feature / texture bits; LDS mode 0: BVH */
+    int32_t kernel_lds_mode;    /*   in HBM, 1: whole BVH in LDS, 2: its top levels in LDS), or k_paths (LDS mode 3, the */
+                                /*   LDS scene image); -1 for the per-depth wavefront variants */
 } rt_stats;
 
 typedef struct rt_scene_info {  /* scene_manager.h:6-14 */
@@ -137,6 +144,21 @@ typedef struct rt_scene_info {  /* scene_manager.h:6-14 */
 int rt_abi_version(void);
 const char* rt_last_error(void);
 int rt_device_count(void);
+/* Process-wide options, by name (every one is also readable with rt_option_get).  The library reads no environment
+ * variables for them (only multi.timeout_ms falls back to ART_MULTI_TIMEOUT_MS while never set).  Unknown names and
+ * values outside an option's range are RT_E_INVALID; name NULL resets every option to its default.
+ *   compile.world_merge (2: 0 off, 1 BVH runs only), compile.hoist (1), bvh.collapse (0 greedy, 1 SAH-optimal DP),
+ *   bvh.collapse_ci (0.6), bvh.dp_binary_leaf (1), bvh.sah_ci (1.5), bvh.sah_leaf (4), bvh.sbvh (1.5), bvh.sbvh_alpha
+ *   (1e-5): scene compilation, for scenes built after the call (builder experiments; the defaults are what was measured
+ *   best);
+ *   render.codes16 (1; 0 = always the 32-bit-child-code kernels), render.lds_nodes_max (diagnostic cap on LDS nodes):
+ *   uploads and renders after the call;
+ *   multi.timeout_ms (the RCCL deadline), multi.rccl_blocking (0; 1 = blocking communicators, diagnosis);
+ *   test.fault_workspace_bytes (0 = off; N refuses workspace growth beyond N bytes), test.fault_gather_abort (0; 1 = the
+ *   next gather fails in flight), test.fault_rccl_group (0; 1 / 2 = an error inside rt_multi_create's / the gather's
+ *   RCCL group): fault points for the tests, each failing a later call exactly as the real fault would. */
+int rt_option_set(const char* name, double value);
+int rt_option_get(const char* name, double* value);
 
 /* ---- scenes ---- */
 /* Builtin scenes = scene_manager::build(alias): "1".."8" or "random", "two_spheres", "two_perlin_spheres", "earth",
@@ -204,7 +226,10 @@ void rt_image_free(uint8_t* pixels);
 /* ---- multi-GPU (one process, one host thread per GPU, RCCL) ----
  * Replaces the reference's CPU-parallel drivers (engine.h:335-376 _run_parallel_stripes: 4 threads on 4 row stripes;
  * SURVEY.md §8(b) rt_render_multi).  An rt_multi holds the scene uploaded on every listed device and one RCCL
- * communicator per device (one group of ncclCommInitRankConfig, non-blocking), made once at creation.  rt_render_multi renders the whole frame: device k
+ * communicator per device (one group of ncclCommInitRankConfig, non-blocking), both made at creation: the first
+ * rt_render_multi spends no time on the upload (the reference times engine::run only, main.cpp:44-46; the pass
+ * workspace, sized by the render's W, H and spp, is still allocated by the first render of a size).
+ * rt_render_multi renders the whole frame: device k
  * renders the row bands b (params->band_rows rows each) with b % ngpus == k -- params->band_count / band_index are
  * ignored -- packs them into one buffer, and a single ncclGather moves every device's block to devices[0], whose unpack
  * kernel writes the rows in image order.  out_rgb8: W*H*3 bytes, row 0 = top; host memory, or device memory on
@@ -213,9 +238,11 @@ void rt_image_free(uint8_t* pixels);
  * Threading: one rt_multi per process at a time per device set; calls are blocking.
  * Failure behaviour: a device whose render fails makes the call return that error before any collective starts (the
  * rt_multi stays usable).  The communicators are non-blocking (ncclConfig_t.blocking = 0); their creation and the
- * gather are polled (ncclCommGetAsyncError, hipStreamQuery) against a deadline of ART_MULTI_TIMEOUT_MS milliseconds
- * (environment, default 120000).  An RCCL error or an expired deadline aborts every communicator (ncclCommAbort) and
- * returns RT_E_DEVICE; the rt_multi then refuses renders until it is destroyed and created again. */
+ * gather are polled (ncclCommGetAsyncError, hipStreamQuery) against a deadline of multi.timeout_ms milliseconds
+ * (rt_option_set; while unset, the environment's ART_MULTI_TIMEOUT_MS, default 120000).  An RCCL error or an expired
+ * deadline aborts every communicator (ncclCommAbort) and returns RT_E_DEVICE; the rt_multi then refuses renders until
+ * it is destroyed and created again.  Both RCCL groups (creation, gather) are closed on every error path and the
+ * communicators aborted, so a failure never leaves the calling thread inside an open ncclGroupStart. */
 typedef struct rt_multi rt_multi;
 int rt_multi_create(const char* name, const char* asset_dir, const int* devices, int ngpus, rt_multi** out);
 int rt_multi_from_graph(rt_graph* g, const int* devices, int ngpus, rt_multi** out);

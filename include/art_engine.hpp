@@ -120,6 +120,13 @@ private:
 };
 
 // Writes a built or loaded scene as a versioned flat-scene file (rt_scene_save); scene_manager::load reads it back.
+// Process-wide library options (rt_option_set / rt_option_get: builder experiments, the RCCL deadline, test fault points)
+inline void set_option(const std::string& name, double value) { check(rt_option_set(name.c_str(), value), "rt_option_set"); }
+inline double get_option(const std::string& name) {
+    double v = 0;
+    check(rt_option_get(name.c_str(), &v), "rt_option_get");
+    return v;
+}
 inline void save_scene(const scene& world, const std::string& path) { check(rt_scene_save(world.objects.get(), path.c_str()), "save_scene"); }
 
 // The engine with a runtime image size (the reference fixes W, H, C at compile time: engine<W,H,C> below); samples

@@ -34,6 +34,15 @@ def has_gpu():
         return False
 
 
+@pytest.fixture
+def options():
+    """rt_option_set for one test: every library option is back at its default afterwards."""
+    import another_raytracer_amd as art
+    art.set_option(None, 0)
+    yield art.set_option
+    art.set_option(None, 0)
+
+
 @pytest.fixture(scope="session")
 def gpu():
     if not has_gpu():

@@ -27,7 +27,7 @@ def test_every_declared_symbol_is_exported_and_bound():
     exported = set(re.findall(r" T (rt_\w+)", nm))
     assert set(decl) <= exported, set(decl) - exported
     assert set(decl) == set(_lib.SIGNATURES), set(decl) ^ set(_lib.SIGNATURES)
-    assert _lib.lib.rt_abi_version() == _lib.RT_ABI_VERSION == 4
+    assert _lib.lib.rt_abi_version() == _lib.RT_ABI_VERSION == 5
 
 
 def test_struct_layouts_match_the_header(tmp_path):
@@ -49,6 +49,57 @@ def test_struct_layouts_match_the_header(tmp_path):
         assert int(c[st]) == ctypes.sizeof(cls), st
         for f in fs:
             assert int(c[f"{st}.{f}"]) == getattr(cls, f).offset, f"{st}.{f}"
+
+
+OPTIONS = {  # include/art.h rt_option_set: name -> default
+    "compile.world_merge": 2, "compile.hoist": 1, "bvh.collapse": 0, "bvh.collapse_ci": 0.6, "bvh.dp_binary_leaf": 1,
+    "bvh.sah_ci": 1.5, "bvh.sah_leaf": 4, "bvh.sbvh": 1.5, "bvh.sbvh_alpha": 1e-5, "render.codes16": 1,
+    "render.lds_nodes_max": 4294967295, "multi.rccl_blocking": 0, "test.fault_workspace_bytes": 0,
+    "test.fault_gather_abort": 0, "test.fault_rccl_group": 0,
+}
+
+
+def test_options_defaults_set_get_and_reset():
+    art.set_option(None, 0)
+    for name, default in OPTIONS.items():
+        assert art.get_option(name) == pytest.approx(default), name
+    art.set_option("compile.world_merge", 1)
+    art.set_option("test.fault_workspace_bytes", 1 << 20)
+    art.set_option("multi.timeout_ms", 2500)
+    assert art.get_option("compile.world_merge") == 1 and art.get_option("test.fault_workspace_bytes") == 1 << 20
+    assert art.get_option("multi.timeout_ms") == 2500
+    art.set_option(None, 0)  # NULL name: every option back to its default
+    assert art.get_option("compile.world_merge") == 2 and art.get_option("test.fault_workspace_bytes") == 0
+    assert art.get_option("multi.timeout_ms") == 120000  # unset: ART_MULTI_TIMEOUT_MS (not set here) or 120 s
+
+
+@pytest.mark.parametrize("name,value", [("no.such.option", 1), ("compile.world_merge", 3), ("compile.hoist", 0.5),
+                                        ("bvh.sah_leaf", 0), ("bvh.sah_ci", -1), ("test.fault_rccl_group", 7)])
+def test_options_refuse_unknown_names_and_out_of_range_values(name, value):
+    before = {n: art.get_option(n) for n in OPTIONS}
+    with pytest.raises(art.RTError) as e:
+        art.set_option(name, value)
+    assert e.value.code == -1 and name in str(e.value)
+    assert {n: art.get_option(n) for n in OPTIONS} == before  # a refused value changes nothing
+
+
+def test_environment_knobs_no_longer_change_the_tree():
+    # the r4 builder knobs were environment variables; now only rt_option_set changes the compiled scene (a stray
+    # variable in an embedding application's environment is ignored)
+    import sys
+    code = ("import sys; sys.path.insert(0, {root!r}); import another_raytracer_amd as art; "
+            "w = art.scene_manager().build('8'); print(w.info['bvh_nodes'], w.info['objects'])").format(root=ROOT)
+    env = dict(os.environ, ART_WORLD_MERGE="0", ART_BVH_COLLAPSE="1", ART_HOIST="0", ART_SAH_LEAF="2", ART_CODE16="0",
+               ART_FAULT_WORKSPACE_BYTES="1", ART_FAULT_GATHER_ABORT="1")
+    plain = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, check=True, timeout=300).stdout.split()
+    knobs = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True, timeout=300).stdout.split()
+    assert plain == knobs == ["566", "6"]
+    art.set_option("compile.world_merge", 0)
+    try:
+        info = art.scene_manager().build("8").info
+    finally:
+        art.set_option("compile.world_merge", 2)
+    assert info["objects"] > 6  # the option does take effect
 
 
 @pytest.mark.parametrize("H,band_rows,bands", [(1080, 16, 1), (1080, 16, 8), (37, 4, 3), (5, 16, 4), (225, 8, 7)])

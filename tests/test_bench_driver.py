@@ -30,6 +30,9 @@ def test_torchrun_world_must_match_gpus():
     assert bench.choose_driver(None, 4, 8) == ("procs", 4)
     with pytest.raises(SystemExit, match="WORLD_SIZE=4"):
         bench.choose_driver(8, 4, 8)
+    # one torchrun rank (WORLD_SIZE 1) is the per-process driver too: the A/B switches (--global-scene ...) need it
+    assert bench.choose_driver(None, 1, 1, torchrun=True) == ("procs", 1)
+    assert bench.choose_driver(1, 1, 8, torchrun=True) == ("procs", 1)
 
 
 def test_bench_exits_nonzero_without_the_gpus():

@@ -93,19 +93,19 @@ def test_adaptive_mode_refuses_accum_and_off_grid_sizes(gpu):
         e.run(np.zeros((40, 64, 3), np.uint8))
 
 
-def test_workspace_allocation_failure_leaves_the_scene_usable(gpu, monkeypatch):
-    # a refused workspace allocation (fault injection: ART_FAULT_WORKSPACE_BYTES) is reported as RT_E_DEVICE, and the
-    # next render on the same scene allocates again instead of using a stale size with a null base
+def test_workspace_allocation_failure_leaves_the_scene_usable(gpu, options):
+    # a refused workspace allocation (fault point: option test.fault_workspace_bytes) is reported as RT_E_DEVICE, and
+    # the next render on the same scene allocates again instead of using a stale size with a null base
     e = make()
     first = np.zeros((40, 64, 3), np.uint8)
     e.run(first)
     big = make(W=256, H=160)
     big._scene = e._scene  # same rt_scene (and renderer workspace), larger frame: the workspace must grow
-    monkeypatch.setenv("ART_FAULT_WORKSPACE_BYTES", "1024")
+    options("test.fault_workspace_bytes", 1024)
     with pytest.raises(art.RTError) as err:
         big.run(np.zeros((160, 256, 3), np.uint8))
-    assert err.value.code == -3 and "ART_FAULT_WORKSPACE_BYTES" in str(err.value)
-    monkeypatch.delenv("ART_FAULT_WORKSPACE_BYTES")
+    assert err.value.code == -3 and "test.fault_workspace_bytes" in str(err.value)
+    options("test.fault_workspace_bytes", 0)
     again = np.zeros((40, 64, 3), np.uint8)
     e.run(again)
     assert np.array_equal(again, first)
@@ -231,7 +231,7 @@ def test_render_multi_phase_times(gpu):
     assert m.times()["collectives"] == 2
 
 
-def test_render_multi_failed_render_starts_no_collective(gpu, monkeypatch):
+def test_render_multi_failed_render_starts_no_collective(gpu, options):
     # a device whose render fails (fault injection: its workspace growth is refused) ends rt_render_multi with RT_E_DEVICE
     # before the gather -- no collective starts -- and the multi renders correctly afterwards
     m = _multi()
@@ -239,33 +239,70 @@ def test_render_multi_failed_render_starts_no_collective(gpu, monkeypatch):
     m.run(first)
     assert m.times()["collectives"] == 1
     m.width, m.height = 256, 160  # a larger frame: the renderer's workspace must grow
-    monkeypatch.setenv("ART_FAULT_WORKSPACE_BYTES", "1024")
+    options("test.fault_workspace_bytes", 1024)
     with pytest.raises(art.RTError) as err:
         m.run(np.zeros((160, 256, 3), np.uint8))
-    assert err.value.code == -3 and "ART_FAULT_WORKSPACE_BYTES" in str(err.value)
+    assert err.value.code == -3 and "test.fault_workspace_bytes" in str(err.value)
     assert m.times()["collectives"] == 1
-    monkeypatch.delenv("ART_FAULT_WORKSPACE_BYTES")
+    options("test.fault_workspace_bytes", 0)
     m.width, m.height = 64, 40
     again = np.zeros((40, 64, 3), np.uint8)
     m.run(again)
     assert np.array_equal(again, first) and m.times()["collectives"] == 2
 
 
-def test_render_multi_gather_failure_aborts_and_is_reported(gpu, monkeypatch):
-    # a collective that fails in flight (fault injection after ncclGroupEnd, as a peer error or an expired
-    # ART_MULTI_TIMEOUT_MS deadline would) aborts the communicators and returns RT_E_DEVICE; that rt_multi then refuses
-    # to render, and a new one works
+def test_render_multi_gather_failure_aborts_and_is_reported(gpu, options):
+    # a collective that fails in flight (fault point after ncclGroupEnd, as a peer error or an expired multi.timeout_ms
+    # deadline would) aborts the communicators and returns RT_E_DEVICE; that rt_multi then refuses to render, and a new
+    # one works
     m = _multi()
     ref = np.zeros((40, 64, 3), np.uint8)
     m.run(ref)
-    monkeypatch.setenv("ART_FAULT_GATHER_ABORT", "1")
+    options("test.fault_gather_abort", 1)
     with pytest.raises(art.RTError) as err:
         m.run(np.zeros((40, 64, 3), np.uint8))
     assert err.value.code == -3 and "injected" in str(err.value)
-    monkeypatch.delenv("ART_FAULT_GATHER_ABORT")
+    options("test.fault_gather_abort", 0)
     with pytest.raises(art.RTError, match="unusable"):
         m.run(np.zeros((40, 64, 3), np.uint8))
     del m
     fresh = np.zeros((40, 64, 3), np.uint8)
     _multi().run(fresh)
     assert np.array_equal(fresh, ref)
+
+
+@pytest.mark.parametrize("where", [1, 2])
+def test_failure_inside_an_rccl_group_leaves_the_thread_usable(gpu, options, where):
+    # an error between ncclGroupStart and ncclGroupEnd (fault point test.fault_rccl_group: 1 = inside
+    # rt_multi_create's communicator-init group, 2 = inside rt_render_multi's gather group) must close the group and
+    # abort the communicators before it is reported, or the calling thread stays inside the group and its next
+    # collectives are absorbed into it.  After the failure a new rt_multi on this same thread creates, renders and
+    # matches rt_render.
+    ref = np.zeros((40, 64, 3), np.uint8)
+    make(spp=4).run(ref)
+    options("test.fault_rccl_group", where)
+    with pytest.raises(art.RTError) as err:
+        m = _multi()
+        m.run(np.zeros((40, 64, 3), np.uint8))
+    assert err.value.code == -3 and "injected" in str(err.value) and "aborted" in str(err.value)
+    if where == 2:  # the multi whose gather failed refuses further renders
+        with pytest.raises(art.RTError, match="unusable"):
+            m.run(np.zeros((40, 64, 3), np.uint8))
+        del m
+    options("test.fault_rccl_group", 0)
+    for _ in range(2):  # a second create + render on the same thread: no stale group state
+        fresh = np.zeros((40, 64, 3), np.uint8)
+        m2 = _multi()
+        m2.run(fresh)
+        assert np.array_equal(fresh, ref) and m2.times()["collectives"] == 1
+        del m2
+
+
+def test_multi_create_uploads_the_scene(gpu):
+    # rt_multi_create uploads the scene to every device before it returns (a timed first render of a fresh
+    # multi_engine must not include the upload; the reference times engine::run only, main.cpp:44-46)
+    m = _multi("8")
+    info = m.scene_info()
+    assert info["device_bytes_f64"] > 0  # before any render
+    m.run(np.zeros((40, 64, 3), np.uint8))
+    assert m.scene_info()["device_bytes_f64"] == info["device_bytes_f64"]

@@ -60,16 +60,23 @@ def test_f64_matches_oracle_pcg(gpu, scene):
     assert g["segments"] == o["segments"]
 
 
+F_CODE16 = 1 << 7  # layout.h feature bit of the 16-bit-child-code instantiations
+
+
 @pytest.mark.parametrize("scene", ["cow", "dino", "8", "5"])
-def test_32bit_code_kernels_match_oracle_pcg(gpu, monkeypatch, scene):
+def test_32bit_code_kernels_match_oracle_pcg(gpu, options, scene):
     # a scene whose BVH codes do not fit 16 bits (> 32768 nodes or > 8192 primitive references) takes the k_paths_g
-    # instantiations without F_CODE16 (float keys, 32-bit stack entries); ART_CODE16=0 forces that path on scenes that
-    # fit, so its traversal is pinned for triangle scenes (cow: LM 2, dino: LM 1) and triangle-free ones (final, Cornell)
-    monkeypatch.setenv("ART_CODE16", "0")
+    # instantiations without F_CODE16 (float keys, 32-bit stack entries); option render.codes16 = 0 forces that path on
+    # scenes that fit, so its traversal is pinned for triangle scenes (cow: LM 2, dino: LM 1) and triangle-free ones
+    # (final, Cornell).  rt_stats names the kernel that ran (the test must see the 32-bit-code kernel run).
     W, H, spp = 48, 27, 4
+    default = gpu_render(scene, W, H, spp)["stats"]
+    options("render.codes16", 0)
     g = gpu_render(scene, W, H, spp)
     o = oracle_render(scene, W, H, spp, mode="pcg")
     assert g["stats"]["extend_variant"] == 4
+    assert g["stats"]["kernel_features"] & F_CODE16 == 0, g["stats"]
+    assert default["kernel_features"] & F_CODE16, default
     assert np.array_equal(g["rgb"], o["rgb"]) and np.array_equal(g["acc"], o["acc"]) and g["segments"] == o["segments"]
 
 

@@ -149,41 +149,27 @@ def _leaf_cover(blob):
     return len(nodes), covered, sizes
 
 
-_COLLAPSE_PROBE = r"""
-import sys, tempfile, pathlib
-sys.path.insert(0, {root!r})
-import numpy as np
-import another_raytracer_amd as art
-from tests.test_scene_compile import _leaf_cover
-out = []
-for name in ("1", "8", "cow", "dino"):
-    with tempfile.TemporaryDirectory() as d:
-        p = pathlib.Path(d) / "s.artscene"
-        art.save_scene(art.scene_manager().build(name), p)
-        art.scene_manager().load(p)  # the loader recomputes max_stack / depth and checks every index
-        n, covered, sizes = _leaf_cover(bytearray(p.read_bytes()))
-        out.append((name, n, int(covered.min()), int(covered.max()), max(sizes)))
-print(out)
-"""
-
-
-@pytest.mark.parametrize("mode", ["0", "1"])
-def test_bvh_collapse_covers_every_reference_once(mode):
-    # bvh.cpp collapse: greedy (ART_BVH_COLLAPSE=0, the default) and SAH-optimal dynamic programming (1, which also
+@pytest.mark.parametrize("mode", [0, 1])
+def test_bvh_collapse_covers_every_reference_once(mode, tmp_path):
+    # bvh.cpp collapse: greedy (option bvh.collapse = 0, the default) and SAH-optimal dynamic programming (1, which also
     # merges binary leaves into one wide-tree leaf): every primitive reference sits in exactly one leaf of at most
-    # kMaxLeafPrims (4), except the random scene's hoisted ground sphere (no leaf); the knob is read once per process
-    import ast
-    import os
-    import subprocess
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, ART_BVH_COLLAPSE=mode)
-    r = subprocess.run([sys.executable, "-c", _COLLAPSE_PROBE.format(root=root)], env=env, capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stderr
-    res = ast.literal_eval(r.stdout.strip().splitlines()[-1])
+    # kMaxLeafPrims (4), except the random scene's hoisted ground sphere (no leaf); the option applies to scenes
+    # compiled after it is set
+    import pathlib
+    art.set_option("bvh.collapse", mode)
+    try:
+        res = []
+        for name in ("1", "8", "cow", "dino"):
+            p = pathlib.Path(tmp_path) / f"s{name}.artscene"
+            art.save_scene(art.scene_manager().build(name), p)
+            art.scene_manager().load(p)  # the loader recomputes max_stack / depth and checks every index
+            n, covered, sizes = _leaf_cover(bytearray(p.read_bytes()))
+            res.append((name, n, int(covered.min()), int(covered.max()), max(sizes)))
+    finally:
+        art.set_option("bvh.collapse", 0)
     for name, n, lo, hi, biggest in res:
         assert hi == 1 and biggest <= 4, (name, hi, biggest)
         assert lo == (0 if name == "1" else 1), name
     nodes = {name: n for name, n, *_ in res}
-    if mode == "1":  # the optimal collapse fills the 4-wide nodes: fewer nodes than the greedy one's 259 / 566 / 1884 / 159
+    if mode == 1:  # the optimal collapse fills the 4-wide nodes: fewer nodes than the greedy one's 259 / 566 / 1884 / 159
         assert nodes["1"] < 259 and nodes["8"] < 566 and nodes["cow"] < 1884 and nodes["dino"] < 159
