@@ -149,14 +149,38 @@ template <> struct HitRecD<double> {
 
 template <class R> struct ResRec;  // final per-slot radiance
 template <> struct ResRec<float> { float4 v; };
+#ifndef ART_RES_PITCH
+#define ART_RES_PITCH 24
+#endif
+#ifndef ART_RES_NT
+#define ART_RES_NT 1
+#endif
+#if ART_RES_PITCH == 32
+template <> struct alignas(32) ResRec<double> { double x, y, z, pad; };  // one 32-B sector per record
+#else
 template <> struct ResRec<double> { double x, y, z; };  // 24 B, unpadded: k_accum streams these at HBM rate
+#endif
 __device__ __forceinline__ void store_res(ResRec<float>* res, uint32_t q, V3<float> L) { res[q].v = make_float4(L.x, L.y, L.z, 0.0f); }
 // The radiance records stream out with non-temporal stores (read once, by k_accum after the pass), so they
 // do not evict the L2-resident camera-ray rings of k_paths
 __device__ __forceinline__ void store_res(ResRec<double>* res, uint32_t q, V3<double> L) {
+#if ART_RES_PITCH == 32
+    typedef double d4v __attribute__((ext_vector_type(4)));
+    const d4v v = {L.x, L.y, L.z, 0.0};
+#if ART_RES_NT
+    __builtin_nontemporal_store(v, reinterpret_cast<d4v*>(&res[q]));
+#else
+    *reinterpret_cast<d4v*>(&res[q]) = v;
+#endif
+#elif ART_RES_NT
     __builtin_nontemporal_store(L.x, &res[q].x);
     __builtin_nontemporal_store(L.y, &res[q].y);
     __builtin_nontemporal_store(L.z, &res[q].z);
+#else
+    res[q].x = L.x;
+    res[q].y = L.y;
+    res[q].z = L.z;
+#endif
 }
 __device__ __forceinline__ void load_res(const ResRec<float>* res, uint32_t q, double& r, double& g, double& b) {
     const float4 v = res[q].v;

@@ -74,7 +74,10 @@ def gather_frame(send, height, band_rows, group=None, dst=0, recv=None, frame=No
     """Gathers every rank's padded block `send` ([block_rows, W, C]: its band rows first, as rendered in place by
     render_frame) to `dst` with one collective (RCCL on GPUs, gloo on CPU), then places the rows with rt_unpack_bands.
     Returns the [H, W, C] frame on dst (None elsewhere).  A `send` that is not exactly one padded block is refused on
-    every rank before the collective (the unpadded [rows_r, W, C] form of ABI 3 included)."""
+    every rank before the collective (the unpadded [rows_r, W, C] form of ABI 3 included): each rank checks its own
+    block, and the layout is the same on every rank.  A wrong `recv` or `frame` exists on dst alone, where the peers
+    may already be inside the collective: dst then still joins it with a correctly sized buffer of its own and raises
+    once the collective has completed, so no peer is left blocked in dist.gather."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     block = block_rows(height, band_rows, world)
@@ -85,11 +88,19 @@ def gather_frame(send, height, band_rows, group=None, dst=0, recv=None, frame=No
         dist.gather(send, None, dst=dst, group=group)
         return None
     width, chans = send.shape[1], send.shape[2]
+    bad = None
+    if recv is not None and (tuple(recv.shape) != (world * block, width, chans) or recv.dtype != send.dtype or recv.device != send.device
+                             or not recv.is_contiguous()):
+        bad = ValueError(f"recv must be one contiguous {send.dtype} buffer of {world} blocks of {block} rows on {send.device}, "
+                         f"got shape {tuple(recv.shape)} {recv.dtype} on {recv.device}")
+        recv = None
+    if frame is not None and (tuple(frame.shape) != (int(height), width, chans) or frame.dtype != send.dtype):
+        bad = bad or ValueError(f"frame must have shape {(int(height), width, chans)} and dtype {send.dtype}, got {tuple(frame.shape)} {frame.dtype}")
     if recv is None:
         recv = torch.empty((world * block, width, chans), dtype=send.dtype, device=send.device)
-    if tuple(recv.shape) != (world * block, width, chans):
-        raise ValueError(f"recv must hold {world} blocks of {block} rows, got shape {tuple(recv.shape)}")
     dist.gather(send, list(recv.chunk(world)), dst=dst, group=group)  # views of one contiguous buffer
+    if bad is not None:  # raised only now: every peer's gather has completed
+        raise bad
     if frame is None:
         frame = torch.empty((height, width, chans), dtype=send.dtype, device=send.device)
     return unpack_bands(recv, frame, height, band_rows, world)
@@ -120,7 +131,8 @@ class frame_renderer:
             stats = dict(self.eng.stats)
         else:
             stats = {"segments": 0, "primary": 0, "ms": 0.0, "extend_ms": 0.0, "shade_ms": 0.0, "extend_launches": 0,
-                     "shade_launches": 0, "passes": 0, "samples_per_pass": 0, "local_rows": 0, "extend_variant": -1}
+                     "shade_launches": 0, "passes": 0, "samples_per_pass": 0, "local_rows": 0, "extend_variant": -1,
+                     "kernel_features": 0, "kernel_textures": 0, "kernel_lds_mode": -1}
         if self.world == 1:
             return self.send, stats
         return gather_frame(self.send, self.eng.height, self.band_rows, self.group, self.dst, self.recv, self.frame), stats
@@ -182,7 +194,7 @@ class multi_engine:
         return st.ms
 
     def scene_info(self):
-        """rt_multi_scene_info: the scene_manager view and sizes (device_bytes_f64 per device, once rendered)."""
+        """rt_multi_scene_info: the scene_manager view and sizes (device_bytes_f64: uploaded on each device at creation)."""
         from ._lib import rt_scene_info
         info = rt_scene_info()
         check(lib.rt_multi_scene_info(self._m, ctypes.byref(info)), "rt_multi_scene_info")

@@ -37,6 +37,13 @@ def _worker(rank, world, port, q):
     # the collective, so no rank waits in a gather the others never join
     with pytest.raises(ValueError, match="padded gather block"):
         gather_frame(send[:-1], H, BAND)
+    # a wrong recv buffer exists on rank 0 alone: rank 0 still joins the collective (the peers are not left blocked in
+    # it) and raises afterwards; the next gather then works on every rank
+    if rank == 0:
+        with pytest.raises(ValueError, match="recv must be"):
+            gather_frame(send, H, BAND, recv=torch.empty((1, W, 3), dtype=torch.uint8))
+    else:
+        assert gather_frame(send, H, BAND) is None
     frame = gather_frame(send, H, BAND)
     if rank == 0:
         q.put(frame.numpy())

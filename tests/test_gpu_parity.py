@@ -63,6 +63,19 @@ def test_f64_matches_oracle_pcg(gpu, scene):
 F_CODE16 = 1 << 7  # layout.h feature bit of the 16-bit-child-code instantiations
 
 
+def test_scene_kernel_map(gpu):
+    # the persistent kernel every builtin scene runs (rt_stats.kernel_*) is the one tests/test_kernel_resources.py
+    # checks for spills
+    from tests.test_kernel_resources import SCENE_KERNELS
+    for scene, key in SCENE_KERNELS.items():
+        st = gpu_render(scene, 32, 18, 1)["stats"]
+        got = (st["kernel_features"], st["kernel_textures"], st["kernel_lds_mode"])
+        if key is None:
+            assert st["extend_variant"] == 1 and got == (0, 0, -1), (scene, st)
+        else:
+            assert got == key, (scene, got, key)
+
+
 @pytest.mark.parametrize("scene", ["cow", "dino", "8", "5"])
 def test_32bit_code_kernels_match_oracle_pcg(gpu, options, scene):
     # a scene whose BVH codes do not fit 16 bits (> 32768 nodes or > 8192 primitive references) takes the k_paths_g

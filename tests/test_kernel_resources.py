@@ -6,7 +6,10 @@ analysis assumes them, so a source change that breaks one shows up here, on the 
   * the mesh kernels with solid/checker textures (cow, dino: F_CODE16 | kFeatMesh, kTexBasic) spill nothing in
     LM 1 (dino) and at most a few registers elsewhere;
   * every LM 1 kernel with 16-bit codes spills nothing -- the Next-Week final's <189, 15, 1> among them (54 spilled
-    VGPRs before csrc/sphere_uv.h replaced the device library's acos / atan2, whose hoisted constants were the spills)."""
+    VGPRs before csrc/sphere_uv.h replaced the device library's acos / atan2, whose hoisted constants were the spills);
+  * SCENE_KERNELS: the persistent kernel each builtin scene runs (rt_stats.kernel_*; tests/test_gpu_parity.py checks the
+    map on the GPU, tools/kernel_map.py prints it) spills no VGPR, except the capsule's textured LM 2 mesh kernel:
+    20 VGPRs the allocator parks around the whole path loop, all used at path start only (profiles/r5b_ab_instantiations.txt)."""
 import os
 import re
 import sys
@@ -34,6 +37,26 @@ def _paths_g(ks):
         if m:
             out[tuple(int(x) for x in m.groups())] = k
     return out
+
+
+# scene -> (features, textures, LDS mode) of the persistent kernel it runs: k_paths_g<F, TF, LM>, k_paths = (1, 0, 3),
+# None = the per-depth LDS wavefront variant (scene 3: a noise texture the LDS shading table cannot hold)
+SCENE_KERNELS = {
+    "c1": (1, 0, 3), "1": (1, 0, 3), "2": (1, 0, 3), "3": None, "4": (129, 15, 1), "5": (165, 15, 1), "6": (189, 15, 1),
+    "7": (125, 3, 1), "8": (189, 15, 1), "cow": (167, 3, 2), "dino": (167, 3, 1), "9": (39, 15, 2),
+}
+SPILL_ALLOWED = {(39, 15, 2): 20}  # the capsule (scene 9, the reference's default): path-start values only
+
+
+def test_every_kernel_a_builtin_scene_runs_is_spill_free(ks):
+    pg = _paths_g(ks)
+    for scene, key in SCENE_KERNELS.items():
+        if key is None or key[2] == 3:
+            continue
+        assert key in pg, (scene, key)
+        spilled = pg[key].get(".vgpr_spill_count", 0)
+        assert spilled <= SPILL_ALLOWED.get(key, 0), (scene, key, spilled)
+        assert pg[key][".vgpr_count"] + pg[key].get(".agpr_count", 0) <= 168, (scene, key)
 
 
 def test_every_code_object_is_gfx950_and_has_the_path_kernels(ks):
