@@ -149,38 +149,26 @@ template <> struct HitRecD<double> {
 
 template <class R> struct ResRec;  // final per-slot radiance
 template <> struct ResRec<float> { float4 v; };
-#ifndef ART_RES_PITCH
-#define ART_RES_PITCH 24
-#endif
-#ifndef ART_RES_NT
-#define ART_RES_NT 1
-#endif
-#if ART_RES_PITCH == 32
-template <> struct alignas(32) ResRec<double> { double x, y, z, pad; };  // one 32-B sector per record
-#else
 template <> struct ResRec<double> { double x, y, z; };  // 24 B, unpadded: k_accum streams these at HBM rate
-#endif
 __device__ __forceinline__ void store_res(ResRec<float>* res, uint32_t q, V3<float> L) { res[q].v = make_float4(L.x, L.y, L.z, 0.0f); }
-// The radiance records stream out with non-temporal stores (read once, by k_accum after the pass), so they
-// do not evict the L2-resident camera-ray rings of k_paths
+// NT: non-temporal stores (read once, by k_accum after the pass), so the records do not evict k_paths' L2-resident
+// camera-ray rings.  Measured (r5c, profiles/r5c_write_traffic.txt, HBM bytes per segment vs the 24-B records' own):
+// each 8-B non-temporal store reaches HBM as its own partial write, 2.0x the record bytes (Next-Week final: 12.6 B
+// against 6.3); temporal stores merge in L2 first, 1.18x (7.4 B), at equal speed -- so k_paths_g, which has no rings,
+// stores temporally.  k_paths keeps NT: its writes are ring lines evicted between laps (27.8 B per segment with NT
+// 24-B records, 27.2 with NT 32-B ones), and temporal records evict more of them (32.9 B written + 6.8 B re-read,
+// -0.25 %).  32-B records cost k_accum a third more reads and lose 0.8-1.2 %.
+template <bool NT = true>
 __device__ __forceinline__ void store_res(ResRec<double>* res, uint32_t q, V3<double> L) {
-#if ART_RES_PITCH == 32
-    typedef double d4v __attribute__((ext_vector_type(4)));
-    const d4v v = {L.x, L.y, L.z, 0.0};
-#if ART_RES_NT
-    __builtin_nontemporal_store(v, reinterpret_cast<d4v*>(&res[q]));
-#else
-    *reinterpret_cast<d4v*>(&res[q]) = v;
-#endif
-#elif ART_RES_NT
-    __builtin_nontemporal_store(L.x, &res[q].x);
-    __builtin_nontemporal_store(L.y, &res[q].y);
-    __builtin_nontemporal_store(L.z, &res[q].z);
-#else
-    res[q].x = L.x;
-    res[q].y = L.y;
-    res[q].z = L.z;
-#endif
+    if constexpr (NT) {
+        __builtin_nontemporal_store(L.x, &res[q].x);
+        __builtin_nontemporal_store(L.y, &res[q].y);
+        __builtin_nontemporal_store(L.z, &res[q].z);
+    } else {
+        res[q].x = L.x;
+        res[q].y = L.y;
+        res[q].z = L.z;
+    }
 }
 __device__ __forceinline__ void load_res(const ResRec<float>* res, uint32_t q, double& r, double& g, double& b) {
     const float4 v = res[q].v;
@@ -1200,7 +1188,7 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
             } else if (cont) {
                 ++depth;
             } else {
-                store_res(w.res, q, st.L);
+                store_res<false>(w.res, q, st.L);
                 busy = false;
             }
         }
@@ -2028,7 +2016,12 @@ template <class R>
 static int extend_variant(const DeviceScene<R>& ds, int flags) {
     if (!ds.lds_scene || (flags & RT_GLOBAL_SCENE) || (ds.features & ~kFeatSpheres) != 0)
         return (std::is_same<R, double>::value && !(flags & RT_WAVEFRONT)) ? EXT_MEGA_G : EXT_GLOBAL;
-    if (!ds.lds_shade || (flags & RT_SPLIT_SHADE)) return EXT_LDS;
+    // an LDS-image scene whose shading the LDS table cannot hold (noise / image textures: the two perlin spheres) runs
+    // the persistent HBM-scene kernel, not the per-depth LDS wavefront one: r5 A/B (profiles/r5c_ab_scene3.txt) scene 3
+    // 9 586 -> 23 864 Msamples/s; the wavefront variant stays reachable with RT_SPLIT_SHADE / RT_WAVEFRONT
+    if (!ds.lds_shade)
+        return (std::is_same<R, double>::value && !(flags & (RT_SPLIT_SHADE | RT_WAVEFRONT))) ? EXT_MEGA_G : EXT_LDS;
+    if (flags & RT_SPLIT_SHADE) return EXT_LDS;
     return (flags & RT_WAVEFRONT) ? EXT_FUSED : EXT_MEGA;
 }
 // The persistent kernels' waves index the camera-ray rings (kPoolWavesPerCu per CU allocated)

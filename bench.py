@@ -14,7 +14,9 @@ row-interleaved bands (8 rows; band b on GPU b mod N) and gathered as RGB8 on GP
 The total work per step is fixed as N grows ("scaling": "strong"); value = all segments traced on all GPUs / wall time
 of the K timed steps (max over ranks under torchrun), gather and unpack included.  A segment is one ray traced through
 the world (one world.hit call of engine.h:453), counted exactly on the device.
-C5 (BASELINE configs[4]): python bench.py --gpus 8 --scene dino --width 4096 --height 4096 --spp 8192 --steps 1 --warmup 0
+C5 (BASELINE configs[4]): python bench.py --gpus 8 --scene dino --width 4096 --height 4096 --spp 8192 --steps 1 --warmup 1
+(the scene is uploaded by rt_multi_create, before any step; the warm-up render allocates the pass workspace, so the one
+timed step is the render alone -- the reference times engine::run only, main.cpp:44-46)
 
 Extra fields:
   roofline      the dominant kernel (k_paths / k_paths_g) on the slowest GPU, each launch timed live with HIP events on

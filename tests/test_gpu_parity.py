@@ -70,10 +70,8 @@ def test_scene_kernel_map(gpu):
     for scene, key in SCENE_KERNELS.items():
         st = gpu_render(scene, 32, 18, 1)["stats"]
         got = (st["kernel_features"], st["kernel_textures"], st["kernel_lds_mode"])
-        if key is None:
-            assert st["extend_variant"] == 1 and got == (0, 0, -1), (scene, st)
-        else:
-            assert got == key, (scene, got, key)
+        assert got == key, (scene, got, key)
+        assert st["extend_variant"] == (3 if key[2] == 3 else 4), (scene, st)
 
 
 @pytest.mark.parametrize("scene", ["cow", "dino", "8", "5"])

@@ -39,10 +39,9 @@ def _paths_g(ks):
     return out
 
 
-# scene -> (features, textures, LDS mode) of the persistent kernel it runs: k_paths_g<F, TF, LM>, k_paths = (1, 0, 3),
-# None = the per-depth LDS wavefront variant (scene 3: a noise texture the LDS shading table cannot hold)
+# scene -> (features, textures, LDS mode) of the persistent kernel it runs: k_paths_g<F, TF, LM>, k_paths = (1, 0, 3)
 SCENE_KERNELS = {
-    "c1": (1, 0, 3), "1": (1, 0, 3), "2": (1, 0, 3), "3": None, "4": (129, 15, 1), "5": (165, 15, 1), "6": (189, 15, 1),
+    "c1": (1, 0, 3), "1": (1, 0, 3), "2": (1, 0, 3), "3": (129, 15, 1), "4": (129, 15, 1), "5": (165, 15, 1), "6": (189, 15, 1),
     "7": (125, 3, 1), "8": (189, 15, 1), "cow": (167, 3, 2), "dino": (167, 3, 1), "9": (39, 15, 2),
 }
 SPILL_ALLOWED = {(39, 15, 2): 20}  # the capsule (scene 9, the reference's default): path-start values only
@@ -51,7 +50,7 @@ SPILL_ALLOWED = {(39, 15, 2): 20}  # the capsule (scene 9, the reference's defau
 def test_every_kernel_a_builtin_scene_runs_is_spill_free(ks):
     pg = _paths_g(ks)
     for scene, key in SCENE_KERNELS.items():
-        if key is None or key[2] == 3:
+        if key[2] == 3:
             continue
         assert key in pg, (scene, key)
         spilled = pg[key].get(".vgpr_spill_count", 0)

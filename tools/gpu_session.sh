@@ -10,7 +10,8 @@
 #   pmc:TAG:SCENE[:SPP]         tools/pmc.sh counter passes + kernel trace of the current libart (ART_LIB honoured)
 #   bench:TAG[:ARGS]            bench.py line -> gpurun_out/bench_TAG.log
 #   prof:TAG[:ARGS]             rocprofv3 --kernel-trace --stats of a bench run -> gpurun_out/prof_TAG
-#   configs:TAG                 tools/configs.sh (one bench line per BASELINE GPU config)
+#   configs:TAG                 tools/configs.sh (one bench line per BASELINE GPU config, plus the capsule)
+#   c5full:TAG                  C5 as configured on one GPU: dino 4096^2 x 8192 spp, one timed step after a warm-up
 #   stats:TAG                   tools/stats_configs.sh over the four GPU configs (libart_stats.so: divergence counters
 #                               and the per-phase cycle split) -> gpurun_out/stats_TAG.txt
 # Usage (GPU box): bash tools/gpu_session.sh tests ab:libart_x.so,libart.so pmc:r2b:1
@@ -60,6 +61,9 @@ for step in "$@"; do
       tail -1 gpurun_out/rocprof_$a.log ;;
     configs)
       TAG=$a bash tools/configs.sh || exit 1 ;;
+    c5full)
+      run 300 python bench.py --scene dino --width 4096 --height 4096 --spp 8192 --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/c5full_$a.log 2>&1
+      tail -1 gpurun_out/c5full_$a.log > gpurun_out/c5full_$a.json; cut -c1-400 gpurun_out/c5full_$a.json ;;
     stats)
       CFGS="--scene 1 --spp 64|--scene cow --spp 64|--scene 8 --spp 64|--scene dino --width 4096 --height 4096 --spp 16" bash tools/stats_configs.sh \
         > gpurun_out/stats_$a.txt 2>&1 || exit 1
