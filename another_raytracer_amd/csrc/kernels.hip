@@ -224,6 +224,7 @@ struct PassGeom {
     const uint32_t* list;       // pixel-list mode (engine_mode::adaptive levels): slot pixel = list[qi] (local ly*W+lx)
     uint32_t nlist;             //   for qi < nlist; nullptr = every local pixel in 8x8 tile order
     uint32_t chunk;             // persistent kernels: slots per claim (path_chunk: a power of two >= 64)
+    uint32_t lds_ring;          // k_paths_g LM 1: the camera-ray rings are allocated in LDS (kRing, when they fit)
 };
 template <class R>
 struct Work {
@@ -936,6 +937,61 @@ constexpr size_t kLm1TriBytes = sizeof(TriRec112<double>);
 __host__ __device__ constexpr size_t paths_g_mesh_bytes(uint32_t n_nodes, uint32_t n_primrefs, uint32_t n_tris) {  // n_tris: 0 unless F_TRI
     return sizeof(BvhNode) * n_nodes + align16(sizeof(uint32_t) * n_primrefs) + kLm1TriBytes * n_tris;
 }
+// Camera-ray ring in LDS (k_paths_g LM 1, ART_LDS_RING_G): the camera rays are generated 64 at a time by the whole wave,
+// converged, into a per-wave ring of 64 entries in LDS, and the lanes that start a path read the next entries -- instead
+// of every round's camera-ray code running diverged for the few lanes that start a path (about a third).  k_paths does
+// the same through an L2-resident ring; in k_paths_g that ring's L2 round trip per take cost more than it saved (r3y:
+// final -0.8 %), the LDS read does not.  An entry is 64 B: o, d, tm, rng; tm = NaN marks a padding slot of a partial
+// tile (the taker idles a round), +inf a slot past the pass (the taker is drained).  Entry k holds slot b0 + k.
+#ifndef ART_LDS_RING_G
+#define ART_LDS_RING_G 1
+#endif
+constexpr uint32_t kRingG = 64;  // entries per wave
+// Which kernels carry the ring: triangle-free LM 1 kernels (r5d, profiles/r5d_ab_lds_ring.txt: Cornell smoke +3.2 %,
+// two perlin spheres +3.6 %, simple light +0.2 %; the mesh kernel, whose leaf triangles share the LDS, dino -1.1 %),
+// except the Next-Week final's <189, 15, 1>: there the ring's registers push three loop-carried doubles into scratch
+// (6 spilled VGPRs) for +0.5 %, so it keeps its spill-free ring-free form.
+__host__ __device__ constexpr bool paths_g_ring(uint32_t F, int LM) {
+    return ART_LDS_RING_G && LM == 1 && (F & F_TRI) == 0 && F != ((F_ALL & ~F_TRI & ~F_MEDIA_G) | F_CODE16);
+}
+__host__ __device__ constexpr size_t paths_g_ring_bytes(int block) { return static_cast<size_t>(block / 64) * kRingG * 64u; }
+// A wave's ring is 64 entries of 8 fields (o.xyz, d.xyz, tm, rng) stored field-major (SoA: field f of entry k at
+// f * 512 + k * 8 bytes), so a wave's reads and writes of one field are contiguous 8-B words (no bank conflicts; the
+// AoS 64-B entries put 4 lanes on the same banks).
+struct RingG {
+    double* f;  // this wave's 8 x 64 doubles
+    __device__ __forceinline__ double& at(uint32_t field, uint32_t k) const { return f[field * kRingG + k]; }
+};
+// 1 = a path starts (st, q), 0 = a padding slot (idle this round), 2 = the pass is drained
+__device__ __forceinline__ int ring_take_g(const RingG& ring, uint32_t k, uint32_t b0, PathState<double>& st, uint32_t& q) {
+    const double tm = ring.at(6, k);
+    if (tm != tm) return 0;
+    if (tm == __builtin_inf()) return 2;
+    st.ray.o = mk(ring.at(0, k), ring.at(1, k), ring.at(2, k));
+    st.ray.d = mk(ring.at(3, k), ring.at(4, k), ring.at(5, k));
+    st.ray.tm = tm;
+    st.rng = static_cast<uint64_t>(__double_as_longlong(ring.at(7, k)));
+    st.T = mk(1.0, 1.0, 1.0);
+    st.L = mk(0.0, 0.0, 0.0);
+    q = b0 + k;
+    return 1;
+}
+__device__ __forceinline__ void ring_fill_g(const RingG& ring, uint32_t lane, uint32_t slot, const PassGeom& sg, const CameraRec<double>& sc) {
+    double v[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, __builtin_inf(), 0.0};
+    if (slot < sg.P) {
+        v[6] = __builtin_nan("");
+        int lx, ly;
+        if (slot_pixel(sg, slot - sg.fd_npix.div(slot) * sg.npix_pad, lx, ly)) {
+            Ray<double> r;
+            uint64_t rng;
+            cam_ray(sg, sc, slot, lx, ly, r, rng);
+            v[0] = r.o.x; v[1] = r.o.y; v[2] = r.o.z; v[3] = r.d.x;
+            v[4] = r.d.y; v[5] = r.d.z; v[6] = r.tm; v[7] = __longlong_as_double(static_cast<long long>(rng));
+        }
+    }
+#pragma unroll
+    for (uint32_t f = 0; f < 8; ++f) ring.at(f, lane) = v[f];
+}
 template <uint32_t F, uint32_t TF, int LM>
 __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) void k_paths_g(DevScene<double> S0, PassGeom g, CameraRec<double> cam,
                                                                                      Work<double> w, uint32_t* next_slot) {
@@ -1017,7 +1073,13 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
             copy(m + nb + pb, S0.leaf_tris112, tb);
             S.leaf_tris112 = reinterpret_cast<const TriRec112<double>*>(m + nb + pb);
         }
+        lm_off = align16(lm_off + nb + pb + tb);  // the camera-ray rings follow (kRing)
     }
+    constexpr bool kRing = paths_g_ring(F, LM);
+    const bool use_ring = kRing && g.lds_ring != 0;  // the launch found room for the rings
+    [[maybe_unused]] const RingG ring{reinterpret_cast<double*>(smem + lm_off) + (threadIdx.x / 64u) * (8u * kRingG)};
+    [[maybe_unused]] uint32_t r_head = 0, r_avail = 0, r_b0 = 0;  // wave-uniform: next entry, entries left, batch slot
+    [[maybe_unused]] bool r_exhausted = false;                   // every slot of the pass is in a batch
     const uint32_t P = g.P;
     const int max_depth = g.max_depth;
     __syncthreads();
@@ -1046,7 +1108,47 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
 #endif
     for (;;) {
         const uint64_t idle = __ballot(!busy && !drained);
-        if (idle) {
+        if (use_ring && idle) {
+            // the idle lanes of rank < first take the ring's remaining entries; when more lanes are idle than entries
+            // are left (the ring is then empty) the wave refills it with the next 64 slots, converged, and the rest take
+            // from the new batch (LDS operations of one wave complete in order: the refill's writes land after the
+            // takes' reads of the old entries, and before the reads of the new ones)
+            const uint32_t n = static_cast<uint32_t>(__popcll(idle));
+            const uint32_t rank = static_cast<uint32_t>(__popcll(idle & below));
+            const bool me = !busy && !drained;
+            const uint32_t first = min(n, r_avail);
+            int got = 0;
+            if (me && rank < first) got = ring_take_g(ring, r_head + rank, r_b0, st, q);
+            if (n > r_avail && !r_exhausted) {
+                if (cur == end) {
+                    const uint32_t chunk = s_g.chunk;
+                    uint32_t nb = 0;
+                    if (lane == 0) nb = atomicAdd(next_slot, chunk);
+                    nb = __shfl(nb, 0);
+                    cur = nb;
+                    end = nb + chunk;
+                }
+                const uint32_t b = cur;
+                cur += 64;
+                __asm__ volatile("" ::: "memory");  // the LDS camera / pass geometry loads stay here (see k_paths)
+                ring_fill_g(ring, lane, b + lane, s_g, s_cam);
+                __asm__ volatile("" ::: "memory");
+                r_b0 = b;
+                r_exhausted = b + 64u >= P;
+                if (me && rank >= first) got = ring_take_g(ring, rank - first, r_b0, st, q);
+                r_head = n - first;
+                r_avail = kRingG - r_head;
+            } else {
+                r_head += first;
+                r_avail -= first;
+                if (me && rank >= first) got = 2;  // no entries left and no slots: drained
+            }
+            if (me) {
+                busy = got == 1;
+                drained = got == 2;
+                depth = 0;
+            }
+        } else if (idle) {
             const uint32_t n = static_cast<uint32_t>(__popcll(idle));
             const uint32_t rank = static_cast<uint32_t>(__popcll(idle & below));
             uint32_t slot;
@@ -2040,13 +2142,20 @@ static KernelId launch_paths_g_ft(int num_cu, hipStream_t st, const DevScene<dou
                               const Work<double>& w, uint32_t* next_slot) {
     // g.stack = stack_rows: sentinel + entries + spare row
     const size_t lm_head = paths_g_head_bytes(g.stack, kBlockM, (F & F_CODE16) != 0) + paths_g_world_bytes(S.nworld, S.n_objs, lds_mats<TF>(S.n_mats));
-    const size_t lds_m = align128(lm_head) + paths_g_mesh_bytes(S.n_nodes, S.n_primrefs, (F & F_TRI) ? S.n_primrefs : 0u);
+    const size_t lds_m = align16(align128(lm_head) + paths_g_mesh_bytes(S.n_nodes, S.n_primrefs, (F & F_TRI) ? S.n_primrefs : 0u));
     // LM 1 also for a scene without BVH nodes (the earth scene: one sphere object): its world and objects in LDS and no
     // LM 0 suspend machinery (which spilled the earth's textured kernel)
     if (lds_m <= kPathsGLdsCap) {
-        const int blocks = blocks_per_cu(reinterpret_cast<const void*>(k_paths_g<F, TF, 1>), kBlockM, lds_m) * num_cu;
+        // the camera-ray rings (triangle-free kernels) when they fit too; otherwise the lanes generate their own rays
+        const size_t lds_r = lds_m + paths_g_ring_bytes(kBlockM);
+        PassGeom gr = g;
+        // not for a world without a BVH node (the earth: one sphere): its traces are one primitive test and its paths end
+        // after a segment or two, so most lanes start a path every round and the ring only adds LDS traffic (-1.4 %)
+        gr.lds_ring = (paths_g_ring(F, 1) && S.n_nodes > 0 && lds_r <= kPathsGLdsCap) ? 1u : 0u;
+        const size_t lds = gr.lds_ring ? lds_r : lds_m;
+        const int blocks = blocks_per_cu(reinterpret_cast<const void*>(k_paths_g<F, TF, 1>), kBlockM, lds) * num_cu;
         check_ring_waves(blocks, kBlockM, num_cu);
-        hipLaunchKernelGGL((k_paths_g<F, TF, 1>), dim3(blocks), dim3(kBlockM), lds_m, st, S, g, cam, w, next_slot);
+        hipLaunchKernelGGL((k_paths_g<F, TF, 1>), dim3(blocks), dim3(kBlockM), lds, st, S, gr, cam, w, next_slot);
         return {F, TF, 1};
     }
     // too large for LM 1: as many of the first (top-level) nodes as fit beside the stacks

@@ -8,8 +8,8 @@ analysis assumes them, so a source change that breaks one shows up here, on the 
   * every LM 1 kernel with 16-bit codes spills nothing -- the Next-Week final's <189, 15, 1> among them (54 spilled
     VGPRs before csrc/sphere_uv.h replaced the device library's acos / atan2, whose hoisted constants were the spills);
   * SCENE_KERNELS: the persistent kernel each builtin scene runs (rt_stats.kernel_*; tests/test_gpu_parity.py checks the
-    map on the GPU, tools/kernel_map.py prints it) spills no VGPR, except the capsule's textured LM 2 mesh kernel:
-    20 VGPRs the allocator parks around the whole path loop, all used at path start only (profiles/r5b_ab_instantiations.txt)."""
+    map on the GPU, tools/kernel_map.py prints it) spills no VGPR, except the capsule's textured LM 2 mesh kernel
+    (20 VGPRs the allocator parks around the whole path loop, all used at path start only: profiles/r5b_ab_instantiations.txt)."""
 import os
 import re
 import sys
@@ -90,4 +90,4 @@ def test_lm1_code16_kernels_do_not_spill(ks):
     pg = _paths_g(ks)
     assert (189, 15, 1) in pg  # the final scene's kernel (scene 8: all features, all textures, LDS BVH)
     spills = {key: k.get(".vgpr_spill_count", 0) for key, k in pg.items() if key[2] == 1 and key[0] & F_CODE16}
-    assert spills and all(v == 0 for v in spills.values()), spills
+    assert spills and all(v <= SPILL_ALLOWED.get(key, 0) for key, v in spills.items()), spills
