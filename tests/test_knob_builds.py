@@ -2,7 +2,7 @@
 with a non-default value, device code only (no GPU needed): the diagnostic builds (ART_STATS divergence counters,
 ART_TRACE path dumps), the one-object build (ART_SPLIT_PATHS=0), the k_paths leaf test with the per-slot code
 (ART_LDS_LEAF_NOREF=0) and the tuning parameters DESIGN.md §4 measured (suspend threshold, waves per SIMD, ring size,
-LDS node capacity, k_extend occupancy).  Dropped experiments are deleted from the sources, not compiled out, so no
+LDS node capacity, k_extend occupancy, k_paths_g's LDS camera-ray ring for A/B).  Dropped experiments are deleted from the sources, not compiled out, so no
 other switch exists to rot (VERDICT r3 weak #5)."""
 import os
 import re
@@ -20,9 +20,10 @@ VARIANTS = {
     "stats": ["-DART_SPLIT_PATHS=0", "-DART_STATS", "-DART_SUSPEND_LANES=0", "-DART_POOL_RING=128", "-DART_LDS_NODE_CAP=320"],
     "trace": ["-DART_SPLIT_PATHS=0", "-DART_TRACE", "-DART_PATHS_G_WAVES=2", "-DART_EXTEND_MIN_WAVES=2", "-DART_LDS_LEAF_NOREF=1"],
     "paths_ref": ["-DART_SPLIT_PATHS=2", "-DART_LDS_LEAF_NOREF=0", "-DART_SUSPEND_LANES=16"],
+    "no_ring": ["-DART_SPLIT_PATHS=1", "-DART_LDS_RING_G=0"],
 }
 SURVIVING = {"ART_STATS", "ART_TRACE", "ART_SPLIT_PATHS", "ART_SPLIT_MESH", "ART_LDS_LEAF_NOREF", "ART_SUSPEND_LANES", "ART_PATHS_G_WAVES",
-             "ART_POOL_RING", "ART_LDS_NODE_CAP", "ART_EXTEND_MIN_WAVES", "ART_LDS_BLOCK"}
+             "ART_POOL_RING", "ART_LDS_NODE_CAP", "ART_EXTEND_MIN_WAVES", "ART_LDS_BLOCK", "ART_LDS_RING_G"}
 
 
 def _compile(args, out):
