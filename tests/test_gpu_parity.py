@@ -149,6 +149,33 @@ def test_persistent_paths_small_and_ragged_frames(gpu, W, H, spp):
     assert g["segments"] == o["segments"]
 
 
+@pytest.mark.parametrize("scene", ["7", "3"])
+def test_lds_ring_kernels_small_ragged_split_and_banded(gpu, scene):
+    # the triangle-free LM 1 kernels take their camera rays from a per-wave LDS ring filled 64 slots at a time
+    # (kernels.hip ring_fill_g / ring_take_g): passes shorter than one batch, batches of padding slots of partial 8x8
+    # tiles, passes that end inside a batch, several passes, and band partitions must all trace exactly the oracle's
+    # paths
+    from tests.test_kernel_resources import SCENE_KERNELS
+    for W, H, spp in ((2, 2, 1), (9, 3, 3), (13, 70, 2), (130, 2, 5)):
+        g = gpu_render(scene, W, H, spp)
+        o = oracle_render(scene, W, H, spp, mode="pcg")
+        st = g["stats"]
+        assert (st["kernel_features"], st["kernel_textures"], st["kernel_lds_mode"]) == SCENE_KERNELS[scene]
+        assert np.array_equal(g["rgb"], o["rgb"]) and np.array_equal(g["acc"], o["acc"]) and g["segments"] == o["segments"], (W, H, spp)
+    W, H, spp = 100, 52, 12
+    one = gpu_render(scene, W, H, spp)
+    many = gpu_render(scene, W, H, spp, samples_per_pass=5)
+    assert many["stats"]["passes"] == 3
+    assert np.array_equal(one["acc"], many["acc"]) and one["segments"] == many["segments"]
+    img = np.zeros_like(one["rgb"])
+    segs = 0
+    for b in range(3):
+        part = gpu_render(scene, W, H, spp, band=(8, 3, b))
+        img[part["engine"].local_rows(8, 3, b)] = part["rgb"]
+        segs += part["segments"]
+    assert np.array_equal(img, one["rgb"]) and segs == one["segments"]
+
+
 def test_general_scenes_use_the_hbm_kernels(gpu):
     # triangles/rects/media (or no BVH) never take the LDS variants: persistent paths over the HBM scene (4), or the
     # per-depth HBM kernels (0) with RT_WAVEFRONT
@@ -235,7 +262,7 @@ def gpu_render_adaptive(scene, W, H, spp, band=None, seed=0):
     return img, eng
 
 
-@pytest.mark.parametrize("scene", ["c1", "1", "8", "cow"])
+@pytest.mark.parametrize("scene", ["c1", "1", "8", "cow", "7", "3"])
 def test_adaptive_matches_oracle_pcg(gpu, scene):
     """engine_mode::adaptive (engine.h:96-333) on the GPU vs the oracle's restatement on the same streams: bit-exact
     frame and the exact segment count (every distinct pixel traced once)."""
