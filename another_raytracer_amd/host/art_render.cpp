@@ -2,12 +2,13 @@
 // scene_manager::build -> camera (aspect W/H, focus distance 10, shutter [0, 1]) -> engine::run -> imageio::save_image.
 //
 //   art_render SCENE W H SPP OUT.png [--mode single|stripes|images|adaptive] [--seed N] [--max-depth D] [--device I]
-//                                    [--assets DIR] [--gpus N] [--progressive K] [--save-scene FILE]
+//                                    [--assets DIR] [--gpus N] [--progressive K] [--save-scene FILE] [--option NAME=VALUE]
 //   art_render --info SCENE [--assets DIR]     scene_manager::build only (no GPU needed): prints the scene summary
 //
 // SCENE is a scene_manager alias, or file:PATH for a flat-scene file written by --save-scene.  --gpus N renders on
 // devices 0..N-1 through multi_engine (RCCL); --progressive K traces K samples per pass and prints one JSON line per
-// pass (the headless live preview).  Prints one JSON line: {"scene", "W", "H", "spp", "ms", "segments",
+// pass (the headless live preview); --option sets a library option (rt_option_set, include/art.h) before the scene is
+// built, e.g. --option bvh.sah_ci=1.0 (repeatable).  Prints one JSON line: {"scene", "W", "H", "spp", "ms", "segments",
 // "msamples_per_s", "extend_variant"}.
 #include <cstdlib>
 #include <cstring>
@@ -28,7 +29,7 @@ std::string default_assets(const char* argv0) {  // <repo>/assets next to <repo>
 
 int usage() {
     std::cerr << "usage: art_render SCENE W H SPP OUT.png [--mode single|stripes|images|adaptive] [--seed N] [--max-depth D]"
-                 " [--device I] [--assets DIR] [--gpus N] [--progressive K] [--save-scene FILE]\n"
+                 " [--device I] [--assets DIR] [--gpus N] [--progressive K] [--save-scene FILE] [--option NAME=VALUE]\n"
                  "       art_render --info SCENE [--assets DIR]\n";
     return 2;
 }
@@ -57,7 +58,12 @@ int main(int argc, char** argv) try {
         else if (a == "--gpus") gpus = std::atoi(next().c_str());
         else if (a == "--progressive") progressive = std::atoi(next().c_str());
         else if (a == "--save-scene") save_path = next();
-        else pos.push_back(a);
+        else if (a == "--option") {
+            const std::string kv = next();
+            const size_t eq = kv.find('=');
+            if (eq == std::string::npos) throw std::invalid_argument("--option wants NAME=VALUE, got " + kv);
+            art::set_option(kv.substr(0, eq), std::strtod(kv.c_str() + eq + 1, nullptr));
+        } else pos.push_back(a);
     }
     art::scene_manager sm(assets, device);  // main.cpp:29-30
     if (info) {

@@ -37,6 +37,15 @@ def test_unknown_scene_is_the_references_error():
     assert out.returncode == 1 and "unkwnown scene requested" in out.stderr
 
 
+def test_option_flag_reaches_the_library():
+    # --option NAME=VALUE is rt_option_set before the build: the final scene without world merging keeps its 11 world
+    # objects (6 merged); an unknown option is refused
+    assert json.loads(run("--info", "8").stdout)["objects"] == 6
+    assert json.loads(run("--info", "8", "--option", "compile.world_merge=0").stdout)["objects"] == 11
+    out = run("--info", "8", "--option", "no.such.option=1", check=False)
+    assert out.returncode == 1 and "unknown option" in out.stderr
+
+
 def test_reference_style_main_compiles(tmp_path):
     """main.cpp:25-60 written against the header with the compile-time engine<W,H,C>."""
     src = tmp_path / "main.cpp"
