@@ -1672,7 +1672,7 @@ static std::vector<uint8_t> lds_scene_image(const FlatScene& f, uint32_t& nmov, 
         f.spheres.size() > kLdsRefIndexMask || std::max(extend_lds_bytes(true, stack_rows(f.max_stack)), paths_lds_bytes(stack_rows(f.max_stack))) > kLdsPerCu)
         return img;
     // k_paths shades a hit by its LDS leaf slot: every world object must be a BVH over the image's slots (a loose
-    // OBJ_PRIM object, e.g. with ART_WORLD_MERGE=0 or from a flat-scene file, takes the HBM kernels)
+    // OBJ_PRIM object, e.g. with option compile.world_merge = 0 or from a flat-scene file, takes the HBM kernels)
     for (int32_t w : f.world)
         if (w < 0 || static_cast<size_t>(w) >= f.objs.size() || f.objs[w].kind != OBJ_BVH) return img;
     for (uint32_t ref : f.primrefs) {

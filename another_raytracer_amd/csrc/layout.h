@@ -112,7 +112,7 @@ constexpr int kMaxStackDepth = 64;   // per-lane LDS traversal stack entries (si
 // child plane.  The boxes are the union over the shutter (y motion planes, the lerp of a child's t = 0 and t = 1 boxes,
 // measured 7.6 % fewer node visits but -1.5 % overall: two more loads and FMAs per visit, 21 more VGPR spills).
 // LDS node capacity: the random scene's tree without the hoisted ground sphere has 259 nodes (greedy collapse, bvh.cpp;
-// 223 with ART_BVH_COLLAPSE=1).  Every plane stays a multiple of 256 B (bank 0); the 7.5 KiB saved against a 320 cap
+// 223 with option bvh.collapse = 1).  Every plane stays a multiple of 256 B (bank 0); the 7.5 KiB saved against a 320 cap
 // leave room for deeper traversal stacks (the optimal collapse's tree needs 18 entries instead of 15)
 #ifndef ART_LDS_NODE_CAP
 #define ART_LDS_NODE_CAP 272
