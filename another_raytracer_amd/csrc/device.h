@@ -759,6 +759,8 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
     // with the node's 16-bit child codes (BvhNode::pad, layout.h make_leaf16) in the low half of each key; codes,
     // stack entries (16-bit, the LDS variant's LaneStack) and leaves are then in the 16-bit form throughout the walk
     constexpr bool PK = !L && (F & F_CODE16) != 0;
+    // F_LEAF2: a 16-bit leaf code's first slot is in units of two (layout.h; every leaf on an even slot)
+    constexpr uint32_t kLeafShift = (PK && (F & F_LEAF2) != 0) ? 1u : 0u;
     static_assert(!PK || (F & F_MEDIA_G) == 0, "packed keys need tmin > 0: no medium boundary traversals");
     LaneStack<B, L || PK> st(stk);
     // kNfHoist: the near-plane offsets computed once per traversal in kernels with every node in LDS (PL 2), instead
@@ -796,7 +798,7 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
     // (popped before any other push: no extra stack depth).
     [[maybe_unused]] bool skip_nodes = false;
     if (hoisted != kNodeEmpty && (!RES || rs->fresh)) {
-        const int32_t h = L ? lds_leaf(leaf_first(hoisted), leaf_count(hoisted)) : PK ? make_leaf16(leaf_first(hoisted), leaf_count(hoisted)) : hoisted;
+        const int32_t h = L ? lds_leaf(leaf_first(hoisted), leaf_count(hoisted)) : PK ? make_leaf16(leaf_first(hoisted) >> kLeafShift, leaf_count(hoisted)) : hoisted;
         parked = h;
         skip_nodes = true;
     }
@@ -1008,10 +1010,10 @@ __device__ __forceinline__ bool traverse(const DevScene<R>& S, const uint8_t* ld
             first2 = (x2 & ((1u << kLdsLeafShift) - 1)) - cnt;  // slot of entry k >= cnt: first2 + k
             cnt12 = cnt + (x2 >> kLdsLeafShift);
         } else if constexpr (PK) {
-            first = leaf16_first(leaf);
+            first = leaf16_first(leaf) << kLeafShift;
             cnt = leaf16_count(leaf);
             // leaf2 == kNodeEmpty decodes as an empty range (count 0)
-            first2 = leaf16_first(leaf2) - cnt;
+            first2 = (leaf16_first(leaf2) << kLeafShift) - cnt;
             cnt12 = cnt + leaf16_count(leaf2);
         } else {
             first = leaf_first(leaf);
@@ -1371,7 +1373,8 @@ __device__ __forceinline__ void rect_surface(V3<R>& p, V3<R>& n, bool& ff, R& su
 // material -- without reloading the primitive record (its bounds only feed u, v).
 // uvc: glibc_trig.h's constants (uv_table(S) or k_paths_g's LDS copy of its head; read only when UV); the tables
 // behind them are read from uv_table(S)
-template <class R, uint32_t F, bool UV = true>
+// TUV: triangle u, v (barycentric image textures); UV: u, v of every primitive (TF_IMAGE kernels)
+template <class R, uint32_t F, bool UV = true, bool TUV = UV>
 __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref, uint32_t face, const Ray<R>& r, R t, Surf<R>& s,
                                              uint32_t mat_hint, const double* uvc) {
     const uint32_t idx = primref_index(ref);
@@ -1413,7 +1416,7 @@ __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref,
             const V3<R> p = r.o + t * r.d;
             sp_p = p;
             face_normal(r, N, ff, sp_n);
-            if (UV && (S.mats[tr.mat].flags & MATF_NEEDS_UV)) {  // barycentric u, v feed image textures only (texture.h:135-154)
+            if (TUV && (S.mats[tr.mat].flags & MATF_NEEDS_UV)) {  // barycentric u, v feed image textures only (texture.h:135-154)
                 const R u = dot(N, cross(p3 - p2, p - p2));
                 const R v = dot(N, cross(p1 - p3, p - p3));
                 su = u / len2(N);
@@ -1468,7 +1471,7 @@ __device__ __forceinline__ void prim_surface(const DevScene<R>& S, uint32_t ref,
 
 // Rebuilds the hit_record of the world object that won (transform chain unwound as translate::hit / rotate_y::hit
 // do it: hittable.cpp:7-11, :72-84, including set_face_normal against the transformed ray).
-template <class R, uint32_t F, bool UV = true>
+template <class R, uint32_t F, bool UV = true, bool TUV = UV>
 __device__ __forceinline__ void world_surface(const DevScene<R>& S, const HitOut& h, const Ray<R>& r, R t, Surf<R>& s, const double* uvc = nullptr) {
     const int32_t w = static_cast<int32_t>(h.obj & 0xFFFFu);
     int32_t oi = S.world[w];
@@ -1504,7 +1507,7 @@ __device__ __forceinline__ void world_surface(const DevScene<R>& S, const HitOut
             }
         }
     }
-    prim_surface<R, F, UV>(S, h.prim, h.obj >> 16, r2, t, s, (F & F_TRI) == 0 ? h.mt : kMatUnknown, uvc);
+    prim_surface<R, F, UV, TUV>(S, h.prim, h.obj >> 16, r2, t, s, (F & F_TRI) == 0 ? h.mt : kMatUnknown, uvc);
     if (!(F & F_XFORM)) return;
 #ifdef ART_STATS
     if (o0 >= 0) {
@@ -1618,7 +1621,7 @@ __device__ __forceinline__ V3<R> tex_value(const DevScene<R>& S, int32_t ti, R u
             ART_STAT_LANE(31);
             return image_value(S, t.image, u, v);
         }
-        if ((TF & TF_IMAGE) && t.type == TEX_BARY_IMAGE) {
+        if ((TF & (TF_IMAGE | TF_BARY)) && t.type == TEX_BARY_IMAGE) {
             const R w = R(1) - u - v;
             return image_value(S, t.image, u * t.uv[0] + v * t.uv[2] + w * t.uv[4], u * t.uv[1] + v * t.uv[3] + w * t.uv[5]);
         }

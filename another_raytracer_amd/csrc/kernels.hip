@@ -26,6 +26,7 @@
 #include <functional>
 #include <limits>
 #include <map>
+#include <unordered_map>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -1147,6 +1148,14 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
                 busy = got == 1;
                 drained = got == 2;
                 depth = 0;
+#ifdef ART_TRACE
+                if (busy) {  // as the ring-free path below: is this the traced (pixel, sample)?
+                    int lx = 0, ly = 0;
+                    slot_pixel(s_g, q - s_g.fd_npix.div(q) * s_g.npix_pad, lx, ly);
+                    tracing = static_cast<long long>(global_row(s_g, ly)) * s_g.W + lx == g_trace_pixel &&
+                              static_cast<long long>(s_g.sample_base + s_g.fd_npix.div(q)) == g_trace_sample;
+                }
+#endif
             }
         } else if (idle) {
             const uint32_t n = static_cast<uint32_t>(__popcll(idle));
@@ -1220,7 +1229,7 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
             susp = in_trace;  // suspended: nothing to shade this round
             ART_TICK(tm_trace);
             if (!susp && hitw) {
-                world_surface<R, F, (TF & TF_IMAGE) != 0>(S, h, st.ray, t, s, uvc);
+                world_surface<R, F, (TF & TF_IMAGE) != 0, (TF & (TF_IMAGE | TF_BARY)) != 0>(S, h, st.ray, t, s, uvc);
                 mtype = S.mats[s.mat].type;
             }
         }
@@ -1631,6 +1640,8 @@ struct DeviceScene {
     bool lds_scene = false;                          // view.lds_image holds the layout.h LDS scene image
     bool lds_shade = false;                          // ... including a complete shading table (fused variant)
     bool codes16 = false;                            // every node's child codes fit BvhNode::pad's 16-bit form
+    uint32_t leaf_shift = 0;                         // 1: 16-bit leaf codes count slot pairs (F_LEAF2; leaves on even slots)
+    bool tex_bary = false;                           // image textures are barycentric ones on triangles only (TF_BARY)
     size_t bytes = 0;
 
     template <class T>
@@ -1780,8 +1791,87 @@ static std::vector<uint8_t> lds_scene_image(const FlatScene& f, uint32_t& nmov, 
 }
 
 
+// The 16-bit child codes (layout.h make_leaf16) of a BVH whose leaves start past slot 8191 (more than 8192 primitive
+// references: the capsule's 10 200 triangles) do not fit; with every leaf moved to an even slot of a padded copy of
+// the primitive references they do, as first / 2 (F_LEAF2).  Rewrites the device copies of the leaf codes (nodes and
+// hoisted leaves) and returns the padded references (pad[i]: slot i belongs to no leaf, its records stay zero), or
+// an empty vector when the leaves overlap or the padded codes still do not fit.  A leaf tests the same primitives in
+// the same order, so every closest hit, and the image, is unchanged.
+static std::vector<uint32_t> pair_align_leaves(const std::vector<uint32_t>& primrefs, std::vector<BvhNode>& nodes,
+                                               std::vector<ObjRec<double>>& objs, std::vector<uint8_t>& pad) {
+    std::vector<std::pair<uint32_t, uint32_t>> leaves;  // (first, count)
+    for (const BvhNode& b : nodes)
+        for (int c = 0; c < 4; ++c)
+            if (b.child[c] < 0 && b.child[c] != kNodeEmpty) leaves.emplace_back(leaf_first(b.child[c]), leaf_count(b.child[c]));
+    for (const auto& o : objs)
+        if (o.kind == OBJ_BVH && o.b != kNodeEmpty) leaves.emplace_back(leaf_first(o.b), leaf_count(o.b));
+    std::sort(leaves.begin(), leaves.end());
+    leaves.erase(std::unique(leaves.begin(), leaves.end()), leaves.end());
+    std::unordered_map<uint32_t, uint32_t> moved;  // old first -> new first
+    std::vector<uint32_t> out;
+    pad.clear();
+    uint32_t next = 0;  // first old slot not yet copied
+    for (const auto& lf : leaves) {
+        if (lf.first < next || lf.second < 1 || lf.second > 4 || lf.first + lf.second > primrefs.size()) return {};
+        for (; next < lf.first; ++next) {  // slots outside every leaf keep their order
+            out.push_back(primrefs[next]);
+            pad.push_back(0);
+        }
+        if (out.size() & 1u) {
+            out.push_back(0u);
+            pad.push_back(1);
+        }
+        moved[lf.first] = static_cast<uint32_t>(out.size());
+        if (!leaf16_ok(static_cast<uint32_t>(out.size()) >> 1, lf.second)) return {};
+        for (uint32_t k = 0; k < lf.second; ++k) {
+            out.push_back(primrefs[lf.first + k]);
+            pad.push_back(0);
+        }
+        next = lf.first + lf.second;
+    }
+    for (; next < primrefs.size(); ++next) {
+        out.push_back(primrefs[next]);
+        pad.push_back(0);
+    }
+    auto remap = [&](int32_t c) { return make_leaf(moved.at(leaf_first(c)), leaf_count(c)); };
+    for (BvhNode& b : nodes)
+        for (int c = 0; c < 4; ++c)
+            if (b.child[c] < 0 && b.child[c] != kNodeEmpty) b.child[c] = remap(b.child[c]);
+    for (auto& o : objs)
+        if (o.kind == OBJ_BVH && o.b != kNodeEmpty) o.b = remap(o.b);
+    return out;
+}
+
 template <class R>
-static void build_device_scene(const FlatScene& f, DeviceScene<R>& ds) {
+static void build_device_scene(const FlatScene& f0, DeviceScene<R>& ds) {
+    // the device copy of the BVH arrays, with leaves pair-aligned where 16-bit codes need it (pair_align_leaves)
+    FlatScene f = f0;
+    std::vector<uint8_t> slot_pad(f.primrefs.size(), 0);
+    {
+        bool fit = f.nodes.size() <= 32768u;
+        for (const BvhNode& b : f.nodes)
+            for (int c = 0; c < 4; ++c)
+                if (b.child[c] < 0 && b.child[c] != kNodeEmpty) fit = fit && leaf16_ok(leaf_first(b.child[c]), leaf_count(b.child[c]));
+        for (const auto& o : f.objs)
+            if (o.kind == OBJ_BVH && o.b != kNodeEmpty) fit = fit && leaf16_ok(leaf_first(o.b), leaf_count(o.b));
+        ds.leaf_shift = 0;
+        // only where an F_LEAF2 kernel exists (mesh feature sets with triangles: launch_paths_g); other kernels decode
+        // 16-bit leaves unshifted
+        const bool mesh = (f.features & ~kFeatMesh) == 0 && (f.features & F_TRI) != 0;
+        if (!fit && mesh && f.nodes.size() <= 32768u && opt(Opt::Leaf2) != 0) {
+            std::vector<BvhNode> nodes = f.nodes;
+            std::vector<ObjRec<double>> objs = f.objs;
+            std::vector<uint8_t> pad;
+            std::vector<uint32_t> refs = pair_align_leaves(f.primrefs, nodes, objs, pad);
+            if (!refs.empty()) {
+                f.primrefs = std::move(refs);
+                f.nodes = std::move(nodes);
+                f.objs = std::move(objs);
+                slot_pad = std::move(pad);
+                ds.leaf_shift = 1;
+            }
+        }
+    }
     std::vector<SphereRec<R>> sph(f.spheres.size());
     for (size_t i = 0; i < sph.size(); ++i) cvt_sphere(f.spheres[i], sph[i]);
     std::vector<TriRec<R>> tri(f.tris.size());
@@ -1842,7 +1932,7 @@ static void build_device_scene(const FlatScene& f, DeviceScene<R>& ds) {
     {  // every scene with a BVH: any kernel instantiated with triangles reads it, whatever the scene holds
         std::vector<TriRec<R>> lt(f.primrefs.size());
         for (size_t i = 0; i < lt.size(); ++i)
-            if (primref_type(f.primrefs[i]) == PRIM_TRIANGLE) lt[i] = tri[primref_index(f.primrefs[i])];
+            if (!slot_pad[i] && primref_type(f.primrefs[i]) == PRIM_TRIANGLE) lt[i] = tri[primref_index(f.primrefs[i])];
         ds.view.leaf_tris = ds.upload(lt);
         if constexpr (std::is_same<R, double>::value) {
             // TriRec112: the plane of each leaf triangle by the device's operations in its order (device.h cross, dot;
@@ -1865,6 +1955,7 @@ static void build_device_scene(const FlatScene& f, DeviceScene<R>& ds) {
         }
         std::vector<PrimRec80> lp(f.primrefs.size());  // every primitive type in leaf order (triangle-free kernels)
         for (size_t i = 0; i < lp.size(); ++i) {
+            if (slot_pad[i]) continue;
             const uint32_t ref = f.primrefs[i], idx = primref_index(ref);
             switch (primref_type(ref)) {
                 case PRIM_SPHERE: std::memcpy(lp[i].b, &sph[idx], sizeof(sph[idx])); break;
@@ -1888,8 +1979,8 @@ static void build_device_scene(const FlatScene& f, DeviceScene<R>& ds) {
                 } else if (x == kNodeEmpty) {
                     c16[c] = kNodeEmpty;
                 } else {
-                    ok = ok && leaf16_ok(leaf_first(x), leaf_count(x));
-                    c16[c] = ok ? make_leaf16(leaf_first(x), leaf_count(x)) : kNodeEmpty;
+                    ok = ok && leaf16_ok(leaf_first(x) >> ds.leaf_shift, leaf_count(x));
+                    c16[c] = ok ? make_leaf16(leaf_first(x) >> ds.leaf_shift, leaf_count(x)) : kNodeEmpty;
                 }
             }
             b.pad[0] = static_cast<int32_t>((static_cast<uint32_t>(c16[1]) << 16) | (static_cast<uint32_t>(c16[0]) & 0xFFFFu));
@@ -1897,11 +1988,12 @@ static void build_device_scene(const FlatScene& f, DeviceScene<R>& ds) {
             b.pad[2] = b.pad[3] = 0;
         }
         for (const auto& o : f.objs)
-            if (o.kind == OBJ_BVH && o.b != kNodeEmpty) ok = ok && leaf16_ok(leaf_first(o.b), leaf_count(o.b));
+            if (o.kind == OBJ_BVH && o.b != kNodeEmpty) ok = ok && leaf16_ok(leaf_first(o.b) >> ds.leaf_shift, leaf_count(o.b));
         // option render.codes16 = 0 (read per upload; tests): take the 32-bit-code kernels as a scene whose codes do
         // not fit would (a parity probe of that path on scenes that fit)
         if (opt(Opt::Codes16) == 0) ok = false;
         ds.codes16 = ok;
+        if (!ok) ds.leaf_shift = 0;  // the 32-bit codes (child[]) address the padded slots directly
         ds.view.nodes = ds.upload(nodes);
     }
     ds.view.objs = ds.upload(objs);
@@ -1935,7 +2027,7 @@ static void build_device_scene(const FlatScene& f, DeviceScene<R>& ds) {
     if (std::is_same<R, double>::value) {
         uint32_t nmov = 0;
         bool shade_ok = false;
-        const std::vector<uint8_t> img = lds_scene_image(f, nmov, shade_ok);
+        const std::vector<uint8_t> img = ds.leaf_shift ? std::vector<uint8_t>() : lds_scene_image(f, nmov, shade_ok);
         if (!img.empty()) {
             ds.view.lds_image = ds.upload(img);
             ds.lds_scene = true;
@@ -1954,6 +2046,24 @@ static void build_device_scene(const FlatScene& f, DeviceScene<R>& ds) {
     ds.max_stack = f.max_stack;
     ds.tex_basic = true;
     for (const auto& t : f.texs) ds.tex_basic = ds.tex_basic && (t.type == TEX_SOLID || t.type == TEX_CHECKER);
+    {  // TF_BARY: the texture trees the materials reach hold only solid, checker and barycentric-image nodes (a
+       // mesh's bary_image refers to its image texture, which no material samples directly), and no primitive but a
+       // triangle samples u, v
+        bool bary = !ds.tex_basic;
+        std::function<bool(int32_t, int)> tree_ok = [&](int32_t t, int depth) -> bool {
+            if (t < 0 || static_cast<size_t>(t) >= f.texs.size()) return true;
+            const uint32_t ty = f.texs[t].type;
+            if (ty == TEX_SOLID || ty == TEX_BARY_IMAGE) return true;
+            return ty == TEX_CHECKER && depth < 4 && tree_ok(f.texs[t].even, depth + 1) && tree_ok(f.texs[t].odd, depth + 1);
+        };
+        for (const auto& m : f.mats)
+            if (m.type == MAT_LAMBERTIAN || m.type == MAT_LIGHT || m.type == MAT_ISOTROPIC) bary = bary && tree_ok(m.tex, 0);
+        auto needs_uv = [&](uint32_t m) { return m < f.mats.size() && (f.mats[m].flags & MATF_NEEDS_UV) != 0; };
+        for (const auto& p : f.spheres) bary = bary && !needs_uv(p.mat);
+        for (const auto& p : f.rects) bary = bary && !needs_uv(p.mat);
+        for (const auto& p : f.boxes) bary = bary && !needs_uv(p.mat);
+        ds.tex_bary = bary && opt(Opt::TexBary) != 0;
+    }
     ds.mat_types = 0;
     for (const auto& m : f.mats) ds.mat_types |= 1u << m.type;
 }
@@ -2179,9 +2289,17 @@ static KernelId launch_paths_g_ft(int num_cu, hipStream_t st, const DevScene<dou
     hipLaunchKernelGGL((k_paths_g<F, TF, 0>), dim3(blocks), dim3(kBlock), lds, st, S, g, cam, w, next_slot);
     return {F, TF, 0};
 }
-static KernelId launch_paths_g(uint32_t feat, bool tex_basic, bool codes16, int num_cu, hipStream_t st, const DevScene<double>& S, const PassGeom& g,
-                           const CameraRec<double>& cam, const Work<double>& w, uint32_t* next_slot) {
+static KernelId launch_paths_g(uint32_t feat, bool tex_basic, bool tex_bary, bool codes16, uint32_t leaf_shift, int num_cu, hipStream_t st,
+                               const DevScene<double>& S, const PassGeom& g, const CameraRec<double>& cam, const Work<double>& w,
+                               uint32_t* next_slot) {
     constexpr uint32_t C = F_CODE16;
+    if (leaf_shift) {
+        // pair-aligned leaves (build_device_scene: mesh feature sets with triangles only): the F_LEAF2 mesh kernels
+        if (!codes16 || (feat & ~kFeatMesh) != 0 || !(feat & F_TRI)) throw std::runtime_error("internal: pair-aligned leaves outside the F_LEAF2 kernels");
+        if (tex_basic) return launch_paths_g_ft<kMeshG | F_LEAF2, kTexBasic>(num_cu, st, S, g, cam, w, next_slot);
+        if (tex_bary) return launch_paths_g_ft<kMeshG | F_LEAF2, kTexBary>(num_cu, st, S, g, cam, w, next_slot);
+        return launch_paths_g_ft<kMeshG | F_LEAF2, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
+    }
     if (!codes16 && (feat & F_MEDIA_G) == 0) {
         // 32-bit child codes (more than 32768 nodes or 8192 primitive references): the instantiations without F_CODE16.
         // A mesh scene (the capsule: 10 200 triangles, the reference's default scene) gets the mesh feature set, not
@@ -2201,6 +2319,7 @@ static KernelId launch_paths_g(uint32_t feat, bool tex_basic, bool codes16, int 
         // the F_TRI bit of an instantiation <=> the scene has triangles (leaf_tris exists)
         if (feat & F_TRI) {
             if (tex_basic) return launch_paths_g_ft<kFeatMesh | C, kTexBasic>(num_cu, st, S, g, cam, w, next_slot);
+            if (tex_bary) return launch_paths_g_ft<kFeatMesh | C, kTexBary>(num_cu, st, S, g, cam, w, next_slot);
             else return launch_paths_g_ft<kFeatMesh | C, TF_ALL>(num_cu, st, S, g, cam, w, next_slot);
         } else {
             if (tex_basic) return launch_paths_g_ft<(kFeatMesh & ~F_TRI) | C, kTexBasic>(num_cu, st, S, g, cam, w, next_slot);
@@ -2415,7 +2534,8 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
                             launch_paths(I.num_cu, stream, ds.view, g, cam, w, counter(w, 0, 0, 0));
                             kid = KernelId{kFeatSpheres, 0, 3};
                         } else {
-                            kid = launch_paths_g(ds.features, ds.tex_basic, ds.codes16, I.num_cu, stream, ds.view, g, cam, w, counter(w, 0, 0, 0));
+                            kid = launch_paths_g(ds.features, ds.tex_basic, ds.tex_bary, ds.codes16, ds.leaf_shift, I.num_cu, stream, ds.view, g, cam, w,
+                                                 counter(w, 0, 0, 0));
                         }
                         if (prof) { mark(); mark(); }
                         ++ext_launches;

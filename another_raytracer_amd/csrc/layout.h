@@ -177,6 +177,11 @@ enum Feature : uint32_t { F_SPHERE = 1u, F_TRI = 2u, F_RECT = 4u, F_BOX = 8u, F_
 // keys (device.h traverse); the scene's codes must all fit (DeviceScene::codes16) and it has no F_MEDIA_G boundary
 // traversals (those start at t = -inf, which packed keys cannot order).
 constexpr uint32_t F_CODE16 = 128u;
+// Not a scene feature either: with F_CODE16, a 16-bit leaf code's `first` counts pairs of primitive references (the
+// device copy of the primitive references puts every leaf on an even slot, DeviceScene::leaf_shift 1), so a mesh of up
+// to 16384 references -- the capsule, the reference's default scene: 10 200 triangles -- keeps the packed-key
+// traversal and the 16-bit stacks instead of the 32-bit-code kernels
+constexpr uint32_t F_LEAF2 = 256u;
 ART_HD constexpr uint32_t fbase(uint32_t f) { return f & F_ALL; }
 constexpr uint32_t kFeatSpheres = F_SPHERE;
 constexpr uint32_t kFeatMesh = F_SPHERE | F_TRI | F_RECT | F_MEDIA;
@@ -202,6 +207,11 @@ enum TexType : uint32_t { TEX_SOLID = 0, TEX_CHECKER = 1, TEX_NOISE = 2, TEX_IMA
 // Texture kinds present (shade kernels are instantiated for "solid + checker" and "all").
 enum TexFeature : uint32_t { TF_SOLID = 1u, TF_CHECKER = 2u, TF_NOISE = 4u, TF_IMAGE = 8u, TF_ALL = 15u };
 constexpr uint32_t kTexBasic = TF_SOLID | TF_CHECKER;
+// TF_BARY (not in TF_ALL): barycentric image textures on triangles only -- a mesh's map_Kd (mesh.h:9-27,
+// texture.h:135-154) -- and no image on any other primitive, so the kernel carries triangle u, v and the texel fetch
+// but not get_sphere_uv's acos / atan2 (the capsule's kernel: 20 spilled VGPRs with TF_ALL)
+constexpr uint32_t TF_BARY = 16u;
+constexpr uint32_t kTexBary = kTexBasic | TF_BARY;
 template <class R>
 struct TexRec {
     uint32_t type;

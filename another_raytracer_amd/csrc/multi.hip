@@ -113,7 +113,12 @@ static bool rccl_ok(ncclResult_t r) { return r == ncclSuccess || r == ncclInProg
 using Clock = std::chrono::steady_clock;
 static Clock::time_point deadline_from_now() {  // option multi.timeout_ms (default: ART_MULTI_TIMEOUT_MS, else 120 s)
     const double ms = opt(Opt::MultiTimeoutMs);
-    return Clock::now() + std::chrono::duration_cast<Clock::duration>(std::chrono::duration<double, std::milli>(ms));
+    // inf (or NaN, or any value whose nanoseconds overflow the clock's int64 ticks: > ~292 years) is "no deadline";
+    // the duration_cast of such a value would be undefined behaviour (INT64_MIN on x86: a deadline in the past)
+    const Clock::time_point now = Clock::now();
+    const double max_ms = std::chrono::duration<double, std::milli>(Clock::time_point::max() - now).count() * 0.5;
+    if (!(ms < max_ms)) return Clock::time_point::max();
+    return now + std::chrono::duration_cast<Clock::duration>(std::chrono::duration<double, std::milli>(ms));
 }
 
 // One ncclGroupStart / ncclGroupEnd bracket that is closed on every exit path.  RCCL's group depth is per thread: a
@@ -198,7 +203,7 @@ struct MultiRenderer::Impl {
                 else if (st != ncclSuccess) abort_all(std::string(what) + " on device " + std::to_string(devices[k]) + ": " + ncclGetErrorString(st));
             }
             if (!pending) return;
-            if (std::chrono::steady_clock::now() >= deadline) abort_all(std::string(what) + ": timed out (ART_MULTI_TIMEOUT_MS)");
+            if (std::chrono::steady_clock::now() >= deadline) abort_all(std::string(what) + ": timed out (option multi.timeout_ms)");
             std::this_thread::sleep_for(std::chrono::microseconds(50));
         }
     }
@@ -223,7 +228,7 @@ struct MultiRenderer::Impl {
                     abort_all(std::string(what) + " on device " + std::to_string(devices[k]) + ": " + ncclGetErrorString(st));
             }
             if (all) return;
-            if (std::chrono::steady_clock::now() >= deadline) abort_all(std::string(what) + ": timed out (ART_MULTI_TIMEOUT_MS)");
+            if (std::chrono::steady_clock::now() >= deadline) abort_all(std::string(what) + ": timed out (option multi.timeout_ms)");
             std::this_thread::sleep_for(std::chrono::microseconds(20));
         }
     }

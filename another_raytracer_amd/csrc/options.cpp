@@ -31,6 +31,8 @@ const OptDef kDefs[static_cast<int>(Opt::kCount)] = {
     {"bvh.sbvh_alpha", 1e-5, 0, 1e6, false},
     {"render.codes16", 1, 0, 1, true},
     {"render.lds_nodes_max", 4294967295.0, 0, 4294967295.0, true},
+    {"render.leaf2", 1, 0, 1, true},
+    {"render.tex_bary", 1, 0, 1, true},
     {"multi.timeout_ms", std::numeric_limits<double>::quiet_NaN(), 0, kInf, false},
     {"multi.rccl_blocking", 0, 0, 1, true},
     {"test.fault_workspace_bytes", 0, 0, 1.8e19, true},

@@ -24,9 +24,14 @@ enum class Opt : int {
     // device upload and launch (applies to uploads / renders after the call)
     Codes16,       // render.codes16: 1 (default) 16-bit child codes where they fit, 0 always the 32-bit-code kernels
     LdsNodesMax,   // render.lds_nodes_max: cap on the LDS-resident nodes of a partial-LDS (LM 2) kernel (diagnostic)
+    Leaf2,         // render.leaf2: 1 (default) pair-aligned leaves where 16-bit codes need them (F_LEAF2), 0 off
+    TexBary,       // render.tex_bary: 1 (default) the TF_BARY kernels for meshes whose only images are barycentric, 0 off
     // multi-GPU
-    MultiTimeoutMs,  // multi.timeout_ms: deadline of RCCL init / gather waits (unset: ART_MULTI_TIMEOUT_MS, else 120000)
-    RcclBlocking,    // multi.rccl_blocking: 1 = blocking communicators (diagnosis), 0 (default) non-blocking
+    MultiTimeoutMs,  // multi.timeout_ms: deadline of RCCL init / gather waits (unset: ART_MULTI_TIMEOUT_MS, else 120000;
+                     // inf, or anything beyond ~292 years, means no deadline)
+    RcclBlocking,    // multi.rccl_blocking: 1 = blocking communicators (diagnosis), 0 (default) non-blocking.  Blocking
+                     // gives up the deadline and the error-path protection: an error between the communicator inits
+                     // (before every rank is issued) leaves the group's ncclGroupEnd waiting for ranks never issued
     // test fault points (tests only: each makes a specific later call fail as the real fault would)
     FaultWorkspaceBytes,  // test.fault_workspace_bytes: refuse workspace growth beyond this many bytes (0 = off)
     FaultGatherAbort,     // test.fault_gather_abort: 1 = the next rt_render_multi's gather fails in flight

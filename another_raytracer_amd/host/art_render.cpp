@@ -62,7 +62,12 @@ int main(int argc, char** argv) try {
             const std::string kv = next();
             const size_t eq = kv.find('=');
             if (eq == std::string::npos) throw std::invalid_argument("--option wants NAME=VALUE, got " + kv);
-            art::set_option(kv.substr(0, eq), std::strtod(kv.c_str() + eq + 1, nullptr));
+            // the whole value must be a number: "" or "abc" would parse as 0, which is inside most ranges
+            const char* v = kv.c_str() + eq + 1;
+            char* stop = nullptr;
+            const double x = std::strtod(v, &stop);
+            if (stop == v || *stop != '\0') throw std::invalid_argument("--option " + kv.substr(0, eq) + ": not a number: '" + std::string(v) + "'");
+            art::set_option(kv.substr(0, eq), x);
         } else pos.push_back(a);
     }
     art::scene_manager sm(assets, device);  // main.cpp:29-30

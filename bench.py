@@ -111,7 +111,7 @@ def _median(xs):
     return xs[len(xs) // 2]
 
 
-def cpu_baseline(args, repeats=5):
+def cpu_baseline(args, repeats=9):
     """Two CPU figures on the box's host cores, each the median of `repeats` bounded samples of the same workload
     (same scene, full width and height, reduced spp: the per-segment cost does not depend on spp):
       * the reference itself (oracle/_ref/ref_harness = /root/reference/src compiled unmodified by oracle/Makefile) in
@@ -125,8 +125,10 @@ def cpu_baseline(args, repeats=5):
     threads = 4
     runs, last = [], None
     for _ in range(repeats):
+        # PIN 1: the harness pins its worker t to the t-th CPU of this job's affinity set (sched_setaffinity: no
+        # migrations between the host's shared cores, the run-to-run spread of r4/r5 was +-15 %)
         out = subprocess.run([harness, "render", args.scene, str(args.width), str(args.height), str(args.cpu_baseline_spp),
-                              "/tmp/bench_cpu_ref", "stripes", str(threads)], capture_output=True, text=True, timeout=900)
+                              "/tmp/bench_cpu_ref", "stripes", str(threads), "1"], capture_output=True, text=True, timeout=900)
         if out.returncode != 0:
             return {"error": out.stderr.strip()[-300:]}
         last = json.loads(out.stdout.strip().splitlines()[-1])
@@ -140,8 +142,10 @@ def cpu_baseline(args, repeats=5):
     res = {"value": round(_median(runs), 4), "unit": "Msamples/s", "cores": threads, "kind": "reference",
            "sample": f"scene {args.scene} {args.width}x{args.height}x{args.cpu_baseline_spp}spp "
                      f"({last['segments']} segments, {last['ms'] / 1e3:.1f} s per run), median of {repeats} runs, "
-                     f"engine_mode::parallel_stripes semantics (4 threads, shared global mt19937); per-segment cost is spp-independent",
+                     f"engine_mode::parallel_stripes semantics (4 threads pinned to 4 CPUs, shared global mt19937); "
+                     f"per-segment cost is spp-independent",
            "runs_Msamples_s": [round(x, 4) for x in runs], "spread_Msamples_s": [round(min(runs), 4), round(max(runs), 4)],
+           "max_Msamples_s": round(max(runs), 4), "spread_frac": round((max(runs) - min(runs)) / _median(runs), 4),
            "cpu_model": model, "host_cpus": os.cpu_count()}
     try:
         from tests.oracle_lib import oracle_render
@@ -372,6 +376,7 @@ def main():
         segs += st["segments"]
         primary_segs += st["primary"]
         variant = max(variant, st["extend_variant"])
+        kid = [st.get("kernel_features", 0), st.get("kernel_textures", 0), st.get("kernel_lds_mode", -1)]
         if acc is None:
             acc = [{"segments": 0, "primary": 0, "extend_ms": 0.0, "extend_launches": 0, "local_rows": d["local_rows"], "steps": 0}
                    for d in per_dev]
@@ -417,8 +422,11 @@ def main():
                        else f"scene {args.scene}", "width": args.width, "height": args.height, "spp": args.spp,
                        "max_depth": args.max_depth, "parallelism": parallelism, "driver": driver,
                        "segments_per_step": int(segs / args.steps), "primary_rays_per_step": primary // args.steps,
-                       "mprimary_per_s": round(primary / elapsed / 1e6, 3)},
+                       "mprimary_per_s": round(primary / elapsed / 1e6, 3),
+                       "kernel_f_tf_lm": kid},
         }
+        if args.option:  # the library options this line was measured under (A/B and sweep lines name their setting)
+            line["config"]["options"] = {o.partition("=")[0]: float(o.partition("=")[2]) for o in args.option}
         if n > 1:
             line["config"]["per_gpu_kernel_ms_per_step"] = [round(a["extend_ms"] / max(a["steps"], 1), 3) for a in acc]
         if driver == "multi" and times:

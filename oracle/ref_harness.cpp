@@ -15,13 +15,19 @@
 //
 // Commands:
 //   ref_harness kat N                               first N random_double() of a fresh generator
-//   ref_harness render SCENE W H SPP OUT [single|stripes T|adaptive|images]
+//   ref_harness render SCENE W H SPP OUT [single|stripes T|adaptive|adaptive4|images] [T] [PIN]
 //                                                   writes OUT.rgb (u8) and OUT.acc (f64 sums; zero in adaptive
 //                                                   mode), prints JSON.  "adaptive" = `_run_adaptive` (engine.h:96-333)
 //                                                   with its 4 stripes run one after another (deterministic);
 //                                                   "images" = `_run_parallel_images` (engine.h:378-445) with its 4
 //                                                   partial images traced one after another (OUT.acc: the pixel_acc
-//                                                   sum of the four float images)
+//                                                   sum of the four float images); "adaptive4" = `_run_adaptive`
+//                                                   as the reference threads it (engine.h:298-313: four stripes of
+//                                                   12 * (H / 48) rows, the last one taking the rest, on 4 threads
+//                                                   sharing the global RNG: a timing mode, its image is racy as the
+//                                                   reference's).  PIN = 1: worker t (or the one render thread) is
+//                                                   pinned to the t-th CPU of the process's affinity set
+//                                                   (sched_setaffinity), so a timed baseline does not migrate
 //   ref_harness probe SCENE K                       next K random_double() after the scene build (RNG pin)
 //   ref_harness dump SCENE OUT.json                 canonical dump of the scene graph (scene pin)
 //   ref_harness mesh SCENE|PATH.obj OUT.bin                 post-triangulation triangle list: u32 n, f32 xyz*3*n, f64 rgb*n (solid albedo,
@@ -58,6 +64,7 @@
 #include <variant>
 #include <system_error>
 #include <string_view>
+#include <sched.h>
 #include <charconv>
 #include <unordered_map>
 #include <deque>
@@ -260,7 +267,26 @@ camera make_camera(const scene& w, int W, int H) {
     return camera(w.lookfrom, w.lookat, vup, w.vfov, static_cast<double>(W) / static_cast<double>(H), w.aperture, dist_to_focus, 0.0, 1.0);
 }
 
-int cmd_render(const std::string& name, int W, int H, int spp, const std::string& out, const std::string& mode, int threads) {
+// Pins the calling thread to the t-th CPU (modulo) of the affinity set the process started with.
+void pin_thread(int t) {
+    static const std::vector<int> cpus = [] {
+        std::vector<int> v;
+        cpu_set_t set;
+        CPU_ZERO(&set);
+        if (sched_getaffinity(0, sizeof set, &set) == 0)
+            for (int c = 0; c < CPU_SETSIZE; ++c)
+                if (CPU_ISSET(c, &set)) v.push_back(c);
+        return v;
+    }();
+    if (cpus.empty()) return;
+    cpu_set_t one;
+    CPU_ZERO(&one);
+    CPU_SET(cpus[static_cast<size_t>(t) % cpus.size()], &one);
+    (void)sched_setaffinity(0, sizeof one, &one);
+}
+
+int cmd_render(const std::string& name, int W, int H, int spp, const std::string& out, const std::string& mode, int threads, bool pin) {
+    if (pin) pin_thread(0);
     scene world = build_scene(name);
     camera cam = make_camera(world, W, H);
     std::vector<std::uint8_t> rgb(static_cast<size_t>(W) * H * 3);
@@ -330,8 +356,8 @@ int cmd_render(const std::string& name, int W, int H, int spp, const std::string
                 write_color_raw(p, (y2 - y) * R1 / ydiff + (y - y1) * R2 / ydiff);
             }
     };
-    auto run_adaptive = [&](long long& segs) {  // engine.h:236-292 process_square over every 12-px square, row-major
-        for (int j = 0; j < H; j += 12)
+    auto run_adaptive_rows = [&](int j0, int j1, long long& segs) {  // engine.h:236-292 process_square, row-major
+        for (int j = j0; j < j1; j += 12)
             for (int i = 0; i < W; i += 12) {
                 corners(i, j, 12, segs);
                 if (!subdivide(i, j, 12)) { interpolate(i, j, 12); continue; }
@@ -351,6 +377,23 @@ int cmd_render(const std::string& name, int W, int H, int spp, const std::string
                             }
                     }
             }
+    };
+    auto run_adaptive = [&](long long& segs) {
+        run_adaptive_rows(0, H, segs);
+        std::transform(work.begin(), work.end(), rgb.begin(), [](int v) { return static_cast<std::uint8_t>(v); });
+    };
+    auto run_adaptive4 = [&]() {  // engine.h:298-313: tp.add_job(run_stripe(...)) x 4 on thread_pool tp{4}
+        const int stripe = 12 * (H / (4 * 12));
+        const int bounds[5] = {0, stripe, 2 * stripe, 3 * stripe, H};
+        std::vector<std::thread> pool;
+        for (int t = 0; t < 4; ++t)
+            pool.emplace_back([&, t]() {
+                if (pin) pin_thread(t);
+                long long segs = 0;
+                run_adaptive_rows(bounds[t], bounds[t + 1], segs);
+                g_segments += segs;
+            });
+        for (auto& th : pool) th.join();
         std::transform(work.begin(), work.end(), rgb.begin(), [](int v) { return static_cast<std::uint8_t>(v); });
     };
 
@@ -393,11 +436,15 @@ int cmd_render(const std::string& name, int W, int H, int spp, const std::string
         long long segs = 0;
         run_images(segs);
         g_segments += segs;
-    } else if (mode == "adaptive") {
+    } else if (mode == "adaptive" || mode == "adaptive4") {
         if (W % 12 != 0 || H % 12 != 0) throw std::logic_error("for adaptive strategy image size should perfectly fit big square size for now!!");
-        long long segs = 0;
-        run_adaptive(segs);
-        g_segments += segs;
+        if (mode == "adaptive4") {
+            run_adaptive4();
+        } else {
+            long long segs = 0;
+            run_adaptive(segs);
+            g_segments += segs;
+        }
     } else if (mode == "single") {
         long long segs = 0;
         for (int j = 0; j < H; ++j) run_row(j, segs);
@@ -408,7 +455,8 @@ int cmd_render(const std::string& name, int W, int H, int spp, const std::string
         for (int t = 0; t < threads; ++t) {
             int j0 = static_cast<int>(static_cast<long long>(H) * t / threads);
             int j1 = static_cast<int>(static_cast<long long>(H) * (t + 1) / threads);
-            pool.emplace_back([&, j0, j1]() {
+            pool.emplace_back([&, j0, j1, t]() {
+                if (pin) pin_thread(t);
                 long long segs = 0;
                 for (int j = j0; j < j1; ++j) run_row(j, segs);
                 g_segments += segs;
@@ -422,7 +470,7 @@ int cmd_render(const std::string& name, int W, int H, int spp, const std::string
     std::ofstream(out + ".rgb", std::ios::binary).write(reinterpret_cast<const char*>(rgb.data()), static_cast<std::streamsize>(rgb.size()));
     std::ofstream(out + ".acc", std::ios::binary).write(reinterpret_cast<const char*>(acc.data()), static_cast<std::streamsize>(acc.size() * sizeof(double)));
     std::printf("{\"scene\":\"%s\",\"W\":%d,\"H\":%d,\"spp\":%d,\"mode\":\"%s\",\"threads\":%d,\"segments\":%lld,\"ms\":%.3f,\"mseg_per_s\":%.6f}\n",
-                name.c_str(), W, H, spp, mode.c_str(), mode == "stripes" ? threads : 1, g_segments.load(), ms,
+                name.c_str(), W, H, spp, mode.c_str(), mode == "stripes" ? threads : mode == "adaptive4" ? 4 : 1, g_segments.load(), ms,
                 g_segments.load() / (ms * 1e3));
     return 0;
 }
@@ -441,7 +489,8 @@ int main(int argc, char** argv) try {
         if (argc < 7) return 2;
         std::string mode = argc > 7 ? argv[7] : "single";
         int threads = argc > 8 ? std::atoi(argv[8]) : 4;
-        return cmd_render(argv[2], std::atoi(argv[3]), std::atoi(argv[4]), std::atoi(argv[5]), argv[6], mode, threads);
+        const bool pin = argc > 9 && std::atoi(argv[9]) != 0;
+        return cmd_render(argv[2], std::atoi(argv[3]), std::atoi(argv[4]), std::atoi(argv[5]), argv[6], mode, threads, pin);
     }
     if (cmd == "probe") {
         scene w = build_scene(argv[2]);

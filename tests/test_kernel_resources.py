@@ -9,7 +9,7 @@ analysis assumes them, so a source change that breaks one shows up here, on the 
     VGPRs before csrc/sphere_uv.h replaced the device library's acos / atan2, whose hoisted constants were the spills);
   * SCENE_KERNELS: the persistent kernel each builtin scene runs (rt_stats.kernel_*; tests/test_gpu_parity.py checks the
     map on the GPU, tools/kernel_map.py prints it) spills no VGPR, except the capsule's textured LM 2 mesh kernel
-    (20 VGPRs the allocator parks around the whole path loop, all used at path start only: profiles/r5b_ab_instantiations.txt)."""
+    (10 VGPRs the allocator parks around the path start; 20 in r5's TF_ALL kernel: profiles/r5b_ab_instantiations.txt)."""
 import os
 import re
 import sys
@@ -42,9 +42,11 @@ def _paths_g(ks):
 # scene -> (features, textures, LDS mode) of the persistent kernel it runs: k_paths_g<F, TF, LM>, k_paths = (1, 0, 3)
 SCENE_KERNELS = {
     "c1": (1, 0, 3), "1": (1, 0, 3), "2": (1, 0, 3), "3": (129, 15, 1), "4": (129, 15, 1), "5": (165, 15, 1), "6": (189, 15, 1),
-    "7": (125, 3, 1), "8": (189, 15, 1), "cow": (167, 3, 2), "dino": (167, 3, 1), "9": (39, 15, 2),
+    "7": (125, 3, 1), "8": (189, 15, 1), "cow": (167, 3, 2), "dino": (167, 3, 1), "9": (423, 19, 2),
 }
-SPILL_ALLOWED = {(39, 15, 2): 20}  # the capsule (scene 9, the reference's default): path-start values only
+# the capsule (scene 9, the reference's default; F_LEAF2 | F_CODE16 mesh kernel, barycentric-image textures): 10 VGPRs,
+# path-start values only (r5's F_ALL-texture kernel spilled 20)
+SPILL_ALLOWED = {(423, 19, 2): 10}
 
 
 def test_every_kernel_a_builtin_scene_runs_is_spill_free(ks):

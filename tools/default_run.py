@@ -1,7 +1,13 @@
 """The reference's default run (main.cpp:20-50: the mesh (capsule) scene, engine_mode::adaptive, 720x540 at 100 spp,
-tracer_constants.h) timed on the GPU, next to the same frame in single mode (GPU box):
+tracer_constants.h) timed on the GPU, next to the same frame in single mode, and the reference itself on the same
+box's host CPU (GPU box):
 
-    python tools/default_run.py [--scene 9] [--reps 5] [--json OUT]
+    python tools/default_run.py [--scene 9] [--reps 5] [--cpu-runs 9] [--json OUT]
+
+The CPU line is oracle/_ref/ref_harness (the reference compiled unmodified, its ressources.h pointing at the repo's
+copy of the reference's assets, oracle/Makefile ASSET_ROOT) in mode "adaptive4": `_run_adaptive` threaded as the
+reference threads it (engine.h:298-313: four row stripes on a 4-thread pool sharing the global RNG), each worker pinned
+to one CPU of the job's affinity set; median and best of --cpu-runs runs.
 """
 import argparse
 import json
@@ -23,6 +29,7 @@ def main():
     ap.add_argument("--spp", type=int, default=100)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--cpu-runs", type=int, default=9, help="reference harness runs on the host CPU (0: none)")
     a = ap.parse_args()
     import another_raytracer_amd as art
     w = art.scene_manager().build(a.scene)
@@ -48,6 +55,35 @@ def main():
                "engine_ms": round(rep, 3), "segments": st["segments"], "primary": st["primary"],
                "msamples_s": round(st["segments"] / wall / 1e3, 1), "passes": st["passes"], "kernel_ms_profiled": round(prof["extend_ms"], 3), "launches_profiled": prof["extend_launches"],
                "kernel": [st["extend_variant"], st["kernel_features"], st["kernel_textures"], st["kernel_lds_mode"]]}
+        print(json.dumps(row), flush=True)
+        rows.append(row)
+    harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    if a.cpu_runs > 0 and os.path.exists(harness):
+        import subprocess
+        runs = []
+        for _ in range(a.cpu_runs):
+            out = subprocess.run([harness, "render", a.scene, str(a.width), str(a.height), str(a.spp), "/tmp/default_run_cpu",
+                                  "adaptive4", "4", "1"], capture_output=True, text=True, timeout=600)
+            if out.returncode != 0:
+                raise SystemExit("ref_harness failed: " + out.stderr.strip()[-400:])
+            runs.append(json.loads(out.stdout.strip().splitlines()[-1]))
+            print(json.dumps(runs[-1]), flush=True)
+        ms = sorted(r["ms"] for r in runs)
+        model = ""
+        try:
+            with open("/proc/cpuinfo") as f:
+                model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
+        except OSError:
+            pass
+        row = {"scene": a.scene, "mode": "adaptive", "device": "cpu", "kind": "reference", "threads": 4, "pinned": True,
+               "frame": [a.width, a.height, a.spp], "runs": len(ms), "ms_median": ms[len(ms) // 2], "ms_min": ms[0],
+               "ms_max": ms[-1], "spread_frac": round((ms[-1] - ms[0]) / ms[len(ms) // 2], 4),
+               "segments_last": runs[-1]["segments"], "cpu_model": model,
+               "note": "oracle/_ref/ref_harness render ... adaptive4 4 1: _run_adaptive's four stripes on four pinned threads "
+                       "(engine.h:298-313), the reference's own code compiled unmodified"}
+        gpu = next((r for r in rows if r["mode"] == "adaptive"), None)
+        if gpu:
+            row["gpu_speedup_vs_median"] = round(row["ms_median"] / gpu["wall_ms"], 1)
         print(json.dumps(row), flush=True)
         rows.append(row)
     if a.json:

@@ -7,10 +7,13 @@
 #   uvcheck                     tools/uv_check (device sphere_uv vs host bits and glibc texel choice) -> gpurun_out/uv_check.json
 #   ab:LIB1,LIB2[:ARGS]         tools/ab_quick.sh over in-tree libart builds (bench.py ARGS, default --spp 256)
 #   abenv:ARGS:V1+V2+...        tools/ab_env.sh over LIB[@VAR=VAL,...] variants (bench.py ARGS)
+#   abopt:ARGS:V1+V2+...        tools/ab_opts.sh over option variants of the current build ("base" or NAME=VALUE,...)
 #   pmc:TAG:SCENE[:SPP]         tools/pmc.sh counter passes + kernel trace of the current libart (ART_LIB honoured)
 #   bench:TAG[:ARGS]            bench.py line -> gpurun_out/bench_TAG.log
 #   prof:TAG[:ARGS]             rocprofv3 --kernel-trace --stats of a bench run -> gpurun_out/prof_TAG
 #   configs:TAG                 tools/configs.sh (one bench line per BASELINE GPU config, plus the capsule)
+#   defaultrun:TAG[:CPURUNS]    tools/default_run.py: the reference's default run (capsule, adaptive, 720x540x100) on the GPU and
+#                               the reference itself on the host CPU (CPURUNS pinned 4-thread runs, default 9)
 #   c5full:TAG                  C5 as configured on one GPU: dino 4096^2 x 8192 spp, one timed step after a warm-up
 #   stats:TAG                   tools/stats_configs.sh over the four GPU configs (libart_stats.so: divergence counters
 #                               and the per-phase cycle split) -> gpurun_out/stats_TAG.txt
@@ -46,6 +49,8 @@ for step in "$@"; do
       LIBS="${a//,/ }" ARGS="${b:---spp 256}" bash tools/ab_quick.sh || exit 1 ;;
     abenv)
       ARGS="$a" bash tools/ab_env.sh ${b//+/ } || exit 1 ;;
+    abopt)
+      ARGS="$a" bash tools/ab_opts.sh ${b//+/ } || exit 1 ;;
     pmc)
       spp=${c:-64}
       PMC_GROUPS="$PMC_ALL" TAG=$a SCENE=$b SPP=$spp bash tools/pmc.sh || exit 1
@@ -61,6 +66,9 @@ for step in "$@"; do
       tail -1 gpurun_out/rocprof_$a.log ;;
     configs)
       TAG=$a bash tools/configs.sh || exit 1 ;;
+    defaultrun)
+      run 900 python -u tools/default_run.py --cpu-runs ${b:-9} --json gpurun_out/default_run_$a.jsonl > gpurun_out/default_run_$a.log 2>&1
+      tail -3 gpurun_out/default_run_$a.log ;;
     c5full)
       run 300 python bench.py --scene dino --width 4096 --height 4096 --spp 8192 --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/c5full_$a.log 2>&1
       tail -1 gpurun_out/c5full_$a.log > gpurun_out/c5full_$a.json; cut -c1-400 gpurun_out/c5full_$a.json ;;
