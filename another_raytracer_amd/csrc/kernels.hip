@@ -226,6 +226,11 @@ struct PassGeom {
     uint32_t nlist;             //   for qi < nlist; nullptr = every local pixel in 8x8 tile order
     uint32_t chunk;             // persistent kernels: slots per claim (path_chunk: a power of two >= 64)
     uint32_t lds_ring;          // k_paths_g LM 1: the camera-ray rings are allocated in LDS (kRing, when they fit)
+    // 1: pixel-list mode with the samples of a list entry on consecutive slots (slot = entry * k + sample: a wave's 64
+    // lanes trace one pixel's samples, coherent rays, instead of 64 entries scattered over the image) and the entry
+    // count on the device at list[-1] (the adaptive levels' lists, appended by k_adapt_level: no host round trip);
+    // npix_pad = k then, and the persistent kernels take P = list[-1] * k and nlist = list[-1] at their start
+    uint32_t list_mode;
 };
 template <class R>
 struct Work {
@@ -247,6 +252,13 @@ __host__ __device__ __forceinline__ uint32_t* counter(const Work<R>& w, int d, i
 __device__ __forceinline__ int global_row(const PassGeom& g, int ly) {  // row-interleaved band partition
     const uint32_t b = g.fd_band_rows.div(static_cast<uint32_t>(ly));
     return static_cast<int>(b) * (g.band_rows * g.band_count) + g.band_index * g.band_rows + (ly - static_cast<int>(b) * g.band_rows);
+}
+// slot -> (qi: tile-order pixel or list entry, j: sample of the pass): sample-major slots (j * npix_pad + qi), or
+// entry-major ones in list_mode 1 (qi * k + j, npix_pad == k)
+__device__ __forceinline__ void slot_split(const PassGeom& g, uint32_t slot, uint32_t& qi, uint32_t& j) {
+    const uint32_t a = g.fd_npix.div(slot), b = slot - a * g.npix_pad;
+    qi = g.list_mode ? a : b;
+    j = g.list_mode ? b : a;
 }
 __device__ __forceinline__ bool slot_pixel(const PassGeom& g, uint32_t qi, int& lx, int& ly) {
     if (g.list) {
@@ -335,11 +347,10 @@ __device__ __forceinline__ int find_segment(const uint32_t* pre, int n, uint32_t
 }
 
 // ------------------------------------------------------------------------------------------------ kernels
-// engine.h:58-68 + camera.h:38-47 for slot q (sample j = q / npix_pad of the pass, pixel from the 8x8 tile order).
+// engine.h:58-68 + camera.h:38-47 for sample j of the pass at local pixel (lx, ly) (slot_split).
 // Runs inside the depth-0 extend: the camera ray never round-trips through HBM.
 template <class R>
-__device__ __forceinline__ void cam_ray(const PassGeom& g, const CameraRec<R>& cam, uint32_t q, int lx, int ly, Ray<R>& ray, uint64_t& rng_out) {
-    const uint32_t j = g.fd_npix.div(q);
+__device__ __forceinline__ void cam_ray(const PassGeom& g, const CameraRec<R>& cam, uint32_t j, int lx, int ly, Ray<R>& ray, uint64_t& rng_out) {
     const int gy = global_row(g, ly);
     const uint32_t pixel = static_cast<uint32_t>(gy) * static_cast<uint32_t>(g.W) + static_cast<uint32_t>(lx);
     uint64_t rng = splitmix64(((static_cast<uint64_t>(pixel) << 32) | (g.sample_base + j)) ^ g.seed_mix);  // == pcg_seed(g.seed, ...)
@@ -363,8 +374,8 @@ __device__ __forceinline__ void cam_ray(const PassGeom& g, const CameraRec<R>& c
     rng_out = rng;
 }
 template <class R>
-__device__ __forceinline__ void gen_ray(const PassGeom& g, const CameraRec<R>& cam, uint32_t q, int lx, int ly, PathState<R>& st) {
-    cam_ray(g, cam, q, lx, ly, st.ray, st.rng);
+__device__ __forceinline__ void gen_ray(const PassGeom& g, const CameraRec<R>& cam, uint32_t j, int lx, int ly, PathState<R>& st) {
+    cam_ray(g, cam, j, lx, ly, st.ray, st.rng);
     st.T = mk(R(1), R(1), R(1));
     st.L = mk(R(0), R(0), R(0));
 }
@@ -579,8 +590,10 @@ __global__ __launch_bounds__(L ? kBlockL : kBlock, L ? 1 : ART_EXTEND_MIN_WAVES)
             if (d == 0) {
                 q = i;
                 int lx, ly;
-                live = slot_pixel(g, i - g.fd_npix.div(i) * g.npix_pad, lx, ly);
-                if (live) gen_ray(g, cam, q, lx, ly, st);
+                uint32_t qi, j;
+                slot_split(g, i, qi, j);
+                live = slot_pixel(g, qi, lx, ly);
+                if (live) gen_ray(g, cam, j, lx, ly, st);
             } else {
                 const int s = find_segment(pre, kShards, i);
                 q = in[s * g.cap + (i - pre[s])];
@@ -719,10 +732,12 @@ struct RayRing {
         PoolRay e;
         e.tm = __builtin_nan("");
         int lx, ly;
-        if (slot < sg.P && slot_pixel(sg, slot - sg.fd_npix.div(slot) * sg.npix_pad, lx, ly)) {
+        uint32_t qi, j;
+        slot_split(sg, slot, qi, j);
+        if (slot < sg.P && slot_pixel(sg, qi, lx, ly)) {
             Ray<double> r;
             uint64_t rng;
-            cam_ray(sg, sc, slot, lx, ly, r, rng);
+            cam_ray(sg, sc, j, lx, ly, r, rng);
             e.ox = r.o.x; e.oy = r.o.y; e.oz = r.o.z; e.dx = r.d.x;
             e.dy = r.d.y; e.dz = r.d.z; e.tm = r.tm; e.rng = rng;
         }
@@ -796,6 +811,11 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S0, PassG
     if (threadIdx.x == 0) {
         s_cam = cam;
         s_g = g;
+        if (g.list_mode) {  // the list's entry count, on the device (PassGeom::list_mode)
+            const uint32_t n = g.list[-1];
+            s_g.nlist = n;
+            s_g.P = n * g.k;
+        }
     }
     DevScene<double> S = S0;
     {
@@ -829,7 +849,7 @@ __global__ __launch_bounds__(kBlockL, 1) void k_paths(DevScene<double> S0, PassG
             const uint32_t n = static_cast<uint32_t>(__popcll(idle));
             const uint32_t rank = static_cast<uint32_t>(__popcll(idle & below));
             if (!busy && !drained) {
-                const int got = rr.take(rank, g.P, st, q);
+                const int got = rr.take(rank, s_g.P, st, q);  // g.P, or the device count's (list_mode): read where used
                 drained = got == 2;
                 busy = got == 1;
                 depth = 0;
@@ -982,10 +1002,12 @@ __device__ __forceinline__ void ring_fill_g(const RingG& ring, uint32_t lane, ui
     if (slot < sg.P) {
         v[6] = __builtin_nan("");
         int lx, ly;
-        if (slot_pixel(sg, slot - sg.fd_npix.div(slot) * sg.npix_pad, lx, ly)) {
+        uint32_t qi, j;
+        slot_split(sg, slot, qi, j);
+        if (slot_pixel(sg, qi, lx, ly)) {
             Ray<double> r;
             uint64_t rng;
-            cam_ray(sg, sc, slot, lx, ly, r, rng);
+            cam_ray(sg, sc, j, lx, ly, r, rng);
             v[0] = r.o.x; v[1] = r.o.y; v[2] = r.o.z; v[3] = r.d.x;
             v[4] = r.d.y; v[5] = r.d.z; v[6] = r.tm; v[7] = __longlong_as_double(static_cast<long long>(rng));
         }
@@ -1014,6 +1036,11 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
     if (threadIdx.x == 0) {
         s_cam = cam;
         s_g = g;
+        if (g.list_mode) {  // the list's entry count, on the device (PassGeom::list_mode)
+            const uint32_t n = g.list[-1];
+            s_g.nlist = n;
+            s_g.P = n * g.k;
+        }
     }
     [[maybe_unused]] JumpEntry* jt = reinterpret_cast<JumpEntry*>(smem + align16(paths_g_stack_bytes(g.stack, B, S16) + sizeof(CameraRec<double>) + sizeof(PassGeom)));
     if (threadIdx.x < static_cast<uint32_t>(kJumpEntries)) jt[threadIdx.x] = pcg_jump(3u * threadIdx.x);
@@ -1081,7 +1108,6 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
     [[maybe_unused]] const RingG ring{reinterpret_cast<double*>(smem + lm_off) + (threadIdx.x / 64u) * (8u * kRingG)};
     [[maybe_unused]] uint32_t r_head = 0, r_avail = 0, r_b0 = 0;  // wave-uniform: next entry, entries left, batch slot
     [[maybe_unused]] bool r_exhausted = false;                   // every slot of the pass is in a batch
-    const uint32_t P = g.P;
     const int max_depth = g.max_depth;
     __syncthreads();
     const uint32_t lane = __lane_id();
@@ -1135,7 +1161,7 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
                 ring_fill_g(ring, lane, b + lane, s_g, s_cam);
                 __asm__ volatile("" ::: "memory");
                 r_b0 = b;
-                r_exhausted = b + 64u >= P;
+                r_exhausted = b + 64u >= s_g.P;  // g.P, or the device count's (list_mode): read where used
                 if (me && rank >= first) got = ring_take_g(ring, rank - first, r_b0, st, q);
                 r_head = n - first;
                 r_avail = kRingG - r_head;
@@ -1151,9 +1177,11 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
 #ifdef ART_TRACE
                 if (busy) {  // as the ring-free path below: is this the traced (pixel, sample)?
                     int lx = 0, ly = 0;
-                    slot_pixel(s_g, q - s_g.fd_npix.div(q) * s_g.npix_pad, lx, ly);
+                    uint32_t qi, j;
+                    slot_split(s_g, q, qi, j);
+                    slot_pixel(s_g, qi, lx, ly);
                     tracing = static_cast<long long>(global_row(s_g, ly)) * s_g.W + lx == g_trace_pixel &&
-                              static_cast<long long>(s_g.sample_base + s_g.fd_npix.div(q)) == g_trace_sample;
+                              static_cast<long long>(s_g.sample_base + j) == g_trace_sample;
                 }
 #endif
             }
@@ -1175,19 +1203,21 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
                 cur += n;
             }
             if (!busy && !drained) {
-                if (slot >= P) {
+                if (slot >= s_g.P) {
                     drained = true;
                 } else {
                     int lx, ly;
                     q = slot;
                     __asm__ volatile("" ::: "memory");  // keep the LDS camera/geometry loads here (see k_paths)
-                    if (slot_pixel(s_g, slot - s_g.fd_npix.div(slot) * s_g.npix_pad, lx, ly)) {
-                        gen_ray(s_g, s_cam, q, lx, ly, st);
+                    uint32_t qi, j;
+                    slot_split(s_g, slot, qi, j);
+                    if (slot_pixel(s_g, qi, lx, ly)) {
+                        gen_ray(s_g, s_cam, j, lx, ly, st);
                         busy = true;
                         depth = 0;
 #ifdef ART_TRACE
                         tracing = static_cast<long long>(global_row(s_g, ly)) * s_g.W + lx == g_trace_pixel &&
-                                  static_cast<long long>(s_g.sample_base + s_g.fd_npix.div(slot)) == g_trace_sample;
+                                  static_cast<long long>(s_g.sample_base + j) == g_trace_sample;
 #endif
                     }
                 }
@@ -1513,6 +1543,30 @@ __global__ void k_adapt_store(const uint32_t* list, uint32_t n, const double* ac
     }
 }
 
+// list_mode 1 (the device-counted levels): the pixel sums of every list entry -- its k samples on consecutive slots,
+// summed in sample order from +0.0 as k_accum sums them into the zeroed accumulator (engine.h:58-68) -- written into
+// the work image as k_adapt_store writes them.  The entry count is list[-1].
+__global__ void k_adapt_accum(const uint32_t* list, const ResRec<double>* res, uint32_t k, int spp, int32_t* work) {
+    const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= list[-1]) return;
+    double acc[3] = {0.0, 0.0, 0.0};
+    for (uint32_t j = 0; j < k; ++j) {
+        double x, y, z;
+        load_res(res, e * k + j, x, y, z);
+        acc[0] += x;
+        acc[1] += y;
+        acc[2] += z;
+    }
+    const double scale = 1.0 / spp;
+    int32_t* o = work + 3 * static_cast<size_t>(list[e]);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        double x = sqrt(scale * acc[c]);
+        x = x < 0.0 ? 0.0 : (x > 0.999 ? 0.999 : x);
+        o[c] = static_cast<int32_t>(256 * x);
+    }
+}
+
 // _compute_corners_heuristic (engine.h:96-136): any squared RGB distance between neighbouring corners > 100.
 __device__ __forceinline__ bool adapt_subdivide(const int32_t* work, int W, int x, int y, int L) {
     const int32_t* c1 = work + 3 * (static_cast<size_t>(y) * W + x);
@@ -1528,6 +1582,7 @@ __device__ __forceinline__ bool adapt_subdivide(const int32_t* work, int W, int 
 // Level-0 list: the four corners of every big square (ul, ur, bl, br: engine.h:223-233).
 __global__ void k_adapt_corners(uint32_t* list, int W, int sqx, uint32_t nsq) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s == 0) list[-1] = 4 * nsq;  // the entry count of a device-counted list (PassGeom::list_mode)
     if (s >= nsq) return;
     const uint32_t x = (s % sqx) * kBig, y = (s / sqx) * kBig;
     list[4 * s + 0] = y * W + x;
@@ -2453,12 +2508,13 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     const bool adapt_ws = (p.flags & RT_ADAPTIVE) != 0;
     const size_t nsq_ws = adapt_ws ? local_pix / (kBig * kBig) : 0;
     const size_t o_adw = off; off += adapt_ws ? al(sizeof(int32_t) * 3 * local_pix) : 0;
-    const size_t o_adl = off; off += adapt_ws ? al(4 * local_pix) : 0;
+    // four lists (one per level, at most 4 / 12 / 48 / 80 of every 144 pixels), each after its count word
+    const size_t o_adl = off; off += adapt_ws ? al(4 * local_pix + 4 * 4 * 64) : 0;
     const size_t o_adf = off; off += adapt_ws ? al(21 * nsq_ws) : 0;
     const size_t o_adc = off; off += adapt_ws ? al(4) : 0;
     char* base = static_cast<char*>(I.workspace(off));
     int32_t* ad_work = reinterpret_cast<int32_t*>(base + o_adw);
-    uint32_t* ad_list = reinterpret_cast<uint32_t*>(base + o_adl);
+    uint32_t* ad_list = reinterpret_cast<uint32_t*>(base + o_adl) + 64;  // host-counted levels: one list at a time
     uint8_t* ad_f0 = reinterpret_cast<uint8_t*>(base + o_adf);
     uint8_t* ad_f1 = ad_f0 + nsq_ws;
     uint8_t* ad_f2 = ad_f1 + 4 * nsq_ws;
@@ -2581,12 +2637,70 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     HIP_OK(hipMemsetAsync(w.segments, 0, sizeof(unsigned long long), stream));
     if (p.max_depth == 0) HIP_OK(hipMemsetAsync(w.res, 0, sizeof(ResRec<R>) * Pmax, stream));  // engine.h:451-452
     uint64_t traced = local_pix;
+    uint32_t ad_counts[4] = {0, 0, 0, 0};  // the device-counted levels' entry counts (read back with the frame)
+    bool dev_counted = false;
     if (!adaptive) {
         trace(nullptr, 0);
         const uint32_t npix = static_cast<uint32_t>(local_pix);
         hipLaunchKernelGGL(k_finalize, dim3((npix + 255) / 256), dim3(256), 0, stream, w.acc, drgb, npix, stopped ? spp_done : p.spp);
+    } else if (mega && k == static_cast<uint32_t>(spp_t) && !images && !p.on_pass) {
+        // engine.h:151-333: levels 0..3 (k_adapt_* above), one pass each, with no host round trip: each level's list
+        // count stays on the device (list[-1], PassGeom::list_mode 1), the persistent kernel reads it at its start and
+        // the level's samples are entry-major (a wave traces one pixel's samples: coherent rays)
+        const int sqx = p.width / kBig;
+        const uint32_t nsq = static_cast<uint32_t>(sqx) * static_cast<uint32_t>(nrows / kBig);
+        const uint32_t caps[4] = {4 * nsq, 12 * nsq, 48 * nsq, 80 * nsq};
+        uint32_t* lists[4];
+        {
+            uint32_t* at = reinterpret_cast<uint32_t*>(base + o_adl);
+            for (int L = 0; L < 4; ++L) {
+                lists[L] = at + 64;  // the count word at lists[L][-1]
+                at = lists[L] + ((caps[L] + 63u) & ~63u);
+            }
+        }
+        HIP_OK(hipMemsetAsync(base + o_adl, 0, 4 * local_pix + 4 * 4 * 64, stream));  // every count 0
+        HIP_OK(hipMemsetAsync(ad_work, 0xFF, sizeof(int32_t) * 3 * local_pix, stream));  // the reference's -1 frame
+        hipLaunchKernelGGL(k_adapt_corners, dim3((nsq + 255) / 256), dim3(256), 0, stream, lists[0], p.width, sqx, nsq);
+        g.list_mode = 1;
+        g.k = k;
+        g.npix_pad = k;
+        g.fd_npix = FastDiv::make(k);
+        g.sample_base = 0;
+        for (int level = 0; level < 4; ++level) {
+            g.list = lists[level];
+            g.nlist = caps[level];                      // upper bounds: the kernels read the count
+            g.P = static_cast<uint32_t>(std::min<uint64_t>(static_cast<uint64_t>(caps[level]) * k, kMaxPassSlots));
+            g.live = g.P;
+            if (static_cast<uint64_t>(caps[level]) * k > Pmax) throw std::runtime_error("internal: adaptive level larger than the pass workspace");
+            HIP_OK(hipMemsetAsync(w.counters, 0, 4ull * cnt_words, stream));
+            if (p.max_depth > 0) {
+                if (prof) mark();
+                g.chunk = path_chunk(g.P, I.num_cu);
+                if (variant == EXT_MEGA) {
+                    launch_paths(I.num_cu, stream, ds.view, g, cam, w, counter(w, 0, 0, 0));
+                    kid = KernelId{kFeatSpheres, 0, 3};
+                } else {
+                    kid = launch_paths_g(ds.features, ds.tex_basic, ds.tex_bary, ds.codes16, ds.leaf_shift, I.num_cu, stream, ds.view, g, cam, w,
+                                         counter(w, 0, 0, 0));
+                }
+                if (prof) { mark(); mark(); }
+                ++ext_launches;
+            }
+            ++passes_run;
+            hipLaunchKernelGGL(k_adapt_accum, dim3((caps[level] + 255) / 256), dim3(256), 0, stream, lists[level],
+                               reinterpret_cast<const ResRec<double>*>(w.res), k, p.spp, ad_work);
+            if (level == 3) break;
+            const uint32_t per = level == 0 ? 1u : (level == 1 ? 4u : 16u);
+            hipLaunchKernelGGL(k_adapt_level, dim3((nsq * per + 255) / 256), dim3(256), 0, stream, level, ad_work, p.width, sqx, nsq, ad_f0,
+                               ad_f1, ad_f2, lists[level + 1], lists[level + 1] - 1);
+        }
+        const uint32_t npix = static_cast<uint32_t>(local_pix);
+        hipLaunchKernelGGL(k_adapt_fill, dim3((npix + 255) / 256), dim3(256), 0, stream, ad_work, drgb, p.width, nrows, sqx, ad_f0, ad_f1, ad_f2);
+        for (int L = 0; L < 4; ++L) HIP_OK(hipMemcpyAsync(&ad_counts[L], lists[L] - 1, 4, hipMemcpyDeviceToHost, stream));
+        dev_counted = true;
     } else {
         // engine.h:151-333: levels 0..3 (k_adapt_* above); the list sizes come back to the host between levels
+        // (multi-pass levels, the wavefront variants)
         const int sqx = p.width / kBig;
         const uint32_t nsq = static_cast<uint32_t>(sqx) * static_cast<uint32_t>(nrows / kBig);
         HIP_OK(hipMemsetAsync(ad_work, 0xFF, sizeof(int32_t) * 3 * local_pix, stream));  // the reference's -1 frame
@@ -2650,6 +2764,7 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     unsigned long long segs = 0;
     HIP_OK(hipMemcpyAsync(&segs, w.segments, sizeof segs, hipMemcpyDeviceToHost, stream));
     HIP_OK(hipStreamSynchronize(stream));
+    if (dev_counted) traced = static_cast<uint64_t>(ad_counts[0]) + ad_counts[1] + ad_counts[2] + ad_counts[3];
     float ms = 0;
     HIP_OK(hipEventElapsedTime(&ms, I.ev[0], I.ev[1]));
     stats.ms = ms;
