@@ -250,10 +250,10 @@ def test_segments_match_reference_rate(gpu):
     assert abs(r_gpu - r_ref) / r_ref < 0.01, (r_gpu, r_ref)
 
 
-def gpu_render_adaptive(scene, W, H, spp, band=None, seed=0):
+def gpu_render_adaptive(scene, W, H, spp, band=None, seed=0, **kw):
     world = art.scene_manager().build(scene)
     cam = art.camera(world.lookfrom, world.lookat, (0, 1, 0), world.vfov, W / H, world.aperture, 10.0, 0.0, 1.0)
-    eng = art.engine(cam, art.engine_mode.adaptive, width=W, height=H, samples_per_pixel=spp, seed=seed)
+    eng = art.engine(cam, art.engine_mode.adaptive, width=W, height=H, samples_per_pixel=spp, seed=seed, **kw)
     eng.set_scene(world.objects, world.background)
     band_rows, band_count, band_index = band or (None, 1, 0)
     rows = H if band is None else len(eng.local_rows(band_rows, band_count, band_index))
@@ -262,7 +262,7 @@ def gpu_render_adaptive(scene, W, H, spp, band=None, seed=0):
     return img, eng
 
 
-@pytest.mark.parametrize("scene", ["c1", "1", "8", "cow", "7", "3"])
+@pytest.mark.parametrize("scene", ["c1", "1", "8", "cow", "7", "3", "9"])
 def test_adaptive_matches_oracle_pcg(gpu, scene):
     """engine_mode::adaptive (engine.h:96-333) on the GPU vs the oracle's restatement on the same streams: bit-exact
     frame and the exact segment count (every distinct pixel traced once)."""
@@ -274,6 +274,19 @@ def test_adaptive_matches_oracle_pcg(gpu, scene):
     print(f"adaptive {scene}: rmse {rmse:.4f} max {dmax} segs {eng.stats['segments']} vs {o['segments']}")
     assert np.array_equal(img, o["rgb"])
     assert eng.stats["segments"] == o["segments"]
+
+
+def test_adaptive_launch_forms_agree(gpu):
+    """The capsule (the reference's default run) in adaptive mode two ways -- device-counted levels (one pass per level,
+    entry-major slots, no host round trip) and host-counted levels (samples_per_pass < spp: sample-major slots, the
+    list sizes read back between levels) -- gives one frame and one segment count."""
+    W, H, spp = 120, 96, 6
+    lv, e1 = gpu_render_adaptive("9", W, H, spp)
+    mp, e2 = gpu_render_adaptive("9", W, H, spp, samples_per_pass=2)
+    assert e1.stats["passes"] == 4 and e2.stats["passes"] >= 4
+    assert np.array_equal(lv, mp)
+    assert e1.stats["segments"] == e2.stats["segments"]
+    assert e1.stats["primary"] == e2.stats["primary"]
 
 
 def test_adaptive_band_partition_is_bit_identical(gpu):
