@@ -8,7 +8,8 @@
 #   ab:LIB1,LIB2[:ARGS]         tools/ab_quick.sh over in-tree libart builds (bench.py ARGS, default --spp 256)
 #   abenv:ARGS:V1+V2+...        tools/ab_env.sh over LIB[@VAR=VAL,...] variants (bench.py ARGS)
 #   abopt:ARGS:V1+V2+...        tools/ab_opts.sh over option variants of the current build ("base" or NAME=VALUE,...)
-#   pmc:TAG:SCENE[:SPP]         tools/pmc.sh counter passes + kernel trace of the current libart (ART_LIB honoured)
+#   pmc:TAG:SCENE[:SPP[:OPTS]]  tools/pmc.sh counter passes + kernel trace of the current libart (ART_LIB honoured);
+#                               OPTS: library options NAME=V,NAME=V (bench.py --option)
 #   bench:TAG[:ARGS]            bench.py line -> gpurun_out/bench_TAG.log
 #   prof:TAG[:ARGS]             rocprofv3 --kernel-trace --stats of a bench run -> gpurun_out/prof_TAG
 #   configs:TAG                 tools/configs.sh (one bench line per BASELINE GPU config, plus the capsule)
@@ -52,8 +53,10 @@ for step in "$@"; do
     abopt)
       ARGS="$a" bash tools/ab_opts.sh ${b//+/ } || exit 1 ;;
     pmc)
-      spp=${c:-64}
-      PMC_GROUPS="$PMC_ALL" TAG=$a SCENE=$b SPP=$spp bash tools/pmc.sh || exit 1
+      IFS=':' read -r _k _a _b _c opts <<< "$step"
+      spp=${c:-64}; spp=${spp%%:*}
+      extra=""; for o in ${opts//,/ }; do extra="$extra --option $o"; done
+      PMC_GROUPS="$PMC_ALL" TAG=$a SCENE=$b SPP=$spp BENCH_EXTRA="$extra" bash tools/pmc.sh || exit 1
       SEGS=$(grep -o '"segments_per_step": [0-9]*' gpurun_out/pmc_${a}_trace.log | grep -o '[0-9]*$')
       VAR=4; [ "$b" = "1" ] && VAR=3
       python tools/pmc_summary.py $a $b f64 $SEGS $VAR > gpurun_out/pmc_summary_$a.txt || exit 1

@@ -1,10 +1,10 @@
 #!/bin/bash
 # PMC passes over a short bench run (one counter group per rocprofv3 invocation; no tracing domains combined with
-# --pmc).  Usage (on the GPU box): TAG=r1 SPP=64 bash tools/pmc.sh
+# --pmc).  Usage (on the GPU box): TAG=r1 SPP=64 [BENCH_EXTRA='--option NAME=V'] bash tools/pmc.sh
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
 export TMPDIR=/tmp
 TAG=${TAG:-r1}; SPP=${SPP:-64}; SCENE=${SCENE:-1}; PREC=${PREC:-f64}
-ARGS="--steps 1 --warmup 0 --no-cpu-baseline --no-parity --no-profile --spp $SPP --scene $SCENE --precision $PREC"
+ARGS="--steps 1 --warmup 0 --no-cpu-baseline --no-parity --no-profile --spp $SPP --scene $SCENE --precision $PREC $BENCH_EXTRA"
 run() { local t=$1; shift; timeout -k 10 "$t" "$@"; local rc=$?; echo "== rc=$rc : $*"; if [ $rc -ne 0 ]; then exit $rc; fi; }
 mkdir -p gpurun_out
 rocprofv3 -L > gpurun_out/pmc_list_$TAG.txt 2>&1 || true
