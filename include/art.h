@@ -151,9 +151,12 @@ int rt_device_count(void);
  *   bvh.collapse_ci (0.6), bvh.dp_binary_leaf (1), bvh.sah_ci (1.5), bvh.sah_leaf (4), bvh.sbvh (1.5), bvh.sbvh_alpha
  *   (1e-5): scene compilation, for scenes built after the call (builder experiments; the defaults are what was measured
  *   best);
- *   render.codes16 (1; 0 = always the 32-bit-child-code kernels), render.lds_nodes_max (diagnostic cap on LDS nodes):
- *   uploads and renders after the call;
- *   multi.timeout_ms (the RCCL deadline), multi.rccl_blocking (0; 1 = blocking communicators, diagnosis);
+ *   render.codes16 (1; 0 = always the 32-bit-child-code kernels), render.leaf2 (1; 0 = no pair-aligned leaves: a mesh
+ *   of more than 8192 references takes the 32-bit-code kernels), render.tex_bary (1; 0 = meshes whose only images are
+ *   barycentric take the all-textures kernels), render.lds_nodes_max (diagnostic cap on LDS nodes): uploads and
+ *   renders after the call (kernel-selection switches for A/B; images are identical either way);
+ *   multi.timeout_ms (the RCCL deadline; inf = none), multi.rccl_blocking (0; 1 = blocking communicators, diagnosis:
+ *   gives up the deadline and the error-path protection);
  *   test.fault_workspace_bytes (0 = off; N refuses workspace growth beyond N bytes), test.fault_gather_abort (0; 1 = the
  *   next gather fails in flight), test.fault_rccl_group (0; 1 / 2 = an error inside rt_multi_create's / the gather's
  *   RCCL group): fault points for the tests, each failing a later call exactly as the real fault would. */

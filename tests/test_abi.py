@@ -54,7 +54,7 @@ def test_struct_layouts_match_the_header(tmp_path):
 OPTIONS = {  # include/art.h rt_option_set: name -> default
     "compile.world_merge": 2, "compile.hoist": 1, "bvh.collapse": 0, "bvh.collapse_ci": 0.6, "bvh.dp_binary_leaf": 1,
     "bvh.sah_ci": 1.5, "bvh.sah_leaf": 4, "bvh.sbvh": 1.5, "bvh.sbvh_alpha": 1e-5, "render.codes16": 1,
-    "render.lds_nodes_max": 4294967295, "multi.rccl_blocking": 0, "test.fault_workspace_bytes": 0,
+    "render.lds_nodes_max": 4294967295, "render.leaf2": 1, "render.tex_bary": 1, "multi.rccl_blocking": 0, "test.fault_workspace_bytes": 0,
     "test.fault_gather_abort": 0, "test.fault_rccl_group": 0,
 }
 
@@ -71,6 +71,16 @@ def test_options_defaults_set_get_and_reset():
     art.set_option(None, 0)  # NULL name: every option back to its default
     assert art.get_option("compile.world_merge") == 2 and art.get_option("test.fault_workspace_bytes") == 0
     assert art.get_option("multi.timeout_ms") == 120000  # unset: ART_MULTI_TIMEOUT_MS (not set here) or 120 s
+
+
+def test_infinite_multi_timeout_is_accepted():
+    # "no deadline" (ADVICE r5): inf is inside the option's range; multi.hip turns it (or anything whose nanoseconds
+    # overflow the clock) into no deadline instead of an undefined duration_cast (tests/test_gpu_api.py renders with it)
+    art.set_option("multi.timeout_ms", float("inf"))
+    try:
+        assert art.get_option("multi.timeout_ms") == float("inf")
+    finally:
+        art.set_option(None, 0)
 
 
 @pytest.mark.parametrize("name,value", [("no.such.option", 1), ("compile.world_merge", 3), ("compile.hoist", 0.5),

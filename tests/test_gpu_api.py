@@ -231,6 +231,17 @@ def test_render_multi_phase_times(gpu):
     assert m.times()["collectives"] == 2
 
 
+@pytest.mark.parametrize("timeout_ms", [float("inf"), 1e300])
+def test_render_multi_without_deadline(gpu, options, timeout_ms):
+    # multi.timeout_ms = inf (or beyond the clock's range) is no deadline: creation and the gather complete instead of
+    # aborting at a deadline in the past (r5's duration_cast of inf gave INT64_MIN)
+    art.set_option("multi.timeout_ms", timeout_ms)
+    m = _multi()
+    img = torch.zeros((40, 64, 3), dtype=torch.uint8, device="cuda:0")
+    m.run(img)
+    assert m.times()["collectives"] == 1 and int(img.sum()) > 0
+
+
 def test_render_multi_failed_render_starts_no_collective(gpu, options):
     # a device whose render fails (fault injection: its workspace growth is refused) ends rt_render_multi with RT_E_DEVICE
     # before the gather -- no collective starts -- and the multi renders correctly afterwards
