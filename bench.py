@@ -124,7 +124,8 @@ def cpu_baseline(args, repeats=9):
         return None
     threads = 4
     runs, last = [], None
-    for _ in range(repeats):
+    # one discarded warm-up run first: r6e's first runs came out ~6 % below the rest (clock ramp of the host cores)
+    for i in range(repeats + 1):
         # PIN 1: the harness pins its worker t to the t-th CPU of this job's affinity set (sched_setaffinity: no
         # migrations between the host's shared cores, the run-to-run spread of r4/r5 was +-15 %)
         out = subprocess.run([harness, "render", args.scene, str(args.width), str(args.height), str(args.cpu_baseline_spp),
@@ -132,7 +133,8 @@ def cpu_baseline(args, repeats=9):
         if out.returncode != 0:
             return {"error": out.stderr.strip()[-300:]}
         last = json.loads(out.stdout.strip().splitlines()[-1])
-        runs.append(last["mseg_per_s"])
+        if i > 0:
+            runs.append(last["mseg_per_s"])
     model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -141,8 +143,8 @@ def cpu_baseline(args, repeats=9):
         pass
     res = {"value": round(_median(runs), 4), "unit": "Msamples/s", "cores": threads, "kind": "reference",
            "sample": f"scene {args.scene} {args.width}x{args.height}x{args.cpu_baseline_spp}spp "
-                     f"({last['segments']} segments, {last['ms'] / 1e3:.1f} s per run), median of {repeats} runs, "
-                     f"engine_mode::parallel_stripes semantics (4 threads pinned to 4 CPUs, shared global mt19937); "
+                     f"({last['segments']} segments, {last['ms'] / 1e3:.1f} s per run), median of {repeats} runs after a discarded "
+                     f"warm-up run, engine_mode::parallel_stripes semantics (4 threads pinned to 4 CPUs, shared global mt19937); "
                      f"per-segment cost is spp-independent",
            "runs_Msamples_s": [round(x, 4) for x in runs], "spread_Msamples_s": [round(min(runs), 4), round(max(runs), 4)],
            "max_Msamples_s": round(max(runs), 4), "spread_frac": round((max(runs) - min(runs)) / _median(runs), 4),

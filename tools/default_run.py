@@ -61,13 +61,15 @@ def main():
     if a.cpu_runs > 0 and os.path.exists(harness):
         import subprocess
         runs = []
-        for _ in range(a.cpu_runs):
+        for i in range(a.cpu_runs + 1):  # the first is a discarded warm-up (host clock ramp)
             out = subprocess.run([harness, "render", a.scene, str(a.width), str(a.height), str(a.spp), "/tmp/default_run_cpu",
                                   "adaptive4", "4", "1"], capture_output=True, text=True, timeout=600)
             if out.returncode != 0:
                 raise SystemExit("ref_harness failed: " + out.stderr.strip()[-400:])
-            runs.append(json.loads(out.stdout.strip().splitlines()[-1]))
-            print(json.dumps(runs[-1]), flush=True)
+            r = json.loads(out.stdout.strip().splitlines()[-1])
+            print(json.dumps(r), flush=True)
+            if i > 0:
+                runs.append(r)
         ms = sorted(r["ms"] for r in runs)
         model = ""
         try:
