@@ -158,7 +158,9 @@ __device__ __forceinline__ void store_res(ResRec<float>* res, uint32_t q, V3<flo
 // against 6.3); temporal stores merge in L2 first, 1.18x (7.4 B), at equal speed -- so k_paths_g, which has no rings,
 // stores temporally.  k_paths keeps NT: its writes are ring lines evicted between laps (27.8 B per segment with NT
 // 24-B records, 27.2 with NT 32-B ones), and temporal records evict more of them (32.9 B written + 6.8 B re-read,
-// -0.25 %).  32-B records cost k_accum a third more reads and lose 0.8-1.2 %.
+// -0.25 %).  32-B records cost k_accum a third more reads and lose 0.8-1.2 %.  r6i: the k_paths_g kernels whose BVH is
+// not all in LDS (LM 0 / 2) store non-temporally after all: there the temporal records evict the L2-resident nodes
+// and leaf triangles (capsule +1.7 %, cow +0.8 %, profiles/r6i_ab_res_nt.txt).
 template <bool NT = true>
 __device__ __forceinline__ void store_res(ResRec<double>* res, uint32_t q, V3<double> L) {
     if constexpr (NT) {
@@ -1103,6 +1105,10 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
         }
         lm_off = align16(lm_off + nb + pb + tb);  // the camera-ray rings follow (kRing)
     }
+    // radiance records: non-temporal where the scene's nodes and leaf records come from L2 (LM 0 / 2: the streaming
+    // records would evict them; r6i: capsule +1.7 %, cow +0.8 %), temporal where they sit in LDS (LM 1: each 8-B NT
+    // store reaches HBM as its own partial write, r5c; Cornell smoke -1.5 % with NT, the final and dino +-0)
+    constexpr bool kResNT = LM != 1;
     constexpr bool kRing = paths_g_ring(F, LM);
     const bool use_ring = kRing && g.lds_ring != 0;  // the launch found room for the rings
     [[maybe_unused]] const RingG ring{reinterpret_cast<double*>(smem + lm_off) + (threadIdx.x / 64u) * (8u * kRingG)};
@@ -1329,7 +1335,7 @@ __global__ __launch_bounds__(LM ? kBlockM : kBlock, LM ? 1 : ART_PATHS_G_WAVES) 
             } else if (cont) {
                 ++depth;
             } else {
-                store_res<false>(w.res, q, st.L);
+                store_res<kResNT>(w.res, q, st.L);
                 busy = false;
             }
         }
