@@ -74,7 +74,7 @@ for step in "$@"; do
       tail -3 gpurun_out/default_run_$a.log ;;
     c5full)
       run 300 python bench.py --scene dino --width 4096 --height 4096 --spp 8192 --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/c5full_$a.log 2>&1
-      tail -1 gpurun_out/c5full_$a.log > gpurun_out/c5full_$a.json; cut -c1-400 gpurun_out/c5full_$a.json ;;
+      grep "^{" gpurun_out/c5full_$a.log | tail -1 > gpurun_out/c5full_$a.json; cut -c1-400 gpurun_out/c5full_$a.json ;;
     stats)
       CFGS="--scene 1 --spp 64|--scene cow --spp 64|--scene 8 --spp 64|--scene dino --width 4096 --height 4096 --spp 16" bash tools/stats_configs.sh \
         > gpurun_out/stats_$a.txt 2>&1 || exit 1
