@@ -30,8 +30,12 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--json", default=None)
     ap.add_argument("--cpu-runs", type=int, default=9, help="reference harness runs on the host CPU (0: none)")
+    ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE", help="rt_option_set before the scene build")
     a = ap.parse_args()
     import another_raytracer_amd as art
+    for o in a.option:
+        name, _, value = o.partition("=")
+        art.set_option(name, float(value))
     w = art.scene_manager().build(a.scene)
     cam = art.camera(w.lookfrom, w.lookat, (0, 1, 0), w.vfov, a.width / a.height, w.aperture, 10.0, 0.0, 1.0)
     rows = []
@@ -55,6 +59,8 @@ def main():
                "engine_ms": round(rep, 3), "segments": st["segments"], "primary": st["primary"],
                "msamples_s": round(st["segments"] / wall / 1e3, 1), "passes": st["passes"], "kernel_ms_profiled": round(prof["extend_ms"], 3), "launches_profiled": prof["extend_launches"],
                "kernel": [st["extend_variant"], st["kernel_features"], st["kernel_textures"], st["kernel_lds_mode"]]}
+        if a.option:
+            row["options"] = {o.partition("=")[0]: float(o.partition("=")[2]) for o in a.option}
         print(json.dumps(row), flush=True)
         rows.append(row)
     harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
