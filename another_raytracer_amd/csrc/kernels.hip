@@ -1552,25 +1552,40 @@ __global__ void k_adapt_store(const uint32_t* list, uint32_t n, const double* ac
 // list_mode 1 (the device-counted levels): the pixel sums of every list entry -- its k samples on consecutive slots,
 // summed in sample order from +0.0 as k_accum sums them into the zeroed accumulator (engine.h:58-68) -- written into
 // the work image as k_adapt_store writes them.  The entry count is list[-1].
-__global__ void k_adapt_accum(const uint32_t* list, const ResRec<double>* res, uint32_t k, int spp, int32_t* work) {
-    const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= list[-1]) return;
-    double acc[3] = {0.0, 0.0, 0.0};
-    for (uint32_t j = 0; j < k; ++j) {
-        double x, y, z;
-        load_res(res, e * k + j, x, y, z);
-        acc[0] += x;
-        acc[1] += y;
-        acc[2] += z;
+// One wave per entry (r6o): the entry's k records are consecutive (entry-major slots), so the wave reads 64 of them
+// per coalesced load into LDS and lanes 0-2 (one per channel) add them in sample order from LDS.  One thread per
+// entry, 100 records each, left every level's accumulation latency-bound at ~62 us whatever its size (rocprofv3
+// kernel trace of the default run; 45 us with 20 loads in flight per thread).
+constexpr int kAdaptAccumWaves = 4;
+__global__ __launch_bounds__(64 * kAdaptAccumWaves) void k_adapt_accum(const uint32_t* list, const ResRec<double>* res, uint32_t k, int spp,
+                                                                      int32_t* work) {
+    __shared__ double buf[kAdaptAccumWaves][3 * 64];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t e = blockIdx.x * kAdaptAccumWaves + wv;
+    if (e >= list[-1]) return;  // wave-uniform
+    double* b = buf[wv];
+    double acc = 0.0;  // lane c < 3: channel c
+    const ResRec<double>* r = res + static_cast<size_t>(e) * k;
+    for (uint32_t j0 = 0; j0 < k; j0 += 64) {
+        const uint32_t n = min(64u, k - j0);
+        if (lane < n) {
+            double x, y, z;
+            load_res(r, j0 + lane, x, y, z);
+            b[3 * lane] = x;
+            b[3 * lane + 1] = y;
+            b[3 * lane + 2] = z;
+        }
+        // one wave: its LDS writes complete before its reads (in-order LDS, the waitcnt), and the compiler keeps them apart
+        __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane < 3)
+            for (uint32_t i = 0; i < n; ++i) acc += b[3 * i + lane];
+        __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the next chunk's writes after these reads
     }
+    if (lane >= 3) return;
     const double scale = 1.0 / spp;
-    int32_t* o = work + 3 * static_cast<size_t>(list[e]);
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        double x = sqrt(scale * acc[c]);
-        x = x < 0.0 ? 0.0 : (x > 0.999 ? 0.999 : x);
-        o[c] = static_cast<int32_t>(256 * x);
-    }
+    double x = sqrt(scale * acc);
+    x = x < 0.0 ? 0.0 : (x > 0.999 ? 0.999 : x);
+    work[3 * static_cast<size_t>(list[e]) + lane] = static_cast<int32_t>(256 * x);
 }
 
 // _compute_corners_heuristic (engine.h:96-136): any squared RGB distance between neighbouring corners > 100.
@@ -2503,7 +2518,8 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
     const size_t o_a0 = off; off += wf * al(4ull * kShards * g.cap);
     const size_t o_a1 = off; off += wf * al(4ull * kShards * g.cap);
     const size_t o_mq = off; off += wf * al(4ull * kMatSegs * g.cap);
-    const size_t cnt_words = static_cast<size_t>(depth_slots) * kQueueKinds * kShards * kCounterStride;
+    // (at least 4 depth lines: the device-counted adaptive levels take one each)
+    const size_t cnt_words = static_cast<size_t>(std::max(depth_slots, 4)) * kQueueKinds * kShards * kCounterStride;
     const size_t o_cnt = off; off += al(4ull * cnt_words);
     const size_t o_seg = off; off += al(sizeof(unsigned long long));
     const size_t o_acc = off; off += al(sizeof(double) * 3 * local_pix);
@@ -2584,7 +2600,8 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
             g.k = std::min<uint32_t>(kk, static_cast<uint32_t>(spp_t) - sb);
             g.P = g.k * g.npix_pad;
             g.live = g.k * npix;
-            HIP_OK(hipMemsetAsync(w.counters, 0, 4ull * cnt_words, stream));
+            // the persistent kernels use one counter (counter(w, 0, 0, 0)): clear its line, not the wavefront queues' 1.25 MB
+            HIP_OK(hipMemsetAsync(w.counters, 0, mega ? 4u * kCounterStride : 4ull * cnt_words, stream));
             bool persistent = false;
             if constexpr (std::is_same<R, double>::value) {
                 if (mega) {
@@ -2672,28 +2689,30 @@ static void render_impl(Renderer::Impl& I, DeviceScene<R>& ds, const CameraRec<d
         g.npix_pad = k;
         g.fd_npix = FastDiv::make(k);
         g.sample_base = 0;
+        // one slot counter line per level (counter(w, level, 0, 0): the wavefront variants' depth lines, unused here),
+        // cleared together before level 0 instead of one fill launch per level
+        HIP_OK(hipMemsetAsync(w.counters, 0, 4ull * kQueueKinds * kShards * kCounterStride * 4, stream));
         for (int level = 0; level < 4; ++level) {
             g.list = lists[level];
             g.nlist = caps[level];                      // upper bounds: the kernels read the count
             g.P = static_cast<uint32_t>(std::min<uint64_t>(static_cast<uint64_t>(caps[level]) * k, kMaxPassSlots));
             g.live = g.P;
             if (static_cast<uint64_t>(caps[level]) * k > Pmax) throw std::runtime_error("internal: adaptive level larger than the pass workspace");
-            HIP_OK(hipMemsetAsync(w.counters, 0, 4ull * cnt_words, stream));
             if (p.max_depth > 0) {
                 if (prof) mark();
                 g.chunk = path_chunk(g.P, I.num_cu);
                 if (variant == EXT_MEGA) {
-                    launch_paths(I.num_cu, stream, ds.view, g, cam, w, counter(w, 0, 0, 0));
+                    launch_paths(I.num_cu, stream, ds.view, g, cam, w, counter(w, level, 0, 0));
                     kid = KernelId{kFeatSpheres, 0, 3};
                 } else {
                     kid = launch_paths_g(ds.features, ds.tex_basic, ds.tex_bary, ds.codes16, ds.leaf_shift, I.num_cu, stream, ds.view, g, cam, w,
-                                         counter(w, 0, 0, 0));
+                                         counter(w, level, 0, 0));
                 }
                 if (prof) { mark(); mark(); }
                 ++ext_launches;
             }
             ++passes_run;
-            hipLaunchKernelGGL(k_adapt_accum, dim3((caps[level] + 255) / 256), dim3(256), 0, stream, lists[level],
+            hipLaunchKernelGGL(k_adapt_accum, dim3((caps[level] + kAdaptAccumWaves - 1) / kAdaptAccumWaves), dim3(64 * kAdaptAccumWaves), 0, stream, lists[level],
                                reinterpret_cast<const ResRec<double>*>(w.res), k, p.spp, ad_work);
             if (level == 3) break;
             const uint32_t per = level == 0 ? 1u : (level == 1 ? 4u : 16u);
